@@ -1,0 +1,799 @@
+// narde.hip -- HIP kernels (gfx950) + the C ABI of libnarde (include/narde.h).
+//
+// One lane = one env.  Each env is a 32-byte record split into two planar
+// 16-byte planes (narde_rules.h), so every wave-wide load/store of state is
+// a single contiguous 1 KiB transaction.  The rules engine is branch-light
+// bitmask arithmetic on 24-bit point masks held in VGPRs; nothing is staged
+// through LDS because no data is shared between lanes (envs are independent).
+//
+// Kernels
+//   k_step      NardeEnv.step for B envs (API step and the self-play ply):
+//               Philox dice, list #1, policy or given actions, apply, list #2,
+//               apply, end check, flip, TimeLimit, auto-reset, outputs.
+//   k_selfplay  the same step looped over K plies with the record in VGPRs.
+//   k_legal     Narde.get_valid_moves with 1..4 dice, expanded or compact.
+//   k_reset / k_set_state / k_get_state / k_apply / k_observe / k_mask576 /
+//   k_block / k_peek_dice   state management and the rest of the ABI.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+
+#include "../../include/narde.h"
+#include "narde_rules.h"
+
+using namespace narde;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int64_t kHostCap = 4096;
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof g_err, fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess) return fail(NARDE_EHIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+struct Planes {
+  uint4* p0;
+  uint4* p1;
+  int4* stats;
+};
+
+struct Rng {
+  uint32_t env0, k0, k1;
+  int dice_mode;
+};
+
+__device__ __forceinline__ void draw(const Rng& g, uint32_t t, uint32_t i, uint32_t stream,
+                                     uint32_t r[4]) {
+  philox4x32_10(t, g.env0 + i, 0u, stream, g.k0, g.k1, r);
+}
+
+// ------------------------------------------------------------------ kernels
+__global__ void __launch_bounds__(kBlock) k_reset(Planes pl, int n, Rng g, uint32_t epoch,
+                                                  const uint8_t* __restrict__ mask) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  if (mask && !mask[i]) return;
+  uint32_t r[4];
+  draw(g, epoch, (uint32_t)i, 1u, r);
+  Side s = side_reset(r[0]);
+  uint4 a, b;
+  side_to_record(s, a, b);
+  pl.p0[i] = a;
+  pl.p1[i] = b;
+  pl.stats[i] = make_int4(0, 0, 0, 0);
+}
+
+__global__ void __launch_bounds__(kBlock) k_set_state(Planes pl, int n, const int8_t* __restrict__ board,
+                                                      const uint8_t* __restrict__ off,
+                                                      const uint8_t* __restrict__ ft,
+                                                      const int8_t* __restrict__ player,
+                                                      const uint16_t* __restrict__ elapsed) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  uint4 a, b;
+  record_from_board(board + (size_t)i * 24, off[2 * i], off[2 * i + 1], ft[2 * i], ft[2 * i + 1],
+                    player[i], elapsed ? elapsed[i] : 0u, a, b);
+  pl.p0[i] = a;
+  pl.p1[i] = b;
+}
+
+__global__ void __launch_bounds__(kBlock) k_get_state(Planes pl, int n, int8_t* __restrict__ board,
+                                                      uint8_t* __restrict__ off, uint8_t* __restrict__ ft,
+                                                      int8_t* __restrict__ player,
+                                                      uint16_t* __restrict__ elapsed) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  board_from_record(pl.p0[i], pl.p1[i], board ? board + (size_t)i * 24 : nullptr,
+                    off ? off + 2 * i : nullptr, ft ? ft + 2 * i : nullptr,
+                    player ? player + i : nullptr, elapsed ? elapsed + i : nullptr);
+}
+
+__global__ void __launch_bounds__(kBlock) k_peek_dice(int n, Rng g, uint32_t t, uint8_t* __restrict__ dice) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  uint32_t r[4];
+  draw(g, t, (uint32_t)i, 0u, r);
+  int d0, d1;
+  dice_from(r[0], g.dice_mode, d0, d1);
+  dice[2 * i] = (uint8_t)d0;
+  dice[2 * i + 1] = (uint8_t)d1;
+}
+
+__device__ __forceinline__ uint64_t compact_legal(const Legal& l) {
+  return (uint64_t)l.L[0] | ((uint64_t)l.L[1] << 24) | ((uint64_t)l.d[0] << 48) |
+         ((uint64_t)l.d[1] << 52);
+}
+
+__global__ void __launch_bounds__(kBlock) k_legal(Planes pl, int n, Rng g, uint32_t t,
+                                                  const uint8_t* __restrict__ dice4,
+                                                  int16_t* __restrict__ out_count,
+                                                  int8_t* __restrict__ out_moves,
+                                                  uint64_t* __restrict__ out_compact) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const Side s = side_from_record(pl.p0[i], pl.p1[i]);
+  Legal l;
+  if (dice4) {
+    legal_roll(s, dice4 + 4 * i, l);
+  } else {
+    uint32_t r[4];
+    draw(g, t, (uint32_t)i, 0u, r);
+    int d0, d1;
+    dice_from(r[0], g.dice_mode, d0, d1);
+    legal2(s, d0, d1, l);
+  }
+  const int nd = l.n;
+  out_count[i] = (int16_t)l.count;
+  if (out_compact) out_compact[i] = nd <= 2 ? compact_legal(l) : 0ull;
+  if (out_moves) {
+    int4* row = reinterpret_cast<int4*>(out_moves + (size_t)i * NARDE_MAX_MOVES * 2);
+    const int4 neg = make_int4(-1, -1, -1, -1);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) row[q] = neg;
+    int e = 0;
+    uint16_t* pairs = reinterpret_cast<uint16_t*>(out_moves + (size_t)i * NARDE_MAX_MOVES * 2);
+    for (int k = 0; k < nd; ++k) {
+      uint32_t m = l.L[k];
+      while (m) {
+        const int f = __builtin_ctz(m);
+        m &= m - 1u;
+        const int to = f - l.d[k] < 0 ? OFF : f - l.d[k];
+        pairs[e++] = (uint16_t)((uint32_t)f | ((uint32_t)to << 8));
+      }
+    }
+  }
+}
+
+struct StepArgs {
+  Planes pl;
+  int n;
+  Rng g;
+  uint32_t t;
+  int max_steps;
+  int autoreset;
+  const int16_t* __restrict__ actions;
+  const uint8_t* __restrict__ dice;
+  int32_t* __restrict__ obs;
+  int32_t* __restrict__ reward;
+  uint8_t* __restrict__ term;
+  uint8_t* __restrict__ trunc;
+  uint64_t* __restrict__ legal;
+  int16_t* __restrict__ act_out;
+};
+
+__device__ __forceinline__ void store_obs(int32_t* __restrict__ obs, int i, const Side& s) {
+  int4* o = reinterpret_cast<int4*>(obs + (size_t)i * 24);
+#pragma unroll
+  for (int q = 0; q < 6; ++q)
+    o[q] = make_int4(obs_point(s, 4 * q), obs_point(s, 4 * q + 1), obs_point(s, 4 * q + 2),
+                     obs_point(s, 4 * q + 3));
+}
+
+// one ply for env i: draw, then the shared host/device ply (narde_rules.h)
+__device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t t, uint32_t i,
+                                    const int16_t* actions, const uint8_t* dice, int max_steps,
+                                    bool autoreset, StepOut& o, int& term, int& trunc) {
+  uint32_t r[4];
+  draw(g, t, i, 0u, r);
+  int d0 = 0, d1 = 0, c1 = 0, c2 = 0;
+  if (dice) { d0 = dice[2 * i]; d1 = dice[2 * i + 1]; }
+  if (actions) { c1 = actions[2 * i]; c2 = actions[2 * i + 1]; }
+  env_ply(s, st, r, dice != nullptr, d0, d1, g.dice_mode, actions == nullptr, c1, c2, max_steps,
+          autoreset, o, term, trunc);
+}
+
+__global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= a.n) return;
+  Side s = side_from_record(a.pl.p0[i], a.pl.p1[i]);
+  int4 st = make_int4(0, 0, 0, 0);
+  StepOut o;
+  int term, trunc;
+  ply(s, st, a.g, a.t, (uint32_t)i, a.actions, a.dice, a.max_steps, a.autoreset != 0, o, term,
+      trunc);
+  uint4 ra, rb;
+  side_to_record(s, ra, rb);
+  a.pl.p0[i] = ra;
+  a.pl.p1[i] = rb;
+  if (st.x) {
+    int4 cur = a.pl.stats[i];
+    cur.x += st.x; cur.y += st.y; cur.z += st.z;
+    a.pl.stats[i] = cur;
+  }
+  if (a.obs) store_obs(a.obs, i, s);
+  if (a.reward) a.reward[i] = o.reward;
+  if (a.term) a.term[i] = (uint8_t)term;
+  if (a.trunc) a.trunc[i] = (uint8_t)trunc;
+  if (a.legal) a.legal[i] = compact_legal(o.l1);
+  if (a.act_out) {
+    a.act_out[2 * i] = (int16_t)o.code1;
+    a.act_out[2 * i + 1] = (int16_t)o.code2;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_selfplay(Planes pl, int n, Rng g, uint32_t t0, int plies,
+                                                     int max_steps) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  Side s = side_from_record(pl.p0[i], pl.p1[i]);
+  int4 st = make_int4(0, 0, 0, 0);
+  for (int p = 0; p < plies; ++p) {
+    StepOut o;
+    int term, trunc;
+    ply(s, st, g, t0 + (uint32_t)p, (uint32_t)i, nullptr, nullptr, max_steps, true, o, term,
+        trunc);
+  }
+  uint4 ra, rb;
+  side_to_record(s, ra, rb);
+  pl.p0[i] = ra;
+  pl.p1[i] = rb;
+  if (st.x) {
+    int4 cur = pl.stats[i];
+    cur.x += st.x; cur.y += st.y; cur.z += st.z;
+    pl.stats[i] = cur;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_get_stats(Planes pl, int n, int32_t* __restrict__ out) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int4 s = pl.stats[i];
+  out[3 * i] = s.x; out[3 * i + 1] = s.y; out[3 * i + 2] = s.z;
+}
+
+__global__ void __launch_bounds__(kBlock) k_apply(Planes pl, int n, const int8_t* __restrict__ moves,
+                                                  const int8_t* __restrict__ player) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int f = moves[2 * i], t = moves[2 * i + 1];
+  if (f < 0 || f > 23 || t < 0 || t > OFF) return;
+  Side s = side_from_record(pl.p0[i], pl.p1[i]);
+  const uint32_t want_black = player ? (player[i] == -1 ? 1u : 0u) : s.black;
+  const bool flip = want_black != s.black;
+  if (flip) side_flip(s);
+  apply_move(s, f, t);
+  if (flip) side_flip(s);
+  uint4 a, b;
+  side_to_record(s, a, b);
+  pl.p0[i] = a;
+  pl.p1[i] = b;
+}
+
+__global__ void __launch_bounds__(kBlock) k_observe(Planes pl, int n, int32_t* __restrict__ obs,
+                                                    float* __restrict__ tes) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint4 a = pl.p0[i], b = pl.p1[i];
+  if (obs) {
+    const Side s = side_from_record(a, b);
+    store_obs(obs, i, s);
+  }
+  if (tes) {
+    // README.md:42-102 layout, absolute points: [white 24x4, bar, off,
+    // black 24x4, bar, off, player one-hot]
+    const Nib w{(uint64_t)a.x | ((uint64_t)a.y << 32), b.x};
+    const Nib k{(uint64_t)a.z | ((uint64_t)a.w << 32), b.y};
+    float2* o = reinterpret_cast<float2*>(tes + (size_t)i * 198);
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const Nib& c = side == 0 ? w : k;
+#pragma unroll
+      for (int p = 0; p < 24; ++p) {
+        const uint32_t v = nib_get(c, p);
+        const int base = side * 49 + p * 2;  // in float2 units
+        o[base] = make_float2(v >= 1u ? 1.0f : 0.0f, v >= 2u ? 1.0f : 0.0f);
+        o[base + 1] = make_float2(v >= 3u ? 1.0f : 0.0f, v >= 3u ? (float)(v - 3u) / 2.0f : 0.0f);
+      }
+      const uint32_t offc = side == 0 ? (b.z & 15u) : ((b.z >> 4) & 15u);
+      o[side * 49 + 48] = make_float2(0.0f, (float)offc / 15.0f);
+    }
+    const bool black = (b.z >> 10) & 1u;
+    o[98] = make_float2(black ? 0.0f : 1.0f, black ? 1.0f : 0.0f);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_mask576(Planes pl, int n, Rng g, uint32_t t,
+                                                    uint64_t* __restrict__ mask) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const Side s = side_from_record(pl.p0[i], pl.p1[i]);
+  uint32_t r[4];
+  draw(g, t, (uint32_t)i, 0u, r);
+  int d0, d1;
+  dice_from(r[0], g.dice_mode, d0, d1);
+  Legal l;
+  legal2(s, d0, d1, l);
+  uint64_t m[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int k = 0; k < l.n; ++k) {
+    uint32_t b = l.L[k];
+    while (b) {
+      const int f = __builtin_ctz(b);
+      b &= b - 1u;
+      const int to = f - l.d[k] < 0 ? OFF : f - l.d[k];
+      if (to == 0 && f <= 5) continue;  // (f, 0) cannot be requested by a code
+      const int c = encode_move(f, to);
+      m[c >> 6] |= 1ull << (c & 63);
+    }
+  }
+  for (int q = 0; q < 9; ++q) mask[(size_t)i * 9 + q] = m[q];
+}
+
+__global__ void __launch_bounds__(kBlock) k_block(const int8_t* __restrict__ boards, int n,
+                                                  uint8_t* __restrict__ out) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  uint32_t O = 0, P = 0;
+  for (int p = 0; p < 24; ++p) {
+    const int v = boards[i * 24 + p];
+    O |= (v > 0 ? 1u : 0u) << p;
+    P |= (v < 0 ? 1u : 0u) << p;
+  }
+  out[i] = (runs6(O) & block_lowmask(P)) ? 1 : 0;
+}
+
+inline int grid(int64_t n) { return (int)((n + kBlock - 1) / kBlock); }
+
+}  // namespace
+
+// ---------------------------------------------------------------- handle
+struct narde_env {
+  int device;
+  int64_t n;
+  int64_t env0;
+  uint64_t seed;
+  int dice_mode;
+  int max_steps;
+  uint32_t t;
+  uint32_t epoch;
+  Planes pl;
+  // host-call staging (scalar facade)
+  Planes hpl;
+  uint8_t* h_in;   // pinned
+  uint8_t* h_out;  // pinned
+  uint8_t* d_in;
+  uint8_t* d_out;
+  hipStream_t hstream;
+  size_t stage_bytes;
+};
+
+namespace {
+
+Rng rng_of(const narde_env* e) {
+  Rng g;
+  g.env0 = (uint32_t)e->env0;
+  g.k0 = (uint32_t)e->seed;
+  g.k1 = (uint32_t)(e->seed >> 32);
+  g.dice_mode = e->dice_mode;
+  return g;
+}
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != d) (void)hipSetDevice(d);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(NARDE_EHIP, "%s launch: %s", what, hipGetErrorString(e));
+  return NARDE_OK;
+}
+
+bool valid_position(const int8_t* board, const uint8_t* off, const uint8_t* ft, const int8_t* player,
+                    int64_t i) {
+  int w = 0, b = 0;
+  for (int p = 0; p < 24; ++p) {
+    const int v = board[i * 24 + p];
+    if (v > 15 || v < -15) return false;
+    if (v > 0) w += v; else b -= v;
+  }
+  if (off[2 * i] > 15 || off[2 * i + 1] > 15) return false;
+  if (w + off[2 * i] > 15 || b + off[2 * i + 1] > 15) return false;
+  if (player && player[i] != 1 && player[i] != -1) return false;
+  (void)ft;
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int narde_version(void) { return 1; }
+const char* narde_last_error(void) { return g_err; }
+
+int narde_create(int device, int64_t num_envs, int64_t env_id_offset, uint64_t seed, int dice_mode,
+                 int max_episode_steps, narde_env** out) {
+  if (!out) return fail(NARDE_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (num_envs <= 0 || num_envs > (int64_t(1) << 31) - kBlock)
+    return fail(NARDE_EINVAL, "num_envs %lld out of range", (long long)num_envs);
+  if (env_id_offset < 0 || env_id_offset + num_envs > (int64_t(1) << 32))
+    return fail(NARDE_EINVAL, "global env ids must fit in 32 bits");
+  if (dice_mode != NARDE_DICE_ALL36 && dice_mode != NARDE_DICE_NODOUBLES)
+    return fail(NARDE_EINVAL, "bad dice_mode %d", dice_mode);
+  if (max_episode_steps < 0 || max_episode_steps > 65535)
+    return fail(NARDE_EINVAL, "max_episode_steps must be in [0, 65535]");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(NARDE_EINVAL, "device %d of %d", device, ndev);
+  DeviceGuard dg(device);
+  narde_env* e = new (std::nothrow) narde_env();
+  if (!e) return fail(NARDE_ENOMEM, "host alloc");
+  e->device = device;
+  e->n = num_envs;
+  e->env0 = env_id_offset;
+  e->seed = seed;
+  e->dice_mode = dice_mode;
+  e->max_steps = max_episode_steps;
+  e->stage_bytes = (size_t)kHostCap * 512;
+  hipError_t err = hipSuccess;
+  err = hipMalloc(&e->pl.p0, num_envs * sizeof(uint4));
+  if (err == hipSuccess) err = hipMalloc(&e->pl.p1, num_envs * sizeof(uint4));
+  if (err == hipSuccess) err = hipMalloc(&e->pl.stats, num_envs * sizeof(int4));
+  if (err == hipSuccess) err = hipMalloc(&e->hpl.p0, kHostCap * sizeof(uint4));
+  if (err == hipSuccess) err = hipMalloc(&e->hpl.p1, kHostCap * sizeof(uint4));
+  if (err == hipSuccess) err = hipMalloc(&e->hpl.stats, kHostCap * sizeof(int4));
+  if (err == hipSuccess) err = hipMalloc(&e->d_in, e->stage_bytes);
+  if (err == hipSuccess) err = hipMalloc(&e->d_out, e->stage_bytes);
+  if (err == hipSuccess) err = hipHostMalloc(&e->h_in, e->stage_bytes, hipHostMallocDefault);
+  if (err == hipSuccess) err = hipHostMalloc(&e->h_out, e->stage_bytes, hipHostMallocDefault);
+  if (err == hipSuccess) err = hipStreamCreateWithFlags(&e->hstream, hipStreamNonBlocking);
+  if (err != hipSuccess) {
+    narde_destroy(e);
+    return fail(NARDE_ENOMEM, "device alloc for %lld envs: %s", (long long)num_envs,
+                hipGetErrorString(err));
+  }
+  k_reset<<<grid(num_envs), kBlock, 0, e->hstream>>>(e->pl, (int)num_envs, rng_of(e), 0u, nullptr);
+  int rc = check_launch("k_reset");
+  if (rc == NARDE_OK) {
+    err = hipStreamSynchronize(e->hstream);
+    if (err != hipSuccess) rc = fail(NARDE_EHIP, "reset sync: %s", hipGetErrorString(err));
+  }
+  if (rc != NARDE_OK) {
+    narde_destroy(e);
+    return rc;
+  }
+  e->epoch = 1;
+  *out = e;
+  return NARDE_OK;
+}
+
+int narde_destroy(narde_env* e) {
+  if (!e) return NARDE_OK;
+  DeviceGuard dg(e->device);
+  if (e->hstream) (void)hipStreamSynchronize(e->hstream);
+  (void)hipFree(e->pl.p0); (void)hipFree(e->pl.p1); (void)hipFree(e->pl.stats);
+  (void)hipFree(e->hpl.p0); (void)hipFree(e->hpl.p1); (void)hipFree(e->hpl.stats);
+  (void)hipFree(e->d_in); (void)hipFree(e->d_out);
+  if (e->h_in) (void)hipHostFree(e->h_in);
+  if (e->h_out) (void)hipHostFree(e->h_out);
+  if (e->hstream) (void)hipStreamDestroy(e->hstream);
+  delete e;
+  return NARDE_OK;
+}
+
+int64_t narde_num_envs(const narde_env* e) { return e ? e->n : -1; }
+
+int narde_get_ply(const narde_env* e, uint32_t* t) {
+  if (!e || !t) return fail(NARDE_EINVAL, "NULL argument");
+  *t = e->t;
+  return NARDE_OK;
+}
+
+int narde_set_ply(narde_env* e, uint32_t t) {
+  if (!e) return fail(NARDE_EINVAL, "NULL handle");
+  e->t = t;
+  return NARDE_OK;
+}
+
+int narde_reset(narde_env* e, const uint8_t* mask, void* stream) {
+  if (!e) return fail(NARDE_EINVAL, "NULL handle");
+  DeviceGuard dg(e->device);
+  k_reset<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), e->epoch, mask);
+  e->epoch += 1;
+  return check_launch("k_reset");
+}
+
+int narde_set_state(narde_env* e, const int8_t* board, const uint8_t* off, const uint8_t* ft,
+                    const int8_t* player, const uint16_t* elapsed, void* stream) {
+  if (!e || !board || !off || !ft || !player) return fail(NARDE_EINVAL, "NULL argument");
+  DeviceGuard dg(e->device);
+  k_set_state<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, board, off, ft, player,
+                                                              elapsed);
+  return check_launch("k_set_state");
+}
+
+int narde_get_state(narde_env* e, int8_t* board, uint8_t* off, uint8_t* ft, int8_t* player,
+                    uint16_t* elapsed, void* stream) {
+  if (!e) return fail(NARDE_EINVAL, "NULL handle");
+  DeviceGuard dg(e->device);
+  k_get_state<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, board, off, ft, player,
+                                                              elapsed);
+  return check_launch("k_get_state");
+}
+
+int narde_peek_dice(narde_env* e, uint8_t* dice, void* stream) {
+  if (!e || !dice) return fail(NARDE_EINVAL, "NULL argument");
+  DeviceGuard dg(e->device);
+  k_peek_dice<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>((int)e->n, rng_of(e), e->t, dice);
+  return check_launch("k_peek_dice");
+}
+
+int narde_legal_moves(narde_env* e, const uint8_t* dice, int16_t* out_count, int8_t* out_moves,
+                      uint64_t* out_compact, void* stream) {
+  if (!e || !out_count) return fail(NARDE_EINVAL, "NULL argument");
+  DeviceGuard dg(e->device);
+  k_legal<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), e->t, dice,
+                                                          out_count, out_moves, out_compact);
+  return check_launch("k_legal");
+}
+
+int narde_step(narde_env* e, const int16_t* actions, const uint8_t* dice, int32_t* obs,
+               int32_t* reward, uint8_t* terminated, uint8_t* truncated, uint64_t* legal_compact,
+               int16_t* actions_out, int autoreset, void* stream) {
+  if (!e) return fail(NARDE_EINVAL, "NULL handle");
+  DeviceGuard dg(e->device);
+  StepArgs a;
+  a.pl = e->pl;
+  a.n = (int)e->n;
+  a.g = rng_of(e);
+  a.t = e->t;
+  a.max_steps = e->max_steps;
+  a.autoreset = autoreset;
+  a.actions = actions;
+  a.dice = dice;
+  a.obs = obs;
+  a.reward = reward;
+  a.term = terminated;
+  a.trunc = truncated;
+  a.legal = legal_compact;
+  a.act_out = actions_out;
+  k_step<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(a);
+  e->t += 1;
+  return check_launch("k_step");
+}
+
+int narde_selfplay(narde_env* e, int plies, void* stream) {
+  if (!e || plies < 0) return fail(NARDE_EINVAL, "bad argument");
+  if (plies == 0) return NARDE_OK;
+  DeviceGuard dg(e->device);
+  k_selfplay<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), e->t, plies,
+                                                             e->max_steps);
+  e->t += (uint32_t)plies;
+  return check_launch("k_selfplay");
+}
+
+int narde_get_stats(narde_env* e, int32_t* stats, void* stream) {
+  if (!e || !stats) return fail(NARDE_EINVAL, "NULL argument");
+  DeviceGuard dg(e->device);
+  k_get_stats<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, stats);
+  return check_launch("k_get_stats");
+}
+
+int narde_apply_moves(narde_env* e, const int8_t* moves, const int8_t* player, void* stream) {
+  if (!e || !moves) return fail(NARDE_EINVAL, "NULL argument");
+  DeviceGuard dg(e->device);
+  k_apply<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, moves, player);
+  return check_launch("k_apply");
+}
+
+int narde_observe(narde_env* e, int32_t* obs, float* tes, void* stream) {
+  if (!e) return fail(NARDE_EINVAL, "NULL handle");
+  if (!obs && !tes) return NARDE_OK;
+  DeviceGuard dg(e->device);
+  k_observe<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, obs, tes);
+  return check_launch("k_observe");
+}
+
+int narde_legal_mask576(narde_env* e, uint64_t* mask, void* stream) {
+  if (!e || !mask) return fail(NARDE_EINVAL, "NULL argument");
+  DeviceGuard dg(e->device);
+  k_mask576<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), e->t, mask);
+  return check_launch("k_mask576");
+}
+
+int narde_violates_block_rule(int device, const int8_t* boards, int64_t n, uint8_t* out, void* stream) {
+  if (!boards || !out || n < 0 || n > (int64_t(1) << 31) - kBlock) return fail(NARDE_EINVAL, "bad argument");
+  if (n == 0) return NARDE_OK;
+  DeviceGuard dg(device);
+  k_block<<<grid(n), kBlock, 0, (hipStream_t)stream>>>(boards, (int)n, out);
+  return check_launch("k_block");
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------- host entry points
+namespace {
+
+struct Carve {
+  uint8_t* base;
+  size_t off = 0;
+  template <class T>
+  T* take(int64_t count) {
+    T* p = reinterpret_cast<T*>(base + off);
+    off += ((size_t)count * sizeof(T) + 255) & ~size_t(255);
+    return p;
+  }
+};
+
+int host_check(narde_env* e, int64_t n) {
+  if (!e) return fail(NARDE_EINVAL, "NULL handle");
+  if (n < 0 || n > kHostCap) return fail(NARDE_EINVAL, "host batch %lld > %lld", (long long)n, (long long)kHostCap);
+  return NARDE_OK;
+}
+
+int host_validate(int64_t n, const int8_t* board, const uint8_t* off, const uint8_t* ft,
+                  const int8_t* player) {
+  for (int64_t i = 0; i < n; ++i)
+    if (!valid_position(board, off, ft, player, i))
+      return fail(NARDE_EINVAL, "invalid position at index %lld", (long long)i);
+  return NARDE_OK;
+}
+
+int host_sync(narde_env* e) {
+  HIP_TRY(hipStreamSynchronize(e->hstream));
+  return NARDE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int narde_host_legal_moves(narde_env* e, int64_t n, const int8_t* board, const uint8_t* off,
+                           const uint8_t* ft, const int8_t* player, const uint8_t* dice4,
+                           int16_t* count, int8_t* moves) {
+  int rc = host_check(e, n);
+  if (rc) return rc;
+  if (n == 0) return NARDE_OK;
+  if (!board || !off || !ft || !player || !dice4 || !count) return fail(NARDE_EINVAL, "NULL argument");
+  if ((rc = host_validate(n, board, off, ft, player))) return rc;
+  DeviceGuard dg(e->device);
+  Carve hi{e->h_in}, di{e->d_in}, ho{e->h_out}, dq{e->d_out};
+  int8_t* hb = hi.take<int8_t>(n * 24); int8_t* db = di.take<int8_t>(n * 24);
+  uint8_t* hoff = hi.take<uint8_t>(n * 2); uint8_t* doff = di.take<uint8_t>(n * 2);
+  uint8_t* hft = hi.take<uint8_t>(n * 2); uint8_t* dft = di.take<uint8_t>(n * 2);
+  int8_t* hp = hi.take<int8_t>(n); int8_t* dp = di.take<int8_t>(n);
+  uint8_t* hd = hi.take<uint8_t>(n * 4); uint8_t* dd = di.take<uint8_t>(n * 4);
+  memcpy(hb, board, n * 24); memcpy(hoff, off, n * 2); memcpy(hft, ft, n * 2);
+  memcpy(hp, player, n); memcpy(hd, dice4, n * 4);
+  int16_t* hc = ho.take<int16_t>(n); int16_t* dc = dq.take<int16_t>(n);
+  int8_t* hm = ho.take<int8_t>(n * NARDE_MAX_MOVES * 2); int8_t* dm = dq.take<int8_t>(n * NARDE_MAX_MOVES * 2);
+  HIP_TRY(hipMemcpyAsync(e->d_in, e->h_in, hi.off, hipMemcpyHostToDevice, e->hstream));
+  k_set_state<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, db, doff, dft, dp, nullptr);
+  k_legal<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, rng_of(e), 0u, dd, dc, moves ? dm : nullptr,
+                                              nullptr);
+  if ((rc = check_launch("host legal"))) return rc;
+  HIP_TRY(hipMemcpyAsync(e->h_out, e->d_out, dq.off, hipMemcpyDeviceToHost, e->hstream));
+  if ((rc = host_sync(e))) return rc;
+  memcpy(count, hc, n * sizeof(int16_t));
+  if (moves) memcpy(moves, hm, n * NARDE_MAX_MOVES * 2);
+  return NARDE_OK;
+}
+
+int narde_host_step(narde_env* e, int64_t n, int8_t* board, uint8_t* off, uint8_t* ft, int8_t* player,
+                    const uint8_t* dice2, const int16_t* actions, int32_t* obs, int32_t* reward,
+                    uint8_t* terminated) {
+  int rc = host_check(e, n);
+  if (rc) return rc;
+  if (n == 0) return NARDE_OK;
+  if (!board || !off || !ft || !player || !dice2 || !actions) return fail(NARDE_EINVAL, "NULL argument");
+  if ((rc = host_validate(n, board, off, ft, player))) return rc;
+  for (int64_t i = 0; i < 2 * n; ++i)
+    if (dice2[i] < 1 || dice2[i] > 6) return fail(NARDE_EINVAL, "die out of range at %lld", (long long)i);
+  DeviceGuard dg(e->device);
+  Carve hi{e->h_in}, di{e->d_in}, ho{e->h_out}, dq{e->d_out};
+  int8_t* hb = hi.take<int8_t>(n * 24); int8_t* db = di.take<int8_t>(n * 24);
+  uint8_t* hoff = hi.take<uint8_t>(n * 2); uint8_t* doff = di.take<uint8_t>(n * 2);
+  uint8_t* hft = hi.take<uint8_t>(n * 2); uint8_t* dft = di.take<uint8_t>(n * 2);
+  int8_t* hp = hi.take<int8_t>(n); int8_t* dp = di.take<int8_t>(n);
+  uint8_t* hd = hi.take<uint8_t>(n * 2); uint8_t* dd = di.take<uint8_t>(n * 2);
+  int16_t* ha = hi.take<int16_t>(n * 2); int16_t* da = di.take<int16_t>(n * 2);
+  memcpy(hb, board, n * 24); memcpy(hoff, off, n * 2); memcpy(hft, ft, n * 2);
+  memcpy(hp, player, n); memcpy(hd, dice2, n * 2); memcpy(ha, actions, n * 4);
+  int8_t* hb2 = ho.take<int8_t>(n * 24); int8_t* db2 = dq.take<int8_t>(n * 24);
+  uint8_t* hoff2 = ho.take<uint8_t>(n * 2); uint8_t* doff2 = dq.take<uint8_t>(n * 2);
+  uint8_t* hft2 = ho.take<uint8_t>(n * 2); uint8_t* dft2 = dq.take<uint8_t>(n * 2);
+  int8_t* hp2 = ho.take<int8_t>(n); int8_t* dp2 = dq.take<int8_t>(n);
+  int32_t* hobs = ho.take<int32_t>(n * 24); int32_t* dobs = dq.take<int32_t>(n * 24);
+  int32_t* hr = ho.take<int32_t>(n); int32_t* dr = dq.take<int32_t>(n);
+  uint8_t* ht = ho.take<uint8_t>(n); uint8_t* dt = dq.take<uint8_t>(n);
+  HIP_TRY(hipMemcpyAsync(e->d_in, e->h_in, hi.off, hipMemcpyHostToDevice, e->hstream));
+  k_set_state<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, db, doff, dft, dp, nullptr);
+  StepArgs a;
+  a.pl = e->hpl;
+  a.n = (int)n;
+  a.g = rng_of(e);
+  a.t = 0;
+  a.max_steps = 0;
+  a.autoreset = 0;
+  a.actions = da;
+  a.dice = dd;
+  a.obs = dobs;
+  a.reward = dr;
+  a.term = dt;
+  a.trunc = nullptr;
+  a.legal = nullptr;
+  a.act_out = nullptr;
+  k_step<<<grid(n), kBlock, 0, e->hstream>>>(a);
+  k_get_state<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, db2, doff2, dft2, dp2, nullptr);
+  if ((rc = check_launch("host step"))) return rc;
+  HIP_TRY(hipMemcpyAsync(e->h_out, e->d_out, dq.off, hipMemcpyDeviceToHost, e->hstream));
+  if ((rc = host_sync(e))) return rc;
+  memcpy(board, hb2, n * 24); memcpy(off, hoff2, n * 2); memcpy(ft, hft2, n * 2); memcpy(player, hp2, n);
+  if (obs) memcpy(obs, hobs, n * 24 * sizeof(int32_t));
+  if (reward) memcpy(reward, hr, n * sizeof(int32_t));
+  if (terminated) memcpy(terminated, ht, n);
+  return NARDE_OK;
+}
+
+int narde_host_apply_moves(narde_env* e, int64_t n, int8_t* board, uint8_t* off, uint8_t* ft,
+                           const int8_t* player, const int8_t* moves) {
+  int rc = host_check(e, n);
+  if (rc) return rc;
+  if (n == 0) return NARDE_OK;
+  if (!board || !off || !ft || !player || !moves) return fail(NARDE_EINVAL, "NULL argument");
+  if ((rc = host_validate(n, board, off, ft, player))) return rc;
+  DeviceGuard dg(e->device);
+  Carve hi{e->h_in}, di{e->d_in}, ho{e->h_out}, dq{e->d_out};
+  int8_t* hb = hi.take<int8_t>(n * 24); int8_t* db = di.take<int8_t>(n * 24);
+  uint8_t* hoff = hi.take<uint8_t>(n * 2); uint8_t* doff = di.take<uint8_t>(n * 2);
+  uint8_t* hft = hi.take<uint8_t>(n * 2); uint8_t* dft = di.take<uint8_t>(n * 2);
+  int8_t* hp = hi.take<int8_t>(n); int8_t* dp = di.take<int8_t>(n);
+  int8_t* hm = hi.take<int8_t>(n * 2); int8_t* dm = di.take<int8_t>(n * 2);
+  memcpy(hb, board, n * 24); memcpy(hoff, off, n * 2); memcpy(hft, ft, n * 2);
+  memcpy(hp, player, n); memcpy(hm, moves, n * 2);
+  int8_t* hb2 = ho.take<int8_t>(n * 24); int8_t* db2 = dq.take<int8_t>(n * 24);
+  uint8_t* hoff2 = ho.take<uint8_t>(n * 2); uint8_t* doff2 = dq.take<uint8_t>(n * 2);
+  uint8_t* hft2 = ho.take<uint8_t>(n * 2); uint8_t* dft2 = dq.take<uint8_t>(n * 2);
+  HIP_TRY(hipMemcpyAsync(e->d_in, e->h_in, hi.off, hipMemcpyHostToDevice, e->hstream));
+  k_set_state<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, db, doff, dft, dp, nullptr);
+  k_apply<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, dm, dp);
+  k_get_state<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, db2, doff2, dft2, nullptr, nullptr);
+  if ((rc = check_launch("host apply"))) return rc;
+  HIP_TRY(hipMemcpyAsync(e->h_out, e->d_out, dq.off, hipMemcpyDeviceToHost, e->hstream));
+  if ((rc = host_sync(e))) return rc;
+  memcpy(board, hb2, n * 24); memcpy(off, hoff2, n * 2); memcpy(ft, hft2, n * 2);
+  return NARDE_OK;
+}
+
+int narde_host_violates_block_rule(narde_env* e, int64_t n, const int8_t* boards, uint8_t* out) {
+  int rc = host_check(e, n);
+  if (rc) return rc;
+  if (n == 0) return NARDE_OK;
+  if (!boards || !out) return fail(NARDE_EINVAL, "NULL argument");
+  DeviceGuard dg(e->device);
+  Carve hi{e->h_in}, di{e->d_in}, ho{e->h_out}, dq{e->d_out};
+  int8_t* hb = hi.take<int8_t>(n * 24); int8_t* db = di.take<int8_t>(n * 24);
+  memcpy(hb, boards, n * 24);
+  uint8_t* hr = ho.take<uint8_t>(n); uint8_t* dr = dq.take<uint8_t>(n);
+  HIP_TRY(hipMemcpyAsync(e->d_in, e->h_in, hi.off, hipMemcpyHostToDevice, e->hstream));
+  k_block<<<grid(n), kBlock, 0, e->hstream>>>(db, (int)n, dr);
+  if ((rc = check_launch("host block"))) return rc;
+  HIP_TRY(hipMemcpyAsync(e->h_out, e->d_out, dq.off, hipMemcpyDeviceToHost, e->hstream));
+  if ((rc = host_sync(e))) return rc;
+  memcpy(out, hr, n);
+  return NARDE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,483 @@
+// narde_rules.h -- branchless-bitmask Narde rules engine for one env per lane.
+//
+// MI355X-native restatement of the reference hot path (cites are
+// /root/reference/<path>:<line>):
+//   Narde.get_valid_moves        gym_narde/envs/narde.py:58-92
+//   Narde._violates_block_rule   gym_narde/envs/narde.py:139-184
+//   Narde._filter_head_moves     gym_narde/envs/narde.py:94-106,127-137
+//   Narde.execute_rotated_move   gym_narde/envs/narde.py:36-56,108-125
+//   NardeEnv.step                gym_narde/envs/narde_env.py:27-103
+//   NardeEnv._check_game_ended   gym_narde/envs/narde_env.py:134-141
+//
+// Representation (all in the MOVER's perspective, mover checkers move toward
+// lower indices, head = 23, home = 0..5, 'off' encoded as to = 24):
+//   * counts: 24 points x 4-bit nibbles per side (Nib: lo = points 0..15,
+//     hi = points 16..23); a side never has more than 15 checkers.
+//   * masks: O (own occupied), P (opponent occupied), S1o/S1p (count == 1).
+//   * a legal-move list is a list of per-die 24-bit source masks L[k] with
+//     dice d[k] sorted descending: entry order = die-major, source ascending,
+//     which is exactly the reference's list order (duplicates included).
+// The whole engine is __host__ __device__ so the same code runs on the GPU
+// and in the test-only host build (tests/hostcheck).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define NARDE_FN __host__ __device__ __forceinline__
+
+namespace narde {
+
+constexpr uint32_t MASK24 = 0xFFFFFFu;
+constexpr int OFF = 24;
+
+// ---------------------------------------------------------------- nibbles
+struct Nib {
+  uint64_t lo;  // points 0..15
+  uint32_t hi;  // points 16..23
+};
+
+NARDE_FN uint32_t nib_get(const Nib& b, int p) {
+  return p < 16 ? (uint32_t)(b.lo >> (4 * p)) & 15u : (b.hi >> (4 * (p - 16))) & 15u;
+}
+NARDE_FN void nib_inc(Nib& b, int p) {
+  if (p < 16) b.lo += 1ull << (4 * p);
+  else b.hi += 1u << (4 * (p - 16));
+}
+NARDE_FN void nib_dec(Nib& b, int p) {
+  if (p < 16) b.lo -= 1ull << (4 * p);
+  else b.hi -= 1u << (4 * (p - 16));
+}
+// perspective flip: new[p] = old[(p + 12) % 24]  (narde.py:16-17 without the sign)
+NARDE_FN Nib nib_rot12(const Nib& b) {
+  Nib r;
+  r.lo = (b.lo >> 48) | ((uint64_t)b.hi << 16) | (b.lo << 48);
+  r.hi = (uint32_t)(b.lo >> 16);
+  return r;
+}
+NARDE_FN uint32_t rot12(uint32_t m) { return ((m >> 12) | (m << 12)) & MASK24; }
+
+// gather bit 4k of x (k = 0..7) into bit k
+NARDE_FN uint32_t compact4(uint32_t x) {
+  x = (x | (x >> 3)) & 0x03030303u;
+  x = (x | (x >> 6)) & 0x000F000Fu;
+  x = (x | (x >> 12)) & 0x000000FFu;
+  return x;
+}
+NARDE_FN uint32_t fold_nz(uint32_t x) {
+  x |= x >> 1;
+  x |= x >> 2;
+  return x & 0x11111111u;
+}
+NARDE_FN uint32_t nz_mask(const Nib& b) {
+  return compact4(fold_nz((uint32_t)b.lo)) | (compact4(fold_nz((uint32_t)(b.lo >> 32))) << 8) |
+         (compact4(fold_nz(b.hi)) << 16);
+}
+NARDE_FN uint32_t eq1_mask(const Nib& b) {
+  const uint32_t k = 0x11111111u;
+  return compact4(~fold_nz((uint32_t)b.lo ^ k) & k) |
+         (compact4(~fold_nz((uint32_t)(b.lo >> 32) ^ k) & k) << 8) |
+         (compact4(~fold_nz(b.hi ^ k) & k) << 16);
+}
+
+// ------------------------------------------------------------ env record
+// HBM record = two 16-byte planes per env (planar => every load/store of a
+// wave is one contiguous 1 KiB):
+//   plane0 = {white nib lo (u64), black nib lo (u64)}      absolute coords
+//   plane1 = {white nib hi, black nib hi, misc, spare}
+//   misc   = off_w[0:4) | off_b[4:8) | ft_w<<8 | ft_b<<9 | black_to_move<<10
+//            | elapsed[16:32)
+struct Side {
+  Nib own, opp;
+  uint32_t O, P, S1o, S1p;
+  uint32_t off_own, off_opp;
+  uint32_t ft_own, ft_opp;
+  uint32_t black;    // 1 if the mover is black (current_player == -1)
+  uint32_t elapsed;  // steps taken in this episode (TimeLimit)
+};
+
+NARDE_FN void side_masks(Side& s) {
+  s.O = nz_mask(s.own);
+  s.P = nz_mask(s.opp);
+  s.S1o = eq1_mask(s.own);
+  s.S1p = eq1_mask(s.opp);
+}
+
+NARDE_FN Side side_from_record(const uint4& a, const uint4& b) {
+  Nib w{(uint64_t)a.x | ((uint64_t)a.y << 32), b.x};
+  Nib k{(uint64_t)a.z | ((uint64_t)a.w << 32), b.y};
+  const uint32_t misc = b.z;
+  Side s;
+  s.black = (misc >> 10) & 1u;
+  const uint32_t offw = misc & 15u, offb = (misc >> 4) & 15u;
+  const uint32_t ftw = (misc >> 8) & 1u, ftb = (misc >> 9) & 1u;
+  if (s.black) {
+    s.own = nib_rot12(k); s.opp = nib_rot12(w);
+    s.off_own = offb; s.off_opp = offw; s.ft_own = ftb; s.ft_opp = ftw;
+  } else {
+    s.own = w; s.opp = k;
+    s.off_own = offw; s.off_opp = offb; s.ft_own = ftw; s.ft_opp = ftb;
+  }
+  s.elapsed = misc >> 16;
+  side_masks(s);
+  return s;
+}
+
+NARDE_FN void side_to_record(const Side& s, uint4& a, uint4& b) {
+  Nib w, k;
+  uint32_t offw, offb, ftw, ftb;
+  if (s.black) {
+    w = nib_rot12(s.opp); k = nib_rot12(s.own);
+    offw = s.off_opp; offb = s.off_own; ftw = s.ft_opp; ftb = s.ft_own;
+  } else {
+    w = s.own; k = s.opp;
+    offw = s.off_own; offb = s.off_opp; ftw = s.ft_own; ftb = s.ft_opp;
+  }
+  a.x = (uint32_t)w.lo; a.y = (uint32_t)(w.lo >> 32);
+  a.z = (uint32_t)k.lo; a.w = (uint32_t)(k.lo >> 32);
+  b.x = w.hi; b.y = k.hi;
+  b.z = offw | (offb << 4) | (ftw << 8) | (ftb << 9) | (s.black << 10) | (s.elapsed << 16);
+  b.w = 0;
+}
+
+// reference layout (int8 board[24] absolute, off {w,b}, first_turn {w,b},
+// player +1/-1) <-> record.  Counts must be in 0..15 (checked by callers).
+NARDE_FN void record_from_board(const int8_t* board, uint32_t offw, uint32_t offb, uint32_t ftw,
+                                uint32_t ftb, int player, uint32_t elapsed, uint4& a, uint4& b) {
+  Nib w{0, 0}, k{0, 0};
+  for (int p = 0; p < 24; ++p) {
+    const int v = board[p];
+    const uint32_t cw = v > 0 ? (uint32_t)v : 0u, ck = v < 0 ? (uint32_t)(-v) : 0u;
+    if (p < 16) {
+      w.lo |= (uint64_t)(cw & 15u) << (4 * p);
+      k.lo |= (uint64_t)(ck & 15u) << (4 * p);
+    } else {
+      w.hi |= (cw & 15u) << (4 * (p - 16));
+      k.hi |= (ck & 15u) << (4 * (p - 16));
+    }
+  }
+  a.x = (uint32_t)w.lo; a.y = (uint32_t)(w.lo >> 32);
+  a.z = (uint32_t)k.lo; a.w = (uint32_t)(k.lo >> 32);
+  b.x = w.hi; b.y = k.hi;
+  b.z = (offw & 15u) | ((offb & 15u) << 4) | ((ftw ? 1u : 0u) << 8) | ((ftb ? 1u : 0u) << 9) |
+        ((player == -1 ? 1u : 0u) << 10) | (elapsed << 16);
+  b.w = 0u;
+}
+
+NARDE_FN void board_from_record(const uint4& a, const uint4& b, int8_t* board, uint8_t* off,
+                                uint8_t* ft, int8_t* player, uint16_t* elapsed) {
+  const Nib w{(uint64_t)a.x | ((uint64_t)a.y << 32), b.x};
+  const Nib k{(uint64_t)a.z | ((uint64_t)a.w << 32), b.y};
+  if (board)
+    for (int p = 0; p < 24; ++p) board[p] = (int8_t)((int)nib_get(w, p) - (int)nib_get(k, p));
+  if (off) { off[0] = b.z & 15u; off[1] = (b.z >> 4) & 15u; }
+  if (ft) { ft[0] = (b.z >> 8) & 1u; ft[1] = (b.z >> 9) & 1u; }
+  if (player) *player = ((b.z >> 10) & 1u) ? -1 : 1;
+  if (elapsed) *elapsed = (uint16_t)(b.z >> 16);
+}
+
+// start position (narde.py:21-29): white 15 on abs 23, black 15 on abs 11
+NARDE_FN Side side_start(uint32_t black_first) {
+  Side s;
+  // in either perspective the mover has 15 on 23 and the opponent 15 on 11
+  s.own.lo = 0; s.own.hi = 15u << 28;
+  s.opp.lo = 15ull << 44; s.opp.hi = 0;
+  s.off_own = s.off_opp = 0;
+  s.ft_own = s.ft_opp = 1;
+  s.black = black_first;
+  s.elapsed = 0;
+  s.O = 1u << 23; s.P = 1u << 11; s.S1o = 0; s.S1p = 0;
+  return s;
+}
+
+// mover change (narde_env.py:99-100)
+NARDE_FN void side_flip(Side& s) {
+  Nib t = s.own;
+  s.own = nib_rot12(s.opp);
+  s.opp = nib_rot12(t);
+  uint32_t m = s.O; s.O = rot12(s.P); s.P = rot12(m);
+  m = s.S1o; s.S1o = rot12(s.S1p); s.S1p = rot12(m);
+  m = s.off_own; s.off_own = s.off_opp; s.off_opp = m;
+  m = s.ft_own; s.ft_own = s.ft_opp; s.ft_opp = m;
+  s.black ^= 1u;
+}
+
+// --------------------------------------------------------- move generation
+// bit i set iff points i..i+5 are all own (a 6-block starting at i)
+NARDE_FN uint32_t runs6(uint32_t m) {
+  const uint32_t a = m & (m >> 1);
+  const uint32_t b = a & (a >> 2);
+  return b & (a >> 4);
+}
+
+// Block rule (narde.py:139-184) as a mask test: a maximal own run of >= 6
+// violates iff no opponent checker sits below its start, i.e. iff some
+// 6-window start i <= lo = lowest opponent point (all 24 if none).
+NARDE_FN uint32_t block_lowmask(uint32_t P) {
+  return P ? ((2u << __builtin_ctz(P)) - 1u) : MASK24;
+}
+
+// narde.py:64-77 for one die: sources with a legal single move
+NARDE_FN uint32_t die_candidates(uint32_t O, uint32_t P, int d) {
+  const uint32_t normal = O & ~(P << d) & (MASK24 << d) & MASK24;
+  const uint32_t off = ((O >> 6) == 0u) ? (O & ((1u << d) - 1u)) : 0u;  // bear-off, :73-77
+  return normal | off;
+}
+
+// narde.py:78-89 block filter of one die's candidates
+NARDE_FN uint32_t die_filter(uint32_t O, uint32_t S1, uint32_t lowmask, uint32_t C, int d) {
+  if ((runs6(O | (C >> d)) & lowmask) == 0u) return C;  // no candidate can form a block
+  uint32_t L = C, m = C;
+  while (m) {
+    const int p = __builtin_ctz(m);
+    m &= m - 1u;
+    const uint32_t bp = 1u << p;
+    const uint32_t Op = (O & ~(S1 & bp)) | (p >= d ? (1u << (p - d)) : 0u);
+    if (runs6(Op) & lowmask) L &= ~bp;
+  }
+  return L;
+}
+
+struct Legal {
+  uint32_t L[4];
+  int d[4];
+  int n;
+  int count;
+};
+
+// Narde.get_valid_moves(roll, mover) for n <= 4 dice already sorted descending.
+// first_turn: mover's first_turn flag (head-rule exception, narde.py:100).
+NARDE_FN void legal_sorted(const Side& s, const int* dd, int n, Legal& l) {
+  const uint32_t low = block_lowmask(s.P);
+  l.n = n;
+  for (int k = 0; k < 4; ++k) { l.L[k] = 0u; l.d[k] = 0; }
+  for (int k = 0; k < n; ++k) {
+    l.d[k] = dd[k];
+    if (k > 0 && dd[k] == dd[k - 1]) { l.L[k] = l.L[k - 1]; continue; }
+    l.L[k] = die_filter(s.O, s.S1o, low, die_candidates(s.O, s.P, dd[k]), dd[k]);
+  }
+  // head rule (narde.py:94-106,127-137): keep the first max_head entries from 23
+  const int max_head =
+      (s.ft_own && n == 2 && dd[0] == dd[1] && (dd[0] == 3 || dd[0] == 4 || dd[0] == 6)) ? 2 : 1;
+  int seen = 0;
+  int count = 0;
+  for (int k = 0; k < n; ++k) {
+    if (l.L[k] >> 23) {
+      if (seen < max_head) ++seen;
+      else l.L[k] &= ~(1u << 23);
+    }
+    count += __builtin_popcount(l.L[k]);
+  }
+  l.count = count;
+}
+
+NARDE_FN void legal2(const Side& s, int d0, int d1, Legal& l) {
+  int dd[2] = {d0 > d1 ? d0 : d1, d0 > d1 ? d1 : d0};
+  legal_sorted(s, dd, 2, l);
+}
+
+// get_valid_moves for an explicit roll of up to 4 dice (0 = unused slot)
+NARDE_FN void legal_roll(const Side& s, const uint8_t* d4, Legal& l) {
+  int dd[4] = {0, 0, 0, 0};
+  int nd = 0;
+  for (int k = 0; k < 4; ++k) {
+    const int v = d4[k];
+    if (v >= 1 && v <= 6) dd[nd++] = v;
+  }
+  // roll = sorted(roll, reverse=True), narde.py:59
+  for (int a = 1; a < 4; ++a)
+    for (int b = a; b > 0; --b)
+      if (dd[b] > dd[b - 1]) { const int x = dd[b]; dd[b] = dd[b - 1]; dd[b - 1] = x; }
+  legal_sorted(s, dd, nd, l);
+}
+
+// j-th (0-based) set bit of m (j < popcount(m))
+NARDE_FN int select_bit(uint32_t m, int j) {
+  for (int i = 0; i < j; ++i) m &= m - 1u;
+  return __builtin_ctz(m);
+}
+
+// list entry i -> (from, to); to = OFF for bear-off
+NARDE_FN void legal_entry(const Legal& l, int i, int& f, int& t) {
+  int k = 0;
+  for (; k < l.n - 1; ++k) {
+    const int c = __builtin_popcount(l.L[k]);
+    if (i < c) break;
+    i -= c;
+  }
+  f = select_bit(l.L[k], i);
+  t = f - l.d[k] < 0 ? OFF : f - l.d[k];
+}
+
+// `move in valid_moves` (narde_env.py:255/281 analogue) in O(n)
+NARDE_FN bool legal_contains(const Legal& l, int f, int t) {
+  if (f < 0 || f > 23) return false;
+  const uint32_t bf = 1u << f;
+  bool hit = false;
+  for (int k = 0; k < l.n; ++k)
+    hit |= (l.L[k] & bf) != 0u && (t == OFF ? (f < l.d[k]) : (f - t == l.d[k]));
+  return hit;
+}
+
+NARDE_FN int encode_move(int f, int t) { return f * 24 + (t == OFF ? 0 : t); }
+
+// narde_env.py:238-254 action decode (the 'off' quirk: to==0 & from<=5)
+NARDE_FN void decode_action(int code, int& f, int& t) {
+  if (code < 0 || code >= 576) { f = -1; t = -1; return; }
+  f = code / 24;
+  t = code % 24;
+  if (t == 0 && f <= 5) t = OFF;
+}
+
+// execute_rotated_move in mover perspective (narde.py:36-56,108-125)
+NARDE_FN void apply_move(Side& s, int f, int t) {
+  const uint32_t cf = nib_get(s.own, f);
+  nib_dec(s.own, f);
+  const uint32_t bf = 1u << f;
+  if (cf == 1u) { s.O &= ~bf; s.S1o &= ~bf; }
+  else if (cf == 2u) { s.S1o |= bf; }
+  if (t == OFF) {
+    s.off_own += 1u;
+  } else {
+    const uint32_t ct = nib_get(s.own, t);
+    nib_inc(s.own, t);
+    const uint32_t bt = 1u << t;
+    if (ct == 0u) { s.O |= bt; s.S1o |= bt; }
+    else if (ct == 1u) { s.S1o &= ~bt; }
+  }
+  s.ft_own = 0u;
+}
+
+NARDE_FN uint32_t mulhi_u32(uint32_t r, uint32_t n) { return (uint32_t)(((uint64_t)r * n) >> 32); }
+
+struct StepOut {
+  Legal l1;
+  uint32_t L2;
+  int d2;
+  int count2;  // -1 when no second list was generated
+  int code1, code2;
+  int reward;
+  int term;
+};
+
+// NardeEnv.step (narde_env.py:27-103) with dice (d0, d1) in roll order.
+// policy: draw code1 from list1 with r1 and code2 from the env's own second
+// list with r2 (the build's random-legal policy); otherwise use code1/code2.
+NARDE_FN void env_step(Side& s, int d0, int d1, int code1, int code2, bool policy, uint32_t r1,
+                       uint32_t r2, StepOut& o) {
+  legal2(s, d0, d1, o.l1);
+  o.L2 = 0u; o.d2 = 0; o.count2 = -1;
+  const int n1 = o.l1.count;
+  if (policy) {
+    code1 = 0; code2 = 0;
+    if (n1 >= 2) {
+      int f, t;
+      legal_entry(o.l1, (int)mulhi_u32(r1, (uint32_t)n1), f, t);
+      code1 = encode_move(f, t);
+    }
+  }
+  if (n1 == 1) {
+    int f, t;
+    legal_entry(o.l1, 0, f, t);
+    apply_move(s, f, t);  // narde_env.py:41-43, action ignored
+  } else if (n1 >= 2) {
+    int f1, t1;
+    decode_action(code1, f1, t1);
+    if (legal_contains(o.l1, f1, t1)) {
+      apply_move(s, f1, t1);
+      // die bookkeeping, narde_env.py:63-83: remove dist if rolled, else pop(0)
+      const int dist = t1 == OFF ? f1 + 1 : (f1 > t1 ? f1 - t1 : t1 - f1);
+      const int rem = (d0 == dist) ? d1 : ((d1 == dist) ? d0 : d1);
+      // second get_valid_moves([rem]) (:88): one die, first_turn already cleared
+      const uint32_t low = block_lowmask(s.P);
+      o.L2 = die_filter(s.O, s.S1o, low, die_candidates(s.O, s.P, rem), rem);
+      o.d2 = rem;
+      o.count2 = __builtin_popcount(o.L2);
+      if (policy) {
+        if (o.count2 > 0) {
+          const int f = select_bit(o.L2, (int)mulhi_u32(r2, (uint32_t)o.count2));
+          code2 = encode_move(f, f - rem < 0 ? OFF : f - rem);
+        }
+      }
+      int f2, t2;
+      decode_action(code2, f2, t2);
+      if (f2 >= 0 && ((o.L2 >> f2) & 1u) && (t2 == OFF ? (f2 < rem) : (f2 - t2 == rem)))
+        apply_move(s, f2, t2);
+    }
+  }
+  o.code1 = code1;
+  o.code2 = code2;
+  // _check_game_ended (narde_env.py:134-141): only the mover is checked
+  o.term = s.off_own == 15u;
+  o.reward = o.term ? (s.off_opp > 0u ? 1 : 2) : 0;
+  if (!o.term) side_flip(s);
+}
+
+// obs = get_perspective_board(current_player) (narde.py:31-34): int32[24]
+NARDE_FN int obs_point(const Side& s, int p) { return (int)nib_get(s.own, p) - (int)nib_get(s.opp, p); }
+
+// ------------------------------------------------------------- Philox4x32-10
+NARDE_FN void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                            uint32_t k1, uint32_t out[4]) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+// dice_mode 0: 36 ordered pairs; 1: the 30 ordered non-double pairs
+NARDE_FN void dice_from(uint32_t r, int dice_mode, int& d0, int& d1) {
+  if (dice_mode == 1) {
+    const uint32_t k = mulhi_u32(r, 30u);
+    const int a = (int)(k / 5u) + 1, j = (int)(k % 5u);
+    d0 = a;
+    d1 = j < a - 1 ? j + 1 : j + 2;
+  } else {
+    const uint32_t k = mulhi_u32(r, 36u);
+    d0 = (int)(k / 6u) + 1;
+    d1 = (int)(k % 6u) + 1;
+  }
+}
+
+// opening roll (narde_env.py:111-117): uniform over the 30 unequal ordered
+// pairs (same law as the reference's redraw loop); higher roll = white moves
+NARDE_FN Side side_reset(uint32_t r) {
+  int w, b;
+  dice_from(r, 1, w, b);
+  return side_start(w > b ? 0u : 1u);
+}
+
+// One lockstep ply for one env: NardeEnv.step + gymnasium TimeLimit
+// (max_episode_steps, gym_narde/__init__.py:3-7) + optional auto-reset.
+// r = Philox4x32-10(ctr = {t, env, 0, 0}): r0 dice (unless given), r1/r2
+// policy picks, r3 opening roll of the next episode.  st = {episodes,
+// white points, black points} increments.
+NARDE_FN void env_ply(Side& s, int4& st, const uint32_t r[4], bool have_dice, int d0, int d1,
+                      int dice_mode, bool policy, int c1, int c2, int max_steps, bool autoreset,
+                      StepOut& o, int& term, int& trunc) {
+  if (!have_dice) dice_from(r[0], dice_mode, d0, d1);
+  const uint32_t mover_black = s.black;
+  env_step(s, d0, d1, c1, c2, policy, r[1], r[2], o);
+  s.elapsed += 1u;
+  term = o.term;
+  trunc = max_steps > 0 && s.elapsed >= (uint32_t)max_steps;
+  if (term | trunc) {
+    st.x += 1;
+    if (term) {
+      if (mover_black) st.z += o.reward;
+      else st.y += o.reward;
+    }
+    if (autoreset) s = side_reset(r[3]);
+  }
+}
+
+}  // namespace narde

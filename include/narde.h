@@ -1,0 +1,161 @@
+/*
+ * narde.h -- C ABI of libnarde, the MI355X-native batched Narde environment.
+ *
+ * The reference (dmytroleonenko/gym-narde) is pure Python and has no FFI;
+ * this ABI is the boundary UNDER a Python facade that reproduces its
+ * gymnasium surface (gym-narde_amd/gym_narde/).  Each entry point names the
+ * reference function it replaces (paths under the reference checkout):
+ *
+ *   narde_reset              NardeEnv.reset           gym_narde/envs/narde_env.py:105-120
+ *   narde_legal_moves        Narde.get_valid_moves    gym_narde/envs/narde.py:58-92
+ *   narde_step               NardeEnv.step            gym_narde/envs/narde_env.py:27-103
+ *   narde_apply_moves        Narde.execute_rotated_move gym_narde/envs/narde.py:36-56
+ *   narde_violates_block_rule Narde._violates_block_rule gym_narde/envs/narde.py:139-184
+ *   narde_observe            NardeEnv._get_obs / get_perspective_board
+ *                                                     gym_narde/envs/narde_env.py:24-25,
+ *                                                     gym_narde/envs/narde.py:31-34
+ *                            + 198-float Tesauro obs   README.md:42-102 (spec only)
+ *   narde_get/set_state      direct `env.unwrapped.game` attribute access
+ *                            (train_deepq_pytorch.py:867-931, evaluate_model.py:22-134)
+ *   narde_selfplay           random-policy self-play loop (no reference equivalent;
+ *                            the benchmark workload of BASELINE.json)
+ *   narde_host_*             the same rules on small HOST batches (the scalar
+ *                            gym facade): staged through pinned memory, synchronous.
+ *
+ * Conventions
+ *   - Every pointer argument of a non-host entry point is a DEVICE pointer on
+ *     the handle's device (e.g. a torch tensor's data_ptr()); NULL means
+ *     "not requested" where documented.  Arrays are C-contiguous.
+ *   - `stream` is a hipStream_t (NULL = the null stream).  Calls are stream-
+ *     ordered and never synchronise unless documented (narde_host_*).
+ *   - Board layout = the reference's: int8[24] absolute points, white > 0,
+ *     black < 0 (point p = index p, white head 23, black head 11).
+ *     off = {borne_off_white, borne_off_black}; first_turn = {white, black};
+ *     player = current mover, +1 white / -1 black.
+ *   - A move is (from, to) in the MOVER's perspective, to = 24 for 'off'.
+ *   - Action codes are the reference's: from*24 + to, with to == 0 and
+ *     from <= 5 meaning (from, 'off') (narde_env.py:238-254).
+ *   - Return value: 0 on success, negative NARDE_E* on error;
+ *     narde_last_error() gives a message (thread-local).
+ */
+#ifndef NARDE_H
+#define NARDE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NARDE_OK 0
+#define NARDE_EINVAL (-1)
+#define NARDE_EHIP (-2)
+#define NARDE_ENOMEM (-3)
+
+#define NARDE_DICE_ALL36 0      /* dice uniform over the 36 ordered pairs      */
+#define NARDE_DICE_NODOUBLES 1  /* uniform over the 30 non-double ordered pairs */
+
+#define NARDE_MAX_MOVES 64      /* list capacity per env (4-die rolls give <= 60) */
+#define NARDE_OFF 24
+
+typedef struct narde_env narde_env; /* B envs resident in HBM on one device */
+
+int narde_version(void);
+const char *narde_last_error(void);
+
+/* Allocate B = num_envs env records on `device`.  Global env ids are
+ * env_id_offset .. env_id_offset+B-1 (device RNG is keyed by the global id,
+ * so a sharded run reproduces a single-GPU run).  max_episode_steps is the
+ * gymnasium TimeLimit (reference registers 1000: gym_narde/__init__.py:3-7);
+ * 0 disables truncation.  Envs start in the reset state of epoch 0. */
+int narde_create(int device, int64_t num_envs, int64_t env_id_offset, uint64_t seed,
+                 int dice_mode, int max_episode_steps, narde_env **out);
+int narde_destroy(narde_env *env);
+int64_t narde_num_envs(const narde_env *env);
+/* lockstep ply counter t: device dice/policy draws of the next step use
+ * Philox4x32-10(ctr = {t, global_env_id, 0, 0}, key = seed) */
+int narde_get_ply(const narde_env *env, uint32_t *t);
+int narde_set_ply(narde_env *env, uint32_t t);
+
+/* NardeEnv.reset: start position + opening roll (device RNG).  mask[B] (u8)
+ * selects envs, NULL = all.  Zeroes the per-env statistics of reset envs. */
+int narde_reset(narde_env *env, const uint8_t *mask, void *stream);
+
+/* Direct state access.  elapsed may be NULL (set: 0).  set_state validates on
+ * device; invalid envs (|board| > 15, > 15 checkers of a colour, off > 15,
+ * mixed player) are reported via the return value of narde_host_* only --
+ * the device path clamps nothing, so callers must pass legal positions. */
+int narde_set_state(narde_env *env, const int8_t *board, const uint8_t *off,
+                    const uint8_t *first_turn, const int8_t *player, const uint16_t *elapsed,
+                    void *stream);
+int narde_get_state(narde_env *env, int8_t *board, uint8_t *off, uint8_t *first_turn,
+                    int8_t *player, uint16_t *elapsed, void *stream);
+
+/* Dice the next narde_step(dice = NULL) will use, in roll order: u8[B][2]. */
+int narde_peek_dice(narde_env *env, uint8_t *dice, void *stream);
+
+/* Narde.get_valid_moves(roll, current_player) for every env's mover.
+ * dice: u8[B][4], 1..4 dice per env, unused slots 0; NULL = the next step's
+ * device dice.  out_count: i16[B].  out_moves (optional): i8[B][64][2] (from,
+ * to), -1 padded, exactly the reference's list (order + duplicates).
+ * out_compact (optional, only for <= 2 dice): u64[B] = L_hi | L_lo<<24 |
+ * d_hi<<48 | d_lo<<52 where L_* are the per-die 24-bit source masks. */
+int narde_legal_moves(narde_env *env, const uint8_t *dice, int16_t *out_count,
+                      int8_t *out_moves, uint64_t *out_compact, void *stream);
+
+/* NardeEnv.step for all B envs.  actions i16[B][2] = (move1_code,
+ * move2_code); NULL = in-kernel random legal policy.  dice u8[B][2] in roll
+ * order; NULL = device RNG for ply t.  Outputs (each optional, NULL = skip):
+ * obs i32[B][24] (next mover's perspective), reward i32[B], terminated u8[B],
+ * truncated u8[B], legal_compact u64[B] (list #1, format above),
+ * actions_out i16[B][2] (codes actually used).  autoreset != 0: envs that
+ * terminate or truncate are reset in the same call (obs is then the new
+ * episode's first obs) and counted in the statistics.  Increments t. */
+int narde_step(narde_env *env, const int16_t *actions, const uint8_t *dice, int32_t *obs,
+               int32_t *reward, uint8_t *terminated, uint8_t *truncated,
+               uint64_t *legal_compact, int16_t *actions_out, int autoreset, void *stream);
+
+/* `plies` lockstep plies of random-legal self-play with auto-reset, state
+ * kept in registers across plies (one launch).  Only statistics are
+ * produced; increments t by plies. */
+int narde_selfplay(narde_env *env, int plies, void *stream);
+
+/* Per-env statistics i32[B][3] = {episodes finished, white points, black
+ * points} since the last reset of that env. */
+int narde_get_stats(narde_env *env, int32_t *stats, void *stream);
+
+/* execute_rotated_move(move, player) per env: moves i8[B][2] in the
+ * perspective of player[B] (+1/-1; NULL = each env's current mover);
+ * from < 0 skips the env.  Clears that player's first_turn flag. */
+int narde_apply_moves(narde_env *env, const int8_t *moves, const int8_t *player, void *stream);
+
+/* obs i32[B][24] (current mover's perspective) and/or the 198-float
+ * Tesauro observation f32[B][198] (absolute points; white block first). */
+int narde_observe(narde_env *env, int32_t *obs, float *tesauro198, void *stream);
+
+/* 576-bit mask of legal move1 action codes for the next step's dice:
+ * u64[B][9], bit c set iff the reference would accept code c as move1. */
+int narde_legal_mask576(narde_env *env, uint64_t *mask, void *stream);
+
+/* Stateless: Narde._violates_block_rule on n perspective boards i8[n][24]. */
+int narde_violates_block_rule(int device, const int8_t *boards, int64_t n, uint8_t *out,
+                              void *stream);
+
+/* ---- host-memory entry points (scalar facade; synchronous) ----------------
+ * Same semantics as above on n <= 4096 envs given explicitly in HOST memory.
+ * The handle's own B envs are untouched.  Return NARDE_EINVAL for an invalid
+ * position (see narde_set_state). */
+int narde_host_legal_moves(narde_env *env, int64_t n, const int8_t *board, const uint8_t *off,
+                           const uint8_t *first_turn, const int8_t *player, const uint8_t *dice4,
+                           int16_t *count, int8_t *moves);
+int narde_host_step(narde_env *env, int64_t n, int8_t *board, uint8_t *off, uint8_t *first_turn,
+                    int8_t *player, const uint8_t *dice2, const int16_t *actions, int32_t *obs,
+                    int32_t *reward, uint8_t *terminated);
+int narde_host_apply_moves(narde_env *env, int64_t n, int8_t *board, uint8_t *off,
+                           uint8_t *first_turn, const int8_t *player, const int8_t *moves);
+int narde_host_violates_block_rule(narde_env *env, int64_t n, const int8_t *boards, uint8_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NARDE_H */

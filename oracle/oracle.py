@@ -1,0 +1,165 @@
+"""ctypes/numpy front-end for the C oracle (oracle/narde_oracle.c).
+
+TEST INFRASTRUCTURE ONLY -- imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, never by the product package (gym-narde_amd/).
+
+All arrays are numpy, C-contiguous; states are the build's absolute int8
+layout (board int8[24], off uint8[2] = (white, black), first_turn uint8[2] =
+(white, black), player int8 = +1/-1).  Moves use to = 24 for 'off'.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libnarde_oracle.so")
+MAXM = 64
+OFF = 24
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(LIB_PATH)
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+def legal_moves(board, ft, player, roll, nroll):
+    """Narde.get_valid_moves over a batch -> (moves int8[n,64,2], count int16[n])."""
+    board = _c(board, np.int8)
+    n = board.shape[0]
+    ft = _c(ft, np.uint8)
+    player = _c(player, np.int8)
+    roll = _c(roll, np.uint8)
+    nroll = _c(nroll, np.uint8)
+    moves = np.empty((n, MAXM, 2), np.int8)
+    count = np.empty(n, np.int16)
+    off = np.zeros((n, 2), np.uint8)
+    lib().or_legal_batch(ctypes.c_int64(n), _p(board), _p(off), _p(ft), _p(player), _p(roll),
+                         _p(nroll), _p(moves), _p(count))
+    return moves, count
+
+
+def violates_block_rule(board):
+    board = _c(board, np.int8)
+    out = np.empty(board.shape[0], np.uint8)
+    lib().or_block_batch(ctypes.c_int64(board.shape[0]), _p(board), _p(out))
+    return out
+
+
+def apply_move(board, off, ft, player, move):
+    board = _c(board, np.int8).copy()
+    off = _c(off, np.uint8).copy()
+    ft = _c(ft, np.uint8).copy()
+    player = _c(player, np.int8)
+    move = _c(move, np.int8)
+    lib().or_apply_batch(ctypes.c_int64(board.shape[0]), _p(board), _p(off), _p(ft), _p(player), _p(move))
+    return board, off, ft
+
+
+def step(board, off, ft, player, dice, action, with_lists=True):
+    """NardeEnv.step with injected dice; returns a dict of post-state + outputs."""
+    board = _c(board, np.int8).copy()
+    off = _c(off, np.uint8).copy()
+    ft = _c(ft, np.uint8).copy()
+    player = _c(player, np.int8).copy()
+    dice = _c(dice, np.uint8)
+    action = _c(action, np.int16)
+    n = board.shape[0]
+    obs = np.empty((n, 24), np.int8)
+    reward = np.empty(n, np.int8)
+    term = np.empty(n, np.uint8)
+    if with_lists:
+        list1 = np.empty((n, MAXM, 2), np.int8)
+        list2 = np.empty((n, MAXM, 2), np.int8)
+        count1 = np.empty(n, np.int16)
+        count2 = np.empty(n, np.int16)
+        roll2 = np.empty(n, np.uint8)
+    else:
+        list1 = list2 = count1 = count2 = roll2 = None
+    lib().or_step_batch(ctypes.c_int64(n), _p(board), _p(off), _p(ft), _p(player), _p(dice),
+                        _p(action), _p(obs), _p(reward), _p(term), _p(list1), _p(count1),
+                        _p(list2), _p(count2), _p(roll2))
+    return dict(board=board, off=off, first_turn=ft, player=player, obs=obs, reward=reward,
+                terminated=term, list1=list1, count1=count1, list2=list2, count2=count2,
+                roll2=roll2)
+
+
+def tesauro198(board, off, player):
+    board = _c(board, np.int8)
+    n = board.shape[0]
+    out = np.empty((n, 198), np.float32)
+    lib().or_tesauro198_batch(ctypes.c_int64(n), _p(board), _p(_c(off, np.uint8)),
+                              _p(_c(player, np.int8)), _p(out))
+    return out
+
+
+def philox(ctr, key):
+    c = (ctypes.c_uint32 * 4)(*ctr)
+    k = (ctypes.c_uint32 * 2)(*key)
+    o = (ctypes.c_uint32 * 4)()
+    lib().or_philox4x32_10(c, k, o)
+    return tuple(o)
+
+
+class SelfPlay:
+    """Batched self-play state for the restated random-legal driver."""
+
+    def __init__(self, n, seed=0, env0=0, dice_mode=0, max_steps=1000):
+        self.n, self.seed, self.env0 = n, seed, env0
+        self.dice_mode, self.max_steps = dice_mode, max_steps
+        self.board = np.zeros((n, 24), np.int8)
+        self.off = np.zeros((n, 2), np.uint8)
+        self.ft = np.zeros((n, 2), np.uint8)
+        self.player = np.zeros(n, np.int8)
+        self.elapsed = np.zeros(n, np.uint16)
+        self.stats = np.zeros((n, 3), np.int32)
+        self.t = 0
+
+    def reset(self, epoch=0):
+        lib().or_reset_batch(ctypes.c_int64(self.n), ctypes.c_int64(self.env0),
+                             ctypes.c_uint64(self.seed), ctypes.c_uint32(epoch),
+                             _p(self.board), _p(self.off), _p(self.ft), _p(self.player),
+                             _p(self.elapsed))
+        self.stats[:] = 0
+
+    def run(self, plies, record=True):
+        n = self.n
+        if record:
+            obs = np.empty((plies, n, 24), np.int8)
+            reward = np.empty((plies, n), np.int8)
+            term = np.empty((plies, n), np.uint8)
+            trunc = np.empty((plies, n), np.uint8)
+            dice = np.empty((plies, n, 2), np.uint8)
+            action = np.empty((plies, n, 2), np.int16)
+            count1 = np.empty((plies, n), np.int16)
+        else:
+            obs = reward = term = trunc = dice = action = count1 = None
+        lib().or_selfplay(ctypes.c_int64(n), ctypes.c_int64(self.env0), ctypes.c_uint64(self.seed),
+                          ctypes.c_uint32(self.t), ctypes.c_int(plies), ctypes.c_int(self.dice_mode),
+                          ctypes.c_int(self.max_steps), _p(self.board), _p(self.off), _p(self.ft),
+                          _p(self.player), _p(self.elapsed), _p(self.stats), _p(obs), _p(reward),
+                          _p(term), _p(trunc), _p(dice), _p(action), _p(count1))
+        self.t += plies
+        if record:
+            return dict(obs=obs, reward=reward, terminated=term, truncated=trunc, dice=dice,
+                        action=action, count1=count1)
+        return None

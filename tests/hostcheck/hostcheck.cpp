@@ -1,0 +1,123 @@
+// hostcheck.cpp -- TEST-ONLY host build of the device rules engine.
+//
+// Compiles gym-narde_amd/csrc/narde_rules.h (__host__ __device__) for the
+// CPU so the bitmask formulation can be diffed against the oracle and the
+// golden vectors in a container without a GPU.  It mirrors the per-lane
+// bodies of k_legal / k_step / k_selfplay / k_reset.  Never loaded by the
+// product: the product path is libnarde.so on the GPU and fails loudly
+// without it.  The GPU tests (tests/test_gpu_*.py) are the parity tests.
+#include <cstring>
+
+#include "../../gym-narde_amd/csrc/narde_rules.h"
+
+using namespace narde;
+
+static void draw(uint64_t seed, uint32_t t, uint32_t env, uint32_t stream, uint32_t r[4]) {
+  philox4x32_10(t, env, 0u, stream, (uint32_t)seed, (uint32_t)(seed >> 32), r);
+}
+
+static Side load(const int8_t* board, const uint8_t* off, const uint8_t* ft, int player,
+                 uint32_t elapsed) {
+  uint4 a, b;
+  record_from_board(board, off[0], off[1], ft[0], ft[1], player, elapsed, a, b);
+  return side_from_record(a, b);
+}
+
+static void store(const Side& s, int8_t* board, uint8_t* off, uint8_t* ft, int8_t* player,
+                  uint16_t* elapsed) {
+  uint4 a, b;
+  side_to_record(s, a, b);
+  board_from_record(a, b, board, off, ft, player, elapsed);
+}
+
+static void expand(const Legal& l, int8_t* out /*[64][2]*/) {
+  memset(out, -1, 128);
+  int e = 0;
+  for (int k = 0; k < l.n; ++k) {
+    uint32_t m = l.L[k];
+    while (m) {
+      const int f = __builtin_ctz(m);
+      m &= m - 1u;
+      out[2 * e] = (int8_t)f;
+      out[2 * e + 1] = (int8_t)(f - l.d[k] < 0 ? OFF : f - l.d[k]);
+      ++e;
+    }
+  }
+}
+
+extern "C" {
+
+void hc_legal_batch(int64_t n, const int8_t* board, const uint8_t* off, const uint8_t* ft,
+                    const int8_t* player, const uint8_t* roll4, int8_t* moves, int16_t* count) {
+  for (int64_t i = 0; i < n; ++i) {
+    const Side s = load(board + i * 24, off + 2 * i, ft + 2 * i, player[i], 0);
+    Legal l;
+    legal_roll(s, roll4 + 4 * i, l);
+    count[i] = (int16_t)l.count;
+    expand(l, moves + i * 128);
+  }
+}
+
+void hc_step_batch(int64_t n, int8_t* board, uint8_t* off, uint8_t* ft, int8_t* player,
+                   const uint8_t* dice, const int16_t* action, int8_t* obs, int8_t* reward,
+                   uint8_t* term, int8_t* list1, int16_t* count1, int8_t* list2, int16_t* count2) {
+  for (int64_t i = 0; i < n; ++i) {
+    Side s = load(board + i * 24, off + 2 * i, ft + 2 * i, player[i], 0);
+    StepOut o;
+    env_step(s, dice[2 * i], dice[2 * i + 1], action[2 * i], action[2 * i + 1], false, 0, 0, o);
+    for (int p = 0; p < 24; ++p) obs[i * 24 + p] = (int8_t)obs_point(s, p);
+    reward[i] = (int8_t)o.reward;
+    term[i] = (uint8_t)o.term;
+    count1[i] = (int16_t)o.l1.count;
+    expand(o.l1, list1 + i * 128);
+    count2[i] = (int16_t)o.count2;
+    Legal l2;
+    l2.n = 1; l2.L[0] = o.L2; l2.d[0] = o.d2; l2.count = o.count2;
+    if (o.count2 >= 0) expand(l2, list2 + i * 128);
+    else memset(list2 + i * 128, -1, 128);
+    store(s, board + i * 24, off + 2 * i, ft + 2 * i, player + i, nullptr);
+  }
+}
+
+void hc_reset_batch(int64_t n, int64_t env0, uint64_t seed, uint32_t epoch, int8_t* board,
+                    uint8_t* off, uint8_t* ft, int8_t* player, uint16_t* elapsed) {
+  for (int64_t i = 0; i < n; ++i) {
+    uint32_t r[4];
+    draw(seed, epoch, (uint32_t)(env0 + i), 1u, r);
+    store(side_reset(r[0]), board + i * 24, off + 2 * i, ft + 2 * i, player + i, elapsed + i);
+  }
+}
+
+void hc_selfplay(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int plies, int dice_mode,
+                 int max_steps, int8_t* board, uint8_t* off, uint8_t* ft, int8_t* player,
+                 uint16_t* elapsed, int32_t* stats, int8_t* obs, int8_t* reward, uint8_t* term,
+                 uint8_t* trunc, uint8_t* dice_out, int16_t* action_out, int16_t* count1_out) {
+  for (int64_t i = 0; i < n; ++i) {
+    Side s = load(board + i * 24, off + 2 * i, ft + 2 * i, player[i], elapsed[i]);
+    int4 st = make_int4(0, 0, 0, 0);
+    for (int p = 0; p < plies; ++p) {
+      uint32_t r[4];
+      draw(seed, t0 + (uint32_t)p, (uint32_t)(env0 + i), 0u, r);
+      int d0, d1;
+      dice_from(r[0], dice_mode, d0, d1);
+      StepOut o;
+      int tm, tr;
+      env_ply(s, st, r, true, d0, d1, dice_mode, true, 0, 0, max_steps, true, o, tm, tr);
+      const int64_t ix = (int64_t)p * n + i;
+      if (obs)
+        for (int q = 0; q < 24; ++q) obs[ix * 24 + q] = (int8_t)obs_point(s, q);
+      if (reward) reward[ix] = (int8_t)o.reward;
+      if (term) term[ix] = (uint8_t)tm;
+      if (trunc) trunc[ix] = (uint8_t)tr;
+      if (dice_out) { dice_out[2 * ix] = (uint8_t)d0; dice_out[2 * ix + 1] = (uint8_t)d1; }
+      if (action_out) { action_out[2 * ix] = (int16_t)o.code1; action_out[2 * ix + 1] = (int16_t)o.code2; }
+      if (count1_out) count1_out[ix] = (int16_t)o.l1.count;
+    }
+    stats[3 * i] += st.x;
+    stats[3 * i + 1] += st.y;
+    stats[3 * i + 2] += st.z;
+    store(s, board + i * 24, off + 2 * i, ft + 2 * i, player + i, elapsed + i);
+  }
+}
+
+}  // extern "C"
