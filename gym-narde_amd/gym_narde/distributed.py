@@ -1,0 +1,56 @@
+"""Multi-GPU: one process per GPU, env-id sharding, one RCCL all-gather.
+
+Envs never interact, so the batch shards with no data-path collective
+(SURVEY.md 8e): rank r of W owns global env ids [r*B/W, (r+1)*B/W).  The
+device RNG is keyed by the global env id, so any W reproduces the W=1 run
+bit for bit.  The only collective is one all_gather_into_tensor of the
+per-env statistics {episodes, white points, black points} at the end of a
+run (backend "nccl" = RCCL over xGMI on ROCm; "gloo" on CPU for tests).
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_shard(global_envs, rank, world):
+    """(first global env id, count) owned by `rank`."""
+    if global_envs % world:
+        raise ValueError(f"{global_envs} envs do not split evenly over {world} ranks")
+    per = global_envs // world
+    return rank * per, per
+
+
+def init_from_env(backend=None):
+    """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/
+    LOCAL_RANK/MASTER_*).  Returns (rank, world, local_rank)."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return rank, world, local
+
+
+def gather_stats(local_stats):
+    """All-gather (B_local, 3) int32 statistics -> (B_global, 3) on every rank,
+    ordered by global env id."""
+    if not dist.is_initialized() or dist.get_world_size() == 1:
+        return local_stats
+    world = dist.get_world_size()
+    out = torch.empty((world * local_stats.shape[0],) + tuple(local_stats.shape[1:]),
+                      dtype=local_stats.dtype, device=local_stats.device)
+    dist.all_gather_into_tensor(out, local_stats.contiguous())
+    return out
+
+
+def summarize(stats):
+    """{episodes, white_points, black_points} of a (B, 3) statistics tensor."""
+    s = stats.to(torch.int64).sum(0).tolist()
+    return {"episodes": int(s[0]), "white_points": int(s[1]), "black_points": int(s[2])}

@@ -1,0 +1,193 @@
+"""VecNardeEnv -- B Narde envs stepped in lockstep on one GPU.
+
+This is the batched hot path the scalar NardeEnv (narde_env.py:27-103 of the
+reference) is replaced by: state stays resident in HBM (32 B/env), every call
+is one stream-ordered kernel launch on the caller's current torch stream, and
+outputs land in preallocated device tensors (valid until the next call of the
+same kind -- clone them to keep them).
+
+Dice of ply t for global env e are Philox4x32-10({t, e, 0, 0}, seed), so
+`dice()` / `legal_moves()` / `legal_mask()` describe exactly the roll the next
+`step()` will use (the reference's callers peek/roll their own dice instead,
+train_deepq_pytorch.py:866).  Actions are the reference's codes
+(from*24 + to, (from<=5, to==0) = bear-off).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+DICE_MODES = {"all36": _lib.DICE_ALL36, "nodoubles": _lib.DICE_NODOUBLES}
+
+
+def decode_compact(compact):
+    """Compact legal set(s) (u64, see include/narde.h) -> list(s) of (from, to)
+    with to == 'off' for bear-off, in the reference's list order."""
+    arr = np.atleast_1d(np.asarray(compact, dtype=np.uint64))
+    out = []
+    for c in arr.tolist():
+        lh, ll = c & 0xFFFFFF, (c >> 24) & 0xFFFFFF
+        dh, dl = (c >> 48) & 0xF, (c >> 52) & 0xF
+        moves = []
+        for L, d in ((lh, dh), (ll, dl)):
+            if d == 0:
+                continue
+            for p in range(24):
+                if (L >> p) & 1:
+                    moves.append((p, "off" if p - d < 0 else p - d))
+        out.append(moves)
+    return out if np.ndim(compact) else out[0]
+
+
+class VecNardeEnv:
+    def __init__(self, num_envs, device=None, seed=0, env_id_offset=0, dice_mode="all36",
+                 max_episode_steps=1000, autoreset=True):
+        import torch
+
+        self.torch = torch
+        dev = torch.device(device if device is not None else "cuda")
+        if dev.type != "cuda":
+            raise ValueError("VecNardeEnv runs on a GPU device only")
+        if dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        self.num_envs = int(num_envs)
+        self.autoreset = bool(autoreset)
+        self.handle = _lib.Handle(dev.index, num_envs, env_id_offset, seed, DICE_MODES[dice_mode],
+                                  max_episode_steps)
+        B = self.num_envs
+        z = dict(device=dev)
+        self.obs = torch.zeros((B, 24), dtype=torch.int32, **z)
+        self.reward = torch.zeros(B, dtype=torch.int32, **z)
+        self.terminated = torch.zeros(B, dtype=torch.uint8, **z)
+        self.truncated = torch.zeros(B, dtype=torch.uint8, **z)
+        self.legal = torch.zeros(B, dtype=torch.int64, **z)
+        self.actions_used = torch.zeros((B, 2), dtype=torch.int16, **z)
+
+    # ------------------------------------------------------------ plumbing
+    def _s(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _dev(self, x, dtype, shape):
+        t = self.torch.as_tensor(x, device=self.device).to(dtype).contiguous()
+        if tuple(t.shape) != tuple(shape):
+            raise ValueError(f"expected shape {tuple(shape)}, got {tuple(t.shape)}")
+        return t
+
+    @property
+    def ply(self):
+        return self.handle.ply
+
+    @ply.setter
+    def ply(self, t):
+        self.handle.ply = t
+
+    # ------------------------------------------------------------ API
+    def reset(self, mask=None):
+        """NardeEnv.reset for all (or the masked) envs; returns obs (B,24) int32."""
+        m = None if mask is None else self._dev(mask, self.torch.uint8, (self.num_envs,))
+        self.handle.call("narde_reset", _lib.ptr(m), self._s())
+        return self.observe()
+
+    def observe(self):
+        self.handle.call("narde_observe", _lib.ptr(self.obs), None, self._s())
+        return self.obs
+
+    def tesauro198(self, out=None):
+        """README.md:42-102 198-float observation, (B,198) float32."""
+        if out is None:
+            out = self.torch.empty((self.num_envs, 198), dtype=self.torch.float32, device=self.device)
+        self.handle.call("narde_observe", None, _lib.ptr(out), self._s())
+        return out
+
+    def dice(self):
+        """Dice of the next device-RNG step, (B,2) uint8 in roll order."""
+        d = self.torch.empty((self.num_envs, 2), dtype=self.torch.uint8, device=self.device)
+        self.handle.call("narde_peek_dice", _lib.ptr(d), self._s())
+        return d
+
+    def legal_moves(self, dice=None, expanded=True):
+        """Narde.get_valid_moves per env.  dice: (B,k) k<=4 (0 = unused) or None
+        for the next step's dice.  Returns (count (B,) int16, moves (B,64,2)
+        int8 or None, compact (B,) int64 or None)."""
+        B = self.num_envs
+        d4 = None
+        if dice is not None:
+            d = self.torch.as_tensor(dice, device=self.device).to(self.torch.uint8)
+            d4 = self.torch.zeros((B, 4), dtype=self.torch.uint8, device=self.device)
+            d4[:, : d.shape[1]] = d
+        count = self.torch.empty(B, dtype=self.torch.int16, device=self.device)
+        moves = (self.torch.empty((B, _lib.MAX_MOVES, 2), dtype=self.torch.int8, device=self.device)
+                 if expanded else None)
+        # compact form is only defined for <= 2 dice (the kernel writes 0 otherwise)
+        compact = self.torch.empty(B, dtype=self.torch.int64, device=self.device)
+        self.handle.call("narde_legal_moves", _lib.ptr(d4), _lib.ptr(count), _lib.ptr(moves),
+                         _lib.ptr(compact), self._s())
+        return count, moves, compact
+
+    def legal_mask(self, out=None):
+        """(B,9) int64 = 576-bit mask of move1 codes the next step accepts."""
+        if out is None:
+            out = self.torch.empty((self.num_envs, 9), dtype=self.torch.int64, device=self.device)
+        self.handle.call("narde_legal_mask576", _lib.ptr(out), self._s())
+        return out
+
+    def step(self, actions=None, dice=None):
+        """NardeEnv.step for all envs.  actions (B,2) codes or None for the
+        in-kernel random legal policy; dice (B,2) or None for device dice.
+        Returns (obs, reward, terminated, truncated, info) device tensors;
+        info = {'legal': compact list #1, 'actions': codes used}."""
+        B = self.num_envs
+        a = None if actions is None else self._dev(actions, self.torch.int16, (B, 2))
+        d = None if dice is None else self._dev(dice, self.torch.uint8, (B, 2))
+        self.handle.call("narde_step", _lib.ptr(a), _lib.ptr(d), _lib.ptr(self.obs),
+                         _lib.ptr(self.reward), _lib.ptr(self.terminated), _lib.ptr(self.truncated),
+                         _lib.ptr(self.legal), _lib.ptr(self.actions_used), int(self.autoreset),
+                         self._s())
+        return (self.obs, self.reward, self.terminated, self.truncated,
+                {"legal": self.legal, "actions": self.actions_used})
+
+    def selfplay(self, plies):
+        """plies lockstep plies of random-legal self-play in ONE launch."""
+        self.handle.call("narde_selfplay", int(plies), self._s())
+
+    def stats(self):
+        """(B,3) int32 {episodes finished, white points, black points}."""
+        out = self.torch.empty((self.num_envs, 3), dtype=self.torch.int32, device=self.device)
+        self.handle.call("narde_get_stats", _lib.ptr(out), self._s())
+        return out
+
+    def get_state(self):
+        B, t, dev = self.num_envs, self.torch, self.device
+        st = dict(board=t.empty((B, 24), dtype=t.int8, device=dev),
+                  off=t.empty((B, 2), dtype=t.uint8, device=dev),
+                  first_turn=t.empty((B, 2), dtype=t.uint8, device=dev),
+                  player=t.empty(B, dtype=t.int8, device=dev),
+                  elapsed=t.empty(B, dtype=t.int16, device=dev))
+        self.handle.call("narde_get_state", _lib.ptr(st["board"]), _lib.ptr(st["off"]),
+                         _lib.ptr(st["first_turn"]), _lib.ptr(st["player"]), _lib.ptr(st["elapsed"]),
+                         self._s())
+        return st
+
+    def set_state(self, board, off, first_turn, player, elapsed=None):
+        B, t = self.num_envs, self.torch
+        b = self._dev(board, t.int8, (B, 24))
+        o = self._dev(off, t.uint8, (B, 2))
+        f = self._dev(first_turn, t.uint8, (B, 2))
+        p = self._dev(player, t.int8, (B,))
+        e = None if elapsed is None else self._dev(elapsed, t.int16, (B,))
+        self.handle.call("narde_set_state", _lib.ptr(b), _lib.ptr(o), _lib.ptr(f), _lib.ptr(p),
+                         _lib.ptr(e), self._s())
+        self._keep = (b, o, f, p, e)  # keep inputs alive until the kernel has read them
+
+    def apply_moves(self, moves, player=None):
+        """execute_rotated_move per env; moves (B,2) int8 (to=24 for off, from<0 skips)."""
+        B, t = self.num_envs, self.torch
+        m = self._dev(moves, t.int8, (B, 2))
+        p = None if player is None else self._dev(player, t.int8, (B,))
+        self.handle.call("narde_apply_moves", _lib.ptr(m), _lib.ptr(p), self._s())
+        self._keep = (m, p)
+
+    def close(self):
+        self.handle.close()

@@ -1,0 +1,118 @@
+"""GPU: the scalar drop-in facade (gym_narde.envs) reproduces the reference.
+
+Episodes in episodes.npz were recorded from the reference NardeEnv with
+reset(seed=s) and a seeded random legal policy; the facade draws its dice
+from numpy's global legacy RNG exactly like the reference, so replaying the
+recorded actions after reset(seed=s) must reproduce every observation,
+reward, termination and mover."""
+import numpy as np
+import pytest
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _moves(row, count):
+    return [(int(f), "off" if t == 24 else int(t)) for f, t in row[:count]]
+
+
+def test_episodes_replay_bit_exact():
+    from gym_narde.envs import NardeEnv
+
+    d = golden("episodes.npz")
+    pos = 0
+    for e, (seed, length) in enumerate(zip(d["seed"], d["length"])):
+        env = NardeEnv()
+        obs, info = env.reset(seed=int(seed))
+        assert np.array_equal(obs, d["reset_obs"][e].astype(np.int32))
+        assert env.current_player == d["reset_player"][e]
+        for k in range(int(length)):
+            st = np.random.get_state()
+            dice = [np.random.randint(1, 7), np.random.randint(1, 7)]
+            np.random.set_state(st)
+            assert dice == d["dice"][pos].tolist(), (e, k)
+            obs, r, term, trunc, _ = env.step(tuple(int(x) for x in d["action"][pos]))
+            assert np.array_equal(obs, d["obs"][pos].astype(np.int32)), (e, k)
+            assert (r, term, trunc) == (int(d["reward"][pos]), bool(d["terminated"][pos]), False)
+            assert env.current_player == d["player"][pos], (e, k)
+            pos += 1
+        assert term or length == 1000
+    assert pos == len(d["action"])
+
+
+def test_reset_draw_pattern():
+    from gym_narde.envs import NardeEnv
+
+    d = golden("resets.npz")
+    env = NardeEnv()
+    for s, pl, nxt in zip(d["seed"], d["player"], d["next_draw"]):
+        env.reset(seed=int(s))
+        assert env.current_player == pl
+        assert np.random.randint(0, 2 ** 31 - 1) == nxt  # same number of RNG draws
+
+
+def test_get_valid_moves_sample_incl_3_and_4_dice():
+    from gym_narde.envs.narde import Narde
+
+    d = golden("legal.npz")
+    g = Narde()
+    idx = list(range(int(d["n_kat"])))
+    idx += list(np.random.RandomState(2).choice(len(d["count"]), 1500, replace=False))
+    idx += list(np.nonzero(d["nroll"] >= 3)[0][:300])
+    for i in idx:
+        g.board = d["board"][i].astype(np.int32)
+        g.borne_off_white, g.borne_off_black = int(d["off"][i][0]), int(d["off"][i][1])
+        g.first_turn_white, g.first_turn_black = bool(d["first_turn"][i][0]), bool(d["first_turn"][i][1])
+        roll = [int(x) for x in d["roll"][i][: d["nroll"][i]]]
+        assert g.get_valid_moves(roll, int(d["player"][i])) == _moves(d["moves"][i], d["count"][i]), i
+
+
+def test_reference_unit_tests_equivalent():
+    """tests/test_move_validation.py:13-29 of the reference."""
+    from gym_narde.envs.narde import Narde
+
+    g = Narde()
+    valid = g.get_valid_moves([3, 5], current_player=1)
+    assert len(valid) > 0
+    assert g.validate_move(valid[0], [3, 5], current_player=1)
+    assert not g.validate_move((23, 20), [3, 5], current_player=1)  # smaller die's head move
+
+
+def test_execute_rotated_move_and_block_rule():
+    from gym_narde.envs.narde import Narde
+
+    d = golden("apply.npz")
+    g = Narde()
+    for i in range(0, len(d["player"]), 37):
+        g.board = d["board"][i].astype(np.int32)
+        g.borne_off_white, g.borne_off_black = int(d["off"][i][0]), int(d["off"][i][1])
+        g.first_turn_white, g.first_turn_black = bool(d["first_turn"][i][0]), bool(d["first_turn"][i][1])
+        f, t = int(d["move"][i][0]), int(d["move"][i][1])
+        g.execute_rotated_move((f, "off" if t == 24 else t), int(d["player"][i]))
+        assert np.array_equal(g.board, d["post_board"][i].astype(np.int32)), i
+        assert (g.borne_off_white, g.borne_off_black) == tuple(d["post_off"][i])
+        assert (g.first_turn_white, g.first_turn_black) == tuple(bool(x) for x in d["post_first_turn"][i])
+    b = golden("block.npz")
+    for i in range(0, len(b["violates"]), 53):
+        assert g._violates_block_rule(b["board"][i].astype(np.int32)) == bool(b["violates"][i])
+
+
+def test_make_timelimit_truncates_at_1000():
+    import gym_narde
+
+    env = gym_narde.make("gym_narde:narde-v0")
+    env.reset(seed=0)
+    trunc = False
+    for k in range(1000):
+        _, _, term, trunc, _ = env.step((0, 0))  # (0,'off') is never legal early: no move
+        if term:
+            break
+    assert trunc and k == 999

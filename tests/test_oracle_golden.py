@@ -1,0 +1,207 @@
+"""Pin the CPU oracle (and the Python port) to the reference's golden vectors.
+
+The fixtures in tests/golden/ were produced by tools/capture_golden.py, which
+imports the reference from /root/reference and drives it with injected dice.
+Also diffs the test-only host build of the device rules engine
+(tests/hostcheck) against the same fixtures and against the oracle's
+self-play -- a CPU pre-check of the bitmask formulation; the GPU parity tests
+are in test_gpu_parity.py.
+"""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+from conftest import golden
+
+import oracle as O
+import narde_port as port
+
+P = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a is not None else None  # noqa: E731
+
+
+def test_philox_known_answers():
+    # Random123 kat_vectors for philox4x32_10
+    assert O.philox((0, 0, 0, 0), (0, 0)) == (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)
+    assert O.philox((0xFFFFFFFF,) * 4, (0xFFFFFFFF,) * 2) == (
+        0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)
+    assert O.philox((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0)) == (
+        0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)
+
+
+def test_oracle_legal_moves_golden():
+    d = golden("legal.npz")
+    m, c = O.legal_moves(d["board"], d["first_turn"], d["player"], d["roll"], d["nroll"])
+    assert np.array_equal(c, d["count"])
+    assert np.array_equal(m, d["moves"])
+
+
+def test_oracle_known_answers_appendix_b():
+    d = golden("legal.npz")
+    k = int(d["n_kat"])
+    lists = [[tuple(x) for x in d["moves"][i][: d["count"][i]].tolist()] for i in range(k)]
+    assert lists[0] == [(23, 18)]                       # start, [5,3]
+    assert lists[2] == [(23, 17), (23, 17)]             # start, [6,6] first turn: 2 head moves
+    assert lists[5] == [(23, 18)]                       # [5,5] is not a head-exception double
+    assert lists[7] == [(23, 18)]                       # 4-die roll: never special
+    assert lists[11] == [(0, 24), (2, 24), (3, 0), (0, 24), (2, 1), (3, 2)]
+    assert lists[13] == [(3, 0), (4, 1), (6, 3), (23, 20), (1, 0), (2, 1), (3, 2), (4, 3)]
+
+
+def test_oracle_block_rule_golden():
+    d = golden("block.npz")
+    assert np.array_equal(O.violates_block_rule(d["board"]), d["violates"])
+    assert 0.05 < d["violates"].mean() < 0.95  # both outcomes covered
+
+
+def test_oracle_apply_golden():
+    d = golden("apply.npz")
+    b, o, f = O.apply_move(d["board"], d["off"], d["first_turn"], d["player"], d["move"])
+    assert np.array_equal(b, d["post_board"])
+    assert np.array_equal(o, d["post_off"])
+    assert np.array_equal(f, d["post_first_turn"])
+
+
+def test_oracle_step_golden():
+    s = golden("steps.npz")
+    r = O.step(s["board"], s["off"], s["first_turn"], s["player"], s["dice"], s["action"])
+    for mine, ref in [("board", "post_board"), ("off", "post_off"), ("first_turn", "post_first_turn"),
+                      ("player", "post_player"), ("obs", "obs"), ("reward", "reward"),
+                      ("terminated", "terminated"), ("count1", "count1"), ("list1", "list1"),
+                      ("count2", "count2"), ("list2", "list2")]:
+        assert np.array_equal(r[mine], s[ref]), mine
+    made = s["count2"] >= 0
+    assert np.array_equal(r["roll2"][made], s["roll2"][made])
+    # coverage of the branches the fixtures must exercise
+    assert (s["count1"] == 0).any() and (s["count1"] == 1).any() and (s["count1"] >= 2).any()
+    assert (s["terminated"] == 1).sum() > 50 and (s["reward"] == 2).any()
+    assert (s["ncalls"] == 2).any()
+
+
+def _port_state(b, off, ft, pl):
+    e = port.PortEnv()
+    g = e.game
+    g.board = b.astype(np.int32).copy()
+    g.borne_off_white, g.borne_off_black = int(off[0]), int(off[1])
+    g.first_turn_white, g.first_turn_black = bool(ft[0]), bool(ft[1])
+    e.current_player = int(pl)
+    return e
+
+
+def test_port_step_golden_sample():
+    s = golden("steps.npz")
+    idx = np.random.RandomState(0).choice(len(s["dice"]), 3000, replace=False)
+    idx = np.concatenate([idx, np.arange(len(s["dice"]) - 4, len(s["dice"]))])  # quirk rows
+    for i in idx:
+        e = _port_state(s["board"][i], s["off"][i], s["first_turn"][i], s["player"][i])
+        obs, rew, done = e.step([int(x) for x in s["dice"][i]], [int(x) for x in s["action"][i]])
+        assert np.array_equal(e.game.board, s["post_board"][i].astype(np.int32)), i
+        assert (e.game.borne_off_white, e.game.borne_off_black) == tuple(s["post_off"][i]), i
+        assert e.current_player == s["post_player"][i], i
+        assert np.array_equal(obs, s["obs"][i].astype(np.int32)), i
+        assert (rew, done) == (s["reward"][i], bool(s["terminated"][i])), i
+
+
+def test_port_legal_golden_sample():
+    d = golden("legal.npz")
+    idx = np.random.RandomState(1).choice(len(d["count"]), 3000, replace=False)
+    g = port.PortNarde()
+    for i in idx:
+        g.board = d["board"][i].astype(np.int32)
+        g.first_turn_white, g.first_turn_black = bool(d["first_turn"][i][0]), bool(d["first_turn"][i][1])
+        roll = [int(x) for x in d["roll"][i][: d["nroll"][i]]]
+        mv = g.get_valid_moves(roll, int(d["player"][i]))
+        ref = [(int(f), "off" if t == 24 else int(t)) for f, t in d["moves"][i][: d["count"][i]]]
+        assert mv == ref, i
+
+
+def test_port_selfplay_runs():
+    steps, secs, eps = port.selfplay_port(8, plies=300, seed=3)
+    assert steps == 2400 and eps > 0
+
+
+# ---------------------------------------------------------------- hostcheck
+def test_hostcheck_legal_golden(hostcheck):
+    d = golden("legal.npz")
+    n = len(d["count"])
+    moves = np.empty((n, 64, 2), np.int8)
+    cnt = np.empty(n, np.int16)
+    hostcheck.hc_legal_batch(ctypes.c_int64(n), P(d["board"]), P(d["off"]), P(d["first_turn"]),
+                             P(d["player"]), P(np.ascontiguousarray(d["roll"])), P(moves), P(cnt))
+    assert np.array_equal(cnt, d["count"])
+    assert np.array_equal(moves, d["moves"])
+
+
+def test_hostcheck_step_golden(hostcheck):
+    s = golden("steps.npz")
+    n = len(s["dice"])
+    b, off, ft, pl = (s["board"].copy(), s["off"].copy(), s["first_turn"].copy(), s["player"].copy())
+    obs = np.empty((n, 24), np.int8)
+    rw = np.empty(n, np.int8)
+    tm = np.empty(n, np.uint8)
+    l1 = np.empty((n, 64, 2), np.int8)
+    c1 = np.empty(n, np.int16)
+    l2 = np.empty((n, 64, 2), np.int8)
+    c2 = np.empty(n, np.int16)
+    hostcheck.hc_step_batch(ctypes.c_int64(n), P(b), P(off), P(ft), P(pl), P(s["dice"]), P(s["action"]),
+                            P(obs), P(rw), P(tm), P(l1), P(c1), P(l2), P(c2))
+    for a, ref in [(b, "post_board"), (off, "post_off"), (ft, "post_first_turn"), (pl, "post_player"),
+                   (obs, "obs"), (rw, "reward"), (tm, "terminated"), (c1, "count1"), (l1, "list1"),
+                   (c2, "count2"), (l2, "list2")]:
+        assert np.array_equal(a, s[ref]), ref
+
+
+@pytest.mark.parametrize("dice_mode", [0, 1])
+def test_hostcheck_selfplay_vs_oracle(hostcheck, dice_mode):
+    n, plies, seed, env0 = 512, 400, 0xDEADBEEF12345, 1000
+    sp = O.SelfPlay(n, seed=seed, env0=env0, dice_mode=dice_mode, max_steps=1000)
+    sp.reset(0)
+    ro = sp.run(plies)
+    b = np.zeros((n, 24), np.int8)
+    off = np.zeros((n, 2), np.uint8)
+    ft = np.zeros((n, 2), np.uint8)
+    pl = np.zeros(n, np.int8)
+    el = np.zeros(n, np.uint16)
+    st = np.zeros((n, 3), np.int32)
+    hostcheck.hc_reset_batch(ctypes.c_int64(n), ctypes.c_int64(env0), ctypes.c_uint64(seed),
+                             ctypes.c_uint32(0), P(b), P(off), P(ft), P(pl), P(el))
+    out = {k: np.empty_like(v) for k, v in ro.items()}
+    hostcheck.hc_selfplay(ctypes.c_int64(n), ctypes.c_int64(env0), ctypes.c_uint64(seed),
+                          ctypes.c_uint32(0), ctypes.c_int(plies), ctypes.c_int(dice_mode),
+                          ctypes.c_int(1000), P(b), P(off), P(ft), P(pl), P(el), P(st),
+                          P(out["obs"]), P(out["reward"]), P(out["terminated"]), P(out["truncated"]),
+                          P(out["dice"]), P(out["action"]), P(out["count1"]))
+    for k in ro:
+        assert np.array_equal(out[k], ro[k]), k
+    assert np.array_equal(st, sp.stats) and np.array_equal(b, sp.board)
+    assert sp.stats[:, 0].sum() > 0
+
+
+def test_oracle_selfplay_invariants():
+    n = 256
+    sp = O.SelfPlay(n, seed=7, max_steps=130)  # short TimeLimit -> truncations too
+    sp.reset(0)
+    r = sp.run(300)
+    assert r["truncated"].any() and r["terminated"].any()
+    # checker conservation: 15 per colour on board + off, no mixed points
+    w = np.where(sp.board > 0, sp.board, 0).sum(1) + sp.off[:, 0]
+    k = np.where(sp.board < 0, -sp.board, 0).sum(1) + sp.off[:, 1]
+    assert (w == 15).all() and (k == 15).all()
+    # codes used are legal action codes or 0
+    assert ((r["action"] >= 0) & (r["action"] < 576)).all()
+
+
+def test_oracle_tesauro_bounds():
+    d = golden("steps.npz")
+    t = O.tesauro198(d["post_board"], d["post_off"], d["post_player"])
+    hi = np.ones(198, np.float32)
+    hi[[3 + 4 * p for p in range(24)]] = 6.0
+    hi[[101 + 4 * p for p in range(24)]] = 6.0
+    hi[96] = hi[194] = 7.5
+    assert (t >= 0).all() and (t <= hi).all()  # tests/test_observation_space.py:37-234 bounds
+    assert np.allclose(t[:, 196] + t[:, 197], 1.0)
+    # white block decodes back to the board
+    w = t[:, 0:96].reshape(-1, 24, 4)
+    cnt = w[..., 0] + w[..., 1] + w[..., 2] + 2 * w[..., 3]
+    assert np.array_equal(cnt.astype(np.int64), np.where(d["post_board"] > 0, d["post_board"], 0))
+    random.seed(0)
