@@ -2,16 +2,20 @@
 """Benchmark: env steps/s of batched random-policy Narde self-play.
 
 Workload (BASELINE.json metric, configs[2] at N=1): 65,536 envs per GPU in
-lockstep; one bench step = one ply of NardeEnv.step over every env (device
+lockstep.  One bench step = one ply of NardeEnv.step over every env: device
 dice uniform over the 36 ordered pairs, list #1, in-kernel random legal
 policy, the reference's action decode and die bookkeeping, list #2, end
-check, flip, TimeLimit 1000, auto-reset) writing every per-env output
-(int32[24] obs, reward, terminated, truncated, compact legal set, actions) --
-one k_step launch per step.  N GPUs = N processes (torchrun), each owning a
-contiguous shard of global env ids (weak scaling); the timed region ends with
-the RCCL all-gather of per-env episode statistics.
+check, flip, TimeLimit 1000, auto-reset -- and every per-env output of the
+ply written to HBM (int32[24] obs, reward, terminated, truncated, compact
+legal set, actions).  The timed path is k_rollout: P plies per launch with
+the env record in VGPRs, each ply's outputs streamed to [P][B] rollout
+buffers (K steps = ceil(K/P) launches).  The per-ply API kernel k_step is
+measured beside it (eager and hipGraph-replayed).  N GPUs = N processes
+(torchrun), each owning a contiguous shard of global env ids (weak
+scaling); the timed region ends with the RCCL all-gather of per-env episode
+statistics.
 
-Prints ONE JSON line on rank 0 (see README/DESIGN.md for the fields).
+Prints ONE JSON line on rank 0 (fields: DESIGN.md section 6).
 """
 import argparse
 import json
@@ -25,11 +29,15 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 METRIC = "env steps/sec at batch=65536, 1 MI355X (+ legal-move bit-exact vs CPU)"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-# algorithmic bytes per env-step of k_step:
-# record read 32 + write 32, obs 96, reward 4, terminated 1, truncated 1,
-# compact legal set 8, actions 4
-BYTES_PER_STEP = 178
-BYTES_PER_STEP_FUSED_STATE = 64  # per env per fused launch (record r+w), amortised over plies
+# algorithmic bytes: per env and ply the outputs
+# obs 96 + reward 4 + terminated 1 + truncated 1 + compact legal set 8 +
+# actions 4 = 114 B; per env and launch the 32-B record read + written = 64 B
+OUT_BYTES_PER_STEP = 114
+RECORD_BYTES = 64
+
+
+def launch_bytes(envs, plies):
+    return envs * (OUT_BYTES_PER_STEP * plies + RECORD_BYTES)
 
 
 def _port_worker(args):
@@ -80,12 +88,14 @@ def cpu_baseline(seconds, cores):
     }
 
 
-def load_traffic(path, envs):
+def load_traffic(path, envs, plies):
+    """HBM bytes per k_rollout launch from the committed rocprofv3 PMC
+    summary (tools/pmc_summary.py), if it was measured at this shape."""
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
         return None
-    if d.get("envs") != envs:
+    if d.get("envs") != envs or d.get("plies") != plies:
         return None
     return d.get("hbm_bytes_per_launch")
 
@@ -93,16 +103,18 @@ def load_traffic(path, envs):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=10000)
+    ap.add_argument("--warmup", type=int, default=1000)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--plies-per-launch", type=int, default=100)
+    ap.add_argument("--api-steps", type=int, default=200)
     ap.add_argument("--fused-plies", type=int, default=100)
     ap.add_argument("--fused-launches", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--cpu-cores", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_k_step.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_k_rollout.json"))
     args = ap.parse_args()
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -127,25 +139,39 @@ def main():
         if world > 1:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        env.step()
+    P = max(1, min(args.plies_per_launch, args.steps))
+    bufs = env.rollout_buffers(P)
+
+    def run_plies(k, events=None):
+        done = 0
+        while done < k:
+            p = min(P, k - done)
+            if events is not None:
+                s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s_.record()
+                env.rollout(p, bufs)
+                e_.record()
+                events.append((s_, e_, p))
+            else:
+                env.rollout(p, bufs)
+            done += p
+
+    run_plies(args.warmup)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
 
     K = args.steps
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    events = []
     t0 = time.perf_counter()
-    for i in range(K):
-        ev[i][0].record()
-        env.step()
-        ev[i][1].record()
+    run_plies(K, events)
     stats = D.gather_stats(env.stats())
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(s.elapsed_time(e) for s, e in ev) / K
+    full = [(s_, e_) for s_, e_, p in events if p == P]
+    kern_ms = sum(s_.elapsed_time(e_) for s_, e_ in full) / max(1, len(full))
 
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -155,29 +181,54 @@ def main():
     value = total_steps / elapsed
     summary = D.summarize(stats)
 
-    # secondary: fused self-play (K plies per launch, state in VGPRs, no per-ply outputs)
-    P, L = args.fused_plies, args.fused_launches
-    env.selfplay(P)
+    # secondary 1: per-ply API kernel k_step (eager, then hipGraph replay)
+    S = args.api_steps
+    for _ in range(10):
+        env.step()
     torch.cuda.synchronize()
-    barrier()
-    fe = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(L)]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(S)]
+    a0 = time.perf_counter()
+    for i in range(S):
+        ev[i][0].record()
+        env.step()
+        ev[i][1].record()
+    torch.cuda.synchronize()
+    api_eager = per * S / (time.perf_counter() - a0)
+    step_ms = sum(x.elapsed_time(y) for x, y in ev) / S
+    G = 50
+    graph = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream()
+    cap.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(cap):
+        env.step()  # warm the capture stream
+        torch.cuda.synchronize()
+        with torch.cuda.graph(graph, stream=cap):
+            for _ in range(G):
+                env.step()
+    torch.cuda.current_stream().wait_stream(cap)
+    graph.replay()
+    torch.cuda.synchronize()
+    reps = max(1, S // G)
+    g0 = time.perf_counter()
+    for _ in range(reps):
+        graph.replay()
+    torch.cuda.synchronize()
+    api_graph = per * G * reps / (time.perf_counter() - g0)
+
+    # secondary 2: fused self-play with no per-ply outputs (statistics only)
+    F = args.fused_plies
+    env.selfplay(F)
+    torch.cuda.synchronize()
     f0 = time.perf_counter()
-    for i in range(L):
-        fe[i][0].record()
-        env.selfplay(P)
-        fe[i][1].record()
+    for _ in range(args.fused_launches):
+        env.selfplay(F)
     torch.cuda.synchronize()
-    barrier()
-    f_elapsed = time.perf_counter() - f0
-    f_kern_ms = sum(s.elapsed_time(e) for s, e in fe) / L
-    ft = torch.tensor([f_elapsed, f_kern_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(ft, op=dist.ReduceOp.MAX)
-    f_elapsed, f_kern_ms = float(ft[0]), float(ft[1])
+    fused = per * F * args.fused_launches / (time.perf_counter() - f0)
 
     if rank == 0:
-        achieved = BYTES_PER_STEP * per / (kern_ms * 1e-3) / 1e9
-        traffic = load_traffic(args.traffic_json, per)
+        nbytes = launch_bytes(per, P)
+        achieved = nbytes / (kern_ms * 1e-3) / 1e9
+        traffic = load_traffic(args.traffic_json, per, P)
         line = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -185,7 +236,7 @@ def main():
             "n_gpus": world,
             "steps": K,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / K * 1e3, 5),
+            "ms_per_step": round(elapsed / K * 1e3, 6),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -194,9 +245,10 @@ def main():
             "config": {
                 "workload": ("configs[2]: batch=65536 random-policy self-play per GPU; rules = "
                              "reference NardeEnv.step (REF2: <=2 checker moves per step, also on "
-                             "doubles); dice uniform over 36 ordered pairs; TimeLimit 1000; one "
-                             "k_step launch per ply writing obs/reward/terminated/truncated/"
-                             "legal set/actions for every env"),
+                             "doubles); dice uniform over 36 ordered pairs; TimeLimit 1000; every "
+                             "ply writes obs/reward/terminated/truncated/legal set/actions for "
+                             "every env"),
+                "kernel": f"k_rollout, {P} plies per launch",
                 "envs_per_gpu": per,
                 "global_envs": world * per,
                 "parallelism": f"dp{world} (env-id shards, 1 RCCL all-gather of stats)",
@@ -204,23 +256,28 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_step",
+                "kernel": "k_rollout",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
-                "bytes_per_env_step": BYTES_PER_STEP,
+                "bytes_per_launch": nbytes,
                 "kernel_ms": round(kern_ms, 5),
             },
             "cpu_baseline": cpu,
-            "fused_selfplay": {
-                "value": round(world * per * P * L / f_elapsed, 1),
+            "api_step": {
+                "kernel": "k_step (one ply per launch, same outputs)",
+                "eager": round(api_eager, 1),
+                "hipgraph": round(api_graph, 1),
                 "unit": "env steps/s",
-                "plies_per_launch": P,
-                "kernel": "k_selfplay",
-                "kernel_ms": round(f_kern_ms, 5),
-                "outputs": "per-env statistics only",
+                "kernel_ms": round(step_ms, 5),
+                "achieved_GBps": round((OUT_BYTES_PER_STEP + RECORD_BYTES) * per / (step_ms * 1e-3) / 1e9, 2),
+            },
+            "selfplay_stats_only": {
+                "kernel": f"k_rollout without per-ply outputs, {F} plies per launch",
+                "value": round(fused, 1),
+                "unit": "env steps/s",
             },
         }
         print(json.dumps(line), flush=True)

@@ -10,7 +10,8 @@
 //   k_step      NardeEnv.step for B envs (API step and the self-play ply):
 //               Philox dice, list #1, policy or given actions, apply, list #2,
 //               apply, end check, flip, TimeLimit, auto-reset, outputs.
-//   k_selfplay  the same step looped over K plies with the record in VGPRs.
+//   k_rollout   the same step looped over K plies with the record in VGPRs,
+//               streaming each ply's outputs to [ply][B] rollout buffers.
 //   k_legal     Narde.get_valid_moves with 1..4 dice, expanded or compact.
 //   k_reset / k_set_state / k_get_state / k_apply / k_observe / k_mask576 /
 //   k_block / k_peek_dice   state management and the rest of the ABI.
@@ -64,14 +65,16 @@ __device__ __forceinline__ void draw(const Rng& g, uint32_t t, uint32_t i, uint3
 }
 
 // ------------------------------------------------------------------ kernels
+// init_t >= 0: also set the RNG counter (create); < 0: keep each env's counter
 __global__ void __launch_bounds__(kBlock) k_reset(Planes pl, int n, Rng g, uint32_t epoch,
-                                                  const uint8_t* __restrict__ mask) {
+                                                  const uint8_t* __restrict__ mask, int64_t init_t) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   if (mask && !mask[i]) return;
   uint32_t r[4];
   draw(g, epoch, (uint32_t)i, 1u, r);
   Side s = side_reset(r[0]);
+  s.t = init_t >= 0 ? (uint32_t)init_t : pl.p1[i].w;
   uint4 a, b;
   side_to_record(s, a, b);
   pl.p0[i] = a;
@@ -79,16 +82,18 @@ __global__ void __launch_bounds__(kBlock) k_reset(Planes pl, int n, Rng g, uint3
   pl.stats[i] = make_int4(0, 0, 0, 0);
 }
 
+// keep_t: preserve each env's RNG counter (device state); else set it to 0
 __global__ void __launch_bounds__(kBlock) k_set_state(Planes pl, int n, const int8_t* __restrict__ board,
                                                       const uint8_t* __restrict__ off,
                                                       const uint8_t* __restrict__ ft,
                                                       const int8_t* __restrict__ player,
-                                                      const uint16_t* __restrict__ elapsed) {
+                                                      const uint16_t* __restrict__ elapsed, int keep_t) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
+  const uint32_t t = keep_t ? pl.p1[i].w : 0u;
   uint4 a, b;
   record_from_board(board + (size_t)i * 24, off[2 * i], off[2 * i + 1], ft[2 * i], ft[2 * i + 1],
-                    player[i], elapsed ? elapsed[i] : 0u, a, b);
+                    player[i], elapsed ? elapsed[i] : 0u, t, a, b);
   pl.p0[i] = a;
   pl.p1[i] = b;
 }
@@ -104,11 +109,17 @@ __global__ void __launch_bounds__(kBlock) k_get_state(Planes pl, int n, int8_t* 
                     player ? player + i : nullptr, elapsed ? elapsed + i : nullptr);
 }
 
-__global__ void __launch_bounds__(kBlock) k_peek_dice(int n, Rng g, uint32_t t, uint8_t* __restrict__ dice) {
+__global__ void __launch_bounds__(kBlock) k_set_ply(Planes pl, int n, uint32_t t) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  pl.p1[i].w = t;
+}
+
+__global__ void __launch_bounds__(kBlock) k_peek_dice(Planes pl, int n, Rng g, uint8_t* __restrict__ dice) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   uint32_t r[4];
-  draw(g, t, (uint32_t)i, 0u, r);
+  draw(g, pl.p1[i].w, (uint32_t)i, 0u, r);
   int d0, d1;
   dice_from(r[0], g.dice_mode, d0, d1);
   dice[2 * i] = (uint8_t)d0;
@@ -120,7 +131,7 @@ __device__ __forceinline__ uint64_t compact_legal(const Legal& l) {
          ((uint64_t)l.d[1] << 52);
 }
 
-__global__ void __launch_bounds__(kBlock) k_legal(Planes pl, int n, Rng g, uint32_t t,
+__global__ void __launch_bounds__(kBlock) k_legal(Planes pl, int n, Rng g,
                                                   const uint8_t* __restrict__ dice4,
                                                   int16_t* __restrict__ out_count,
                                                   int8_t* __restrict__ out_moves,
@@ -133,7 +144,7 @@ __global__ void __launch_bounds__(kBlock) k_legal(Planes pl, int n, Rng g, uint3
     legal_roll(s, dice4 + 4 * i, l);
   } else {
     uint32_t r[4];
-    draw(g, t, (uint32_t)i, 0u, r);
+    draw(g, s.t, (uint32_t)i, 0u, r);
     int d0, d1;
     dice_from(r[0], g.dice_mode, d0, d1);
     legal2(s, d0, d1, l);
@@ -160,37 +171,54 @@ __global__ void __launch_bounds__(kBlock) k_legal(Planes pl, int n, Rng g, uint3
   }
 }
 
+// per-ply outputs; a rollout writes ply p of env i at [p * n + i]
+struct Outs {
+  int32_t* __restrict__ obs;      // [.][n][24]
+  int32_t* __restrict__ reward;   // [.][n]
+  uint8_t* __restrict__ term;     // [.][n]
+  uint8_t* __restrict__ trunc;    // [.][n]
+  uint64_t* __restrict__ legal;   // [.][n] compact list #1
+  int16_t* __restrict__ act_out;  // [.][n][2]
+};
+
 struct StepArgs {
   Planes pl;
   int n;
   Rng g;
-  uint32_t t;
   int max_steps;
   int autoreset;
   const int16_t* __restrict__ actions;
   const uint8_t* __restrict__ dice;
-  int32_t* __restrict__ obs;
-  int32_t* __restrict__ reward;
-  uint8_t* __restrict__ term;
-  uint8_t* __restrict__ trunc;
-  uint64_t* __restrict__ legal;
-  int16_t* __restrict__ act_out;
+  Outs out;
 };
 
-__device__ __forceinline__ void store_obs(int32_t* __restrict__ obs, int i, const Side& s) {
-  int4* o = reinterpret_cast<int4*>(obs + (size_t)i * 24);
+__device__ __forceinline__ void store_obs(int32_t* __restrict__ obs, size_t ix, const Side& s) {
+  int4* o = reinterpret_cast<int4*>(obs + ix * 24);
 #pragma unroll
   for (int q = 0; q < 6; ++q)
     o[q] = make_int4(obs_point(s, 4 * q), obs_point(s, 4 * q + 1), obs_point(s, 4 * q + 2),
                      obs_point(s, 4 * q + 3));
 }
 
-// one ply for env i: draw, then the shared host/device ply (narde_rules.h)
-__device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t t, uint32_t i,
+__device__ __forceinline__ void store_outs(const Outs& out, size_t ix, const Side& s,
+                                           const StepOut& o, int term, int trunc) {
+  if (out.obs) store_obs(out.obs, ix, s);
+  if (out.reward) out.reward[ix] = o.reward;
+  if (out.term) out.term[ix] = (uint8_t)term;
+  if (out.trunc) out.trunc[ix] = (uint8_t)trunc;
+  if (out.legal) out.legal[ix] = compact_legal(o.l1);
+  if (out.act_out)
+    reinterpret_cast<uint32_t*>(out.act_out)[ix] =
+        ((uint32_t)(uint16_t)o.code1) | ((uint32_t)(uint16_t)o.code2 << 16);
+}
+
+// one ply for env i: draw with the env's own counter, then the shared
+// host/device ply (narde_rules.h)
+__device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t i,
                                     const int16_t* actions, const uint8_t* dice, int max_steps,
                                     bool autoreset, StepOut& o, int& term, int& trunc) {
   uint32_t r[4];
-  draw(g, t, i, 0u, r);
+  draw(g, s.t, i, 0u, r);
   int d0 = 0, d1 = 0, c1 = 0, c2 = 0;
   if (dice) { d0 = dice[2 * i]; d1 = dice[2 * i + 1]; }
   if (actions) { c1 = actions[2 * i]; c2 = actions[2 * i + 1]; }
@@ -198,6 +226,15 @@ __device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t t,
           autoreset, o, term, trunc);
 }
 
+__device__ __forceinline__ void add_stats(int4* __restrict__ stats, int i, const int4& st) {
+  if (st.x) {
+    int4 cur = stats[i];
+    cur.x += st.x; cur.y += st.y; cur.z += st.z;
+    stats[i] = cur;
+  }
+}
+
+// NardeEnv.step for every env (API step; one ply of self-play when actions == NULL)
 __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= a.n) return;
@@ -205,30 +242,20 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
   int4 st = make_int4(0, 0, 0, 0);
   StepOut o;
   int term, trunc;
-  ply(s, st, a.g, a.t, (uint32_t)i, a.actions, a.dice, a.max_steps, a.autoreset != 0, o, term,
-      trunc);
+  ply(s, st, a.g, (uint32_t)i, a.actions, a.dice, a.max_steps, a.autoreset != 0, o, term, trunc);
   uint4 ra, rb;
   side_to_record(s, ra, rb);
   a.pl.p0[i] = ra;
   a.pl.p1[i] = rb;
-  if (st.x) {
-    int4 cur = a.pl.stats[i];
-    cur.x += st.x; cur.y += st.y; cur.z += st.z;
-    a.pl.stats[i] = cur;
-  }
-  if (a.obs) store_obs(a.obs, i, s);
-  if (a.reward) a.reward[i] = o.reward;
-  if (a.term) a.term[i] = (uint8_t)term;
-  if (a.trunc) a.trunc[i] = (uint8_t)trunc;
-  if (a.legal) a.legal[i] = compact_legal(o.l1);
-  if (a.act_out) {
-    a.act_out[2 * i] = (int16_t)o.code1;
-    a.act_out[2 * i + 1] = (int16_t)o.code2;
-  }
+  add_stats(a.pl.stats, i, st);
+  store_outs(a.out, (size_t)i, s, o, term, trunc);
 }
 
-__global__ void __launch_bounds__(kBlock) k_selfplay(Planes pl, int n, Rng g, uint32_t t0, int plies,
-                                                     int max_steps) {
+// `plies` plies of random-legal self-play with auto-reset in one launch; the
+// record stays in VGPRs, each ply's outputs (if requested) are streamed to
+// [ply][n] rollout buffers.
+__global__ void __launch_bounds__(kBlock) k_rollout(Planes pl, int n, Rng g, int plies, int max_steps,
+                                                    Outs out) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   Side s = side_from_record(pl.p0[i], pl.p1[i]);
@@ -236,18 +263,14 @@ __global__ void __launch_bounds__(kBlock) k_selfplay(Planes pl, int n, Rng g, ui
   for (int p = 0; p < plies; ++p) {
     StepOut o;
     int term, trunc;
-    ply(s, st, g, t0 + (uint32_t)p, (uint32_t)i, nullptr, nullptr, max_steps, true, o, term,
-        trunc);
+    ply(s, st, g, (uint32_t)i, nullptr, nullptr, max_steps, true, o, term, trunc);
+    store_outs(out, (size_t)p * n + i, s, o, term, trunc);
   }
   uint4 ra, rb;
   side_to_record(s, ra, rb);
   pl.p0[i] = ra;
   pl.p1[i] = rb;
-  if (st.x) {
-    int4 cur = pl.stats[i];
-    cur.x += st.x; cur.y += st.y; cur.z += st.z;
-    pl.stats[i] = cur;
-  }
+  add_stats(pl.stats, i, st);
 }
 
 __global__ void __launch_bounds__(kBlock) k_get_stats(Planes pl, int n, int32_t* __restrict__ out) {
@@ -308,13 +331,13 @@ __global__ void __launch_bounds__(kBlock) k_observe(Planes pl, int n, int32_t* _
   }
 }
 
-__global__ void __launch_bounds__(kBlock) k_mask576(Planes pl, int n, Rng g, uint32_t t,
+__global__ void __launch_bounds__(kBlock) k_mask576(Planes pl, int n, Rng g,
                                                     uint64_t* __restrict__ mask) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const Side s = side_from_record(pl.p0[i], pl.p1[i]);
   uint32_t r[4];
-  draw(g, t, (uint32_t)i, 0u, r);
+  draw(g, s.t, (uint32_t)i, 0u, r);
   int d0, d1;
   dice_from(r[0], g.dice_mode, d0, d1);
   Legal l;
@@ -359,7 +382,6 @@ struct narde_env {
   uint64_t seed;
   int dice_mode;
   int max_steps;
-  uint32_t t;
   uint32_t epoch;
   Planes pl;
   // host-call staging (scalar facade)
@@ -464,7 +486,8 @@ int narde_create(int device, int64_t num_envs, int64_t env_id_offset, uint64_t s
     return fail(NARDE_ENOMEM, "device alloc for %lld envs: %s", (long long)num_envs,
                 hipGetErrorString(err));
   }
-  k_reset<<<grid(num_envs), kBlock, 0, e->hstream>>>(e->pl, (int)num_envs, rng_of(e), 0u, nullptr);
+  k_reset<<<grid(num_envs), kBlock, 0, e->hstream>>>(e->pl, (int)num_envs, rng_of(e), 0u, nullptr,
+                                                     (int64_t)0);
   int rc = check_launch("k_reset");
   if (rc == NARDE_OK) {
     err = hipStreamSynchronize(e->hstream);
@@ -497,20 +520,28 @@ int64_t narde_num_envs(const narde_env* e) { return e ? e->n : -1; }
 
 int narde_get_ply(const narde_env* e, uint32_t* t) {
   if (!e || !t) return fail(NARDE_EINVAL, "NULL argument");
-  *t = e->t;
+  DeviceGuard dg(e->device);
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(t, reinterpret_cast<const char*>(e->pl.p1) + 12, sizeof(uint32_t),
+                    hipMemcpyDeviceToHost));
   return NARDE_OK;
 }
 
 int narde_set_ply(narde_env* e, uint32_t t) {
   if (!e) return fail(NARDE_EINVAL, "NULL handle");
-  e->t = t;
+  DeviceGuard dg(e->device);
+  k_set_ply<<<grid(e->n), kBlock, 0, e->hstream>>>(e->pl, (int)e->n, t);
+  int rc = check_launch("k_set_ply");
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(e->hstream));
   return NARDE_OK;
 }
 
 int narde_reset(narde_env* e, const uint8_t* mask, void* stream) {
   if (!e) return fail(NARDE_EINVAL, "NULL handle");
   DeviceGuard dg(e->device);
-  k_reset<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), e->epoch, mask);
+  k_reset<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), e->epoch, mask,
+                                                           (int64_t)-1);
   e->epoch += 1;
   return check_launch("k_reset");
 }
@@ -520,7 +551,7 @@ int narde_set_state(narde_env* e, const int8_t* board, const uint8_t* off, const
   if (!e || !board || !off || !ft || !player) return fail(NARDE_EINVAL, "NULL argument");
   DeviceGuard dg(e->device);
   k_set_state<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, board, off, ft, player,
-                                                              elapsed);
+                                                              elapsed, 1);
   return check_launch("k_set_state");
 }
 
@@ -536,7 +567,7 @@ int narde_get_state(narde_env* e, int8_t* board, uint8_t* off, uint8_t* ft, int8
 int narde_peek_dice(narde_env* e, uint8_t* dice, void* stream) {
   if (!e || !dice) return fail(NARDE_EINVAL, "NULL argument");
   DeviceGuard dg(e->device);
-  k_peek_dice<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>((int)e->n, rng_of(e), e->t, dice);
+  k_peek_dice<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), dice);
   return check_launch("k_peek_dice");
 }
 
@@ -544,7 +575,7 @@ int narde_legal_moves(narde_env* e, const uint8_t* dice, int16_t* out_count, int
                       uint64_t* out_compact, void* stream) {
   if (!e || !out_count) return fail(NARDE_EINVAL, "NULL argument");
   DeviceGuard dg(e->device);
-  k_legal<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), e->t, dice,
+  k_legal<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), dice,
                                                           out_count, out_moves, out_compact);
   return check_launch("k_legal");
 }
@@ -558,30 +589,28 @@ int narde_step(narde_env* e, const int16_t* actions, const uint8_t* dice, int32_
   a.pl = e->pl;
   a.n = (int)e->n;
   a.g = rng_of(e);
-  a.t = e->t;
   a.max_steps = e->max_steps;
   a.autoreset = autoreset;
   a.actions = actions;
   a.dice = dice;
-  a.obs = obs;
-  a.reward = reward;
-  a.term = terminated;
-  a.trunc = truncated;
-  a.legal = legal_compact;
-  a.act_out = actions_out;
+  a.out = Outs{obs, reward, terminated, truncated, legal_compact, actions_out};
   k_step<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(a);
-  e->t += 1;
   return check_launch("k_step");
 }
 
-int narde_selfplay(narde_env* e, int plies, void* stream) {
+int narde_rollout(narde_env* e, int plies, int32_t* obs, int32_t* reward, uint8_t* terminated,
+                  uint8_t* truncated, uint64_t* legal_compact, int16_t* actions_out, void* stream) {
   if (!e || plies < 0) return fail(NARDE_EINVAL, "bad argument");
   if (plies == 0) return NARDE_OK;
   DeviceGuard dg(e->device);
-  k_selfplay<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), e->t, plies,
-                                                             e->max_steps);
-  e->t += (uint32_t)plies;
-  return check_launch("k_selfplay");
+  k_rollout<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(
+      e->pl, (int)e->n, rng_of(e), plies, e->max_steps,
+      Outs{obs, reward, terminated, truncated, legal_compact, actions_out});
+  return check_launch("k_rollout");
+}
+
+int narde_selfplay(narde_env* e, int plies, void* stream) {
+  return narde_rollout(e, plies, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
 }
 
 int narde_get_stats(narde_env* e, int32_t* stats, void* stream) {
@@ -609,7 +638,7 @@ int narde_observe(narde_env* e, int32_t* obs, float* tes, void* stream) {
 int narde_legal_mask576(narde_env* e, uint64_t* mask, void* stream) {
   if (!e || !mask) return fail(NARDE_EINVAL, "NULL argument");
   DeviceGuard dg(e->device);
-  k_mask576<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), e->t, mask);
+  k_mask576<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), mask);
   return check_launch("k_mask576");
 }
 
@@ -680,8 +709,8 @@ int narde_host_legal_moves(narde_env* e, int64_t n, const int8_t* board, const u
   int16_t* hc = ho.take<int16_t>(n); int16_t* dc = dq.take<int16_t>(n);
   int8_t* hm = ho.take<int8_t>(n * NARDE_MAX_MOVES * 2); int8_t* dm = dq.take<int8_t>(n * NARDE_MAX_MOVES * 2);
   HIP_TRY(hipMemcpyAsync(e->d_in, e->h_in, hi.off, hipMemcpyHostToDevice, e->hstream));
-  k_set_state<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, db, doff, dft, dp, nullptr);
-  k_legal<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, rng_of(e), 0u, dd, dc, moves ? dm : nullptr,
+  k_set_state<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, db, doff, dft, dp, nullptr, 0);
+  k_legal<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, rng_of(e), dd, dc, moves ? dm : nullptr,
                                               nullptr);
   if ((rc = check_launch("host legal"))) return rc;
   HIP_TRY(hipMemcpyAsync(e->h_out, e->d_out, dq.off, hipMemcpyDeviceToHost, e->hstream));
@@ -719,22 +748,16 @@ int narde_host_step(narde_env* e, int64_t n, int8_t* board, uint8_t* off, uint8_
   int32_t* hr = ho.take<int32_t>(n); int32_t* dr = dq.take<int32_t>(n);
   uint8_t* ht = ho.take<uint8_t>(n); uint8_t* dt = dq.take<uint8_t>(n);
   HIP_TRY(hipMemcpyAsync(e->d_in, e->h_in, hi.off, hipMemcpyHostToDevice, e->hstream));
-  k_set_state<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, db, doff, dft, dp, nullptr);
+  k_set_state<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, db, doff, dft, dp, nullptr, 0);
   StepArgs a;
   a.pl = e->hpl;
   a.n = (int)n;
   a.g = rng_of(e);
-  a.t = 0;
   a.max_steps = 0;
   a.autoreset = 0;
   a.actions = da;
   a.dice = dd;
-  a.obs = dobs;
-  a.reward = dr;
-  a.term = dt;
-  a.trunc = nullptr;
-  a.legal = nullptr;
-  a.act_out = nullptr;
+  a.out = Outs{dobs, dr, dt, nullptr, nullptr, nullptr};
   k_step<<<grid(n), kBlock, 0, e->hstream>>>(a);
   k_get_state<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, db2, doff2, dft2, dp2, nullptr);
   if ((rc = check_launch("host step"))) return rc;
@@ -767,7 +790,7 @@ int narde_host_apply_moves(narde_env* e, int64_t n, int8_t* board, uint8_t* off,
   uint8_t* hoff2 = ho.take<uint8_t>(n * 2); uint8_t* doff2 = dq.take<uint8_t>(n * 2);
   uint8_t* hft2 = ho.take<uint8_t>(n * 2); uint8_t* dft2 = dq.take<uint8_t>(n * 2);
   HIP_TRY(hipMemcpyAsync(e->d_in, e->h_in, hi.off, hipMemcpyHostToDevice, e->hstream));
-  k_set_state<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, db, doff, dft, dp, nullptr);
+  k_set_state<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, db, doff, dft, dp, nullptr, 0);
   k_apply<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, dm, dp);
   k_get_state<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, db2, doff2, dft2, nullptr, nullptr);
   if ((rc = check_launch("host apply"))) return rc;

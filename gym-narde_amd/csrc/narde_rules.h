@@ -83,9 +83,13 @@ NARDE_FN uint32_t eq1_mask(const Nib& b) {
 // HBM record = two 16-byte planes per env (planar => every load/store of a
 // wave is one contiguous 1 KiB):
 //   plane0 = {white nib lo (u64), black nib lo (u64)}      absolute coords
-//   plane1 = {white nib hi, black nib hi, misc, spare}
+//   plane1 = {white nib hi, black nib hi, misc, t}
 //   misc   = off_w[0:4) | off_b[4:8) | ft_w<<8 | ft_b<<9 | black_to_move<<10
 //            | elapsed[16:32)
+//   t      = the env's RNG ply counter (Philox counter word 0): the dice and
+//            policy draws of the env's next step; +1 per step, kept across
+//            episodes.  Living in the record (not a launch argument) makes a
+//            step launch replayable from a hipGraph.
 struct Side {
   Nib own, opp;
   uint32_t O, P, S1o, S1p;
@@ -93,6 +97,7 @@ struct Side {
   uint32_t ft_own, ft_opp;
   uint32_t black;    // 1 if the mover is black (current_player == -1)
   uint32_t elapsed;  // steps taken in this episode (TimeLimit)
+  uint32_t t;        // RNG ply counter
 };
 
 NARDE_FN void side_masks(Side& s) {
@@ -118,6 +123,7 @@ NARDE_FN Side side_from_record(const uint4& a, const uint4& b) {
     s.off_own = offw; s.off_opp = offb; s.ft_own = ftw; s.ft_opp = ftb;
   }
   s.elapsed = misc >> 16;
+  s.t = b.w;
   side_masks(s);
   return s;
 }
@@ -136,13 +142,14 @@ NARDE_FN void side_to_record(const Side& s, uint4& a, uint4& b) {
   a.z = (uint32_t)k.lo; a.w = (uint32_t)(k.lo >> 32);
   b.x = w.hi; b.y = k.hi;
   b.z = offw | (offb << 4) | (ftw << 8) | (ftb << 9) | (s.black << 10) | (s.elapsed << 16);
-  b.w = 0;
+  b.w = s.t;
 }
 
 // reference layout (int8 board[24] absolute, off {w,b}, first_turn {w,b},
 // player +1/-1) <-> record.  Counts must be in 0..15 (checked by callers).
 NARDE_FN void record_from_board(const int8_t* board, uint32_t offw, uint32_t offb, uint32_t ftw,
-                                uint32_t ftb, int player, uint32_t elapsed, uint4& a, uint4& b) {
+                                uint32_t ftb, int player, uint32_t elapsed, uint32_t t, uint4& a,
+                                uint4& b) {
   Nib w{0, 0}, k{0, 0};
   for (int p = 0; p < 24; ++p) {
     const int v = board[p];
@@ -160,7 +167,7 @@ NARDE_FN void record_from_board(const int8_t* board, uint32_t offw, uint32_t off
   b.x = w.hi; b.y = k.hi;
   b.z = (offw & 15u) | ((offb & 15u) << 4) | ((ftw ? 1u : 0u) << 8) | ((ftb ? 1u : 0u) << 9) |
         ((player == -1 ? 1u : 0u) << 10) | (elapsed << 16);
-  b.w = 0u;
+  b.w = t;
 }
 
 NARDE_FN void board_from_record(const uint4& a, const uint4& b, int8_t* board, uint8_t* off,
@@ -185,6 +192,7 @@ NARDE_FN Side side_start(uint32_t black_first) {
   s.ft_own = s.ft_opp = 1;
   s.black = black_first;
   s.elapsed = 0;
+  s.t = 0;
   s.O = 1u << 23; s.P = 1u << 11; s.S1o = 0; s.S1p = 0;
   return s;
 }
@@ -456,9 +464,10 @@ NARDE_FN Side side_reset(uint32_t r) {
   return side_start(w > b ? 0u : 1u);
 }
 
-// One lockstep ply for one env: NardeEnv.step + gymnasium TimeLimit
-// (max_episode_steps, gym_narde/__init__.py:3-7) + optional auto-reset.
-// r = Philox4x32-10(ctr = {t, env, 0, 0}): r0 dice (unless given), r1/r2
+// One ply for one env: NardeEnv.step + gymnasium TimeLimit
+// (max_episode_steps, gym_narde/__init__.py:3-7) + optional auto-reset,
+// then t += 1.
+// r = Philox4x32-10(ctr = {s.t, env, 0, 0}): r0 dice (unless given), r1/r2
 // policy picks, r3 opening roll of the next episode.  st = {episodes,
 // white points, black points} increments.
 NARDE_FN void env_ply(Side& s, int4& st, const uint32_t r[4], bool have_dice, int d0, int d1,
@@ -476,8 +485,13 @@ NARDE_FN void env_ply(Side& s, int4& st, const uint32_t r[4], bool have_dice, in
       if (mover_black) st.z += o.reward;
       else st.y += o.reward;
     }
-    if (autoreset) s = side_reset(r[3]);
+    if (autoreset) {
+      const uint32_t t = s.t;
+      s = side_reset(r[3]);
+      s.t = t;
+    }
   }
+  s.t += 1u;
 }
 
 }  // namespace narde

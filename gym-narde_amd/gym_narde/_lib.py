@@ -37,6 +37,7 @@ SIGNATURES = {
     "narde_peek_dice": (_i32, [_vp, _vp, _vp]),
     "narde_legal_moves": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "narde_step": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
+    "narde_rollout": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "narde_selfplay": (_i32, [_vp, _i32, _vp]),
     "narde_get_stats": (_i32, [_vp, _vp, _vp]),
     "narde_apply_moves": (_i32, [_vp, _vp, _vp, _vp]),

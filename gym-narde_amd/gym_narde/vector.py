@@ -149,8 +149,32 @@ class VecNardeEnv:
                 {"legal": self.legal, "actions": self.actions_used})
 
     def selfplay(self, plies):
-        """plies lockstep plies of random-legal self-play in ONE launch."""
+        """plies plies of random-legal self-play in ONE launch (statistics only)."""
         self.handle.call("narde_selfplay", int(plies), self._s())
+
+    def rollout_buffers(self, plies, obs=True, reward=True, terminated=True, truncated=True,
+                        legal=True, actions=True):
+        """Allocate [plies][B] rollout buffers for rollout()."""
+        t, B, dev = self.torch, self.num_envs, self.device
+        mk = lambda on, shape, dt: t.empty(shape, dtype=dt, device=dev) if on else None  # noqa: E731
+        return dict(obs=mk(obs, (plies, B, 24), t.int32), reward=mk(reward, (plies, B), t.int32),
+                    terminated=mk(terminated, (plies, B), t.uint8),
+                    truncated=mk(truncated, (plies, B), t.uint8),
+                    legal=mk(legal, (plies, B), t.int64), actions=mk(actions, (plies, B, 2), t.int16))
+
+    def rollout(self, plies, bufs=None):
+        """plies plies of random-legal self-play (auto-reset) in ONE launch,
+        every ply's outputs streamed into [plies][B] buffers (see
+        rollout_buffers); equals `plies` calls of step()."""
+        if bufs is None:
+            bufs = self.rollout_buffers(plies)
+        for v in bufs.values():
+            if v is not None and v.shape[0] < plies:
+                raise ValueError("rollout buffer shorter than plies")
+        self.handle.call("narde_rollout", int(plies), _lib.ptr(bufs["obs"]), _lib.ptr(bufs["reward"]),
+                         _lib.ptr(bufs["terminated"]), _lib.ptr(bufs["truncated"]),
+                         _lib.ptr(bufs["legal"]), _lib.ptr(bufs["actions"]), self._s())
+        return bufs
 
     def stats(self):
         """(B,3) int32 {episodes finished, white points, black points}."""

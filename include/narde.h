@@ -72,8 +72,12 @@ int narde_create(int device, int64_t num_envs, int64_t env_id_offset, uint64_t s
                  int dice_mode, int max_episode_steps, narde_env **out);
 int narde_destroy(narde_env *env);
 int64_t narde_num_envs(const narde_env *env);
-/* lockstep ply counter t: device dice/policy draws of the next step use
- * Philox4x32-10(ctr = {t, global_env_id, 0, 0}, key = seed) */
+/* Per-env RNG ply counter t (kept in the env record, +1 per step, kept
+ * across episodes): the device dice/policy draws of an env's next step are
+ * Philox4x32-10(ctr = {t, global_env_id, 0, 0}, key = seed).  Because t lives
+ * in device state, narde_step / narde_rollout launches can be captured in a
+ * hipGraph and replayed.  get_ply reads env 0's counter (synchronises the
+ * device); set_ply sets every env's counter (synchronous). */
 int narde_get_ply(const narde_env *env, uint32_t *t);
 int narde_set_ply(narde_env *env, uint32_t t);
 
@@ -105,19 +109,27 @@ int narde_legal_moves(narde_env *env, const uint8_t *dice, int16_t *out_count,
 
 /* NardeEnv.step for all B envs.  actions i16[B][2] = (move1_code,
  * move2_code); NULL = in-kernel random legal policy.  dice u8[B][2] in roll
- * order; NULL = device RNG for ply t.  Outputs (each optional, NULL = skip):
+ * order; NULL = device RNG at each env's counter t.  Outputs (each optional, NULL = skip):
  * obs i32[B][24] (next mover's perspective), reward i32[B], terminated u8[B],
  * truncated u8[B], legal_compact u64[B] (list #1, format above),
  * actions_out i16[B][2] (codes actually used).  autoreset != 0: envs that
  * terminate or truncate are reset in the same call (obs is then the new
- * episode's first obs) and counted in the statistics.  Increments t. */
+ * episode's first obs) and counted in the statistics.  Increments every
+ * env's t. */
 int narde_step(narde_env *env, const int16_t *actions, const uint8_t *dice, int32_t *obs,
                int32_t *reward, uint8_t *terminated, uint8_t *truncated,
                uint64_t *legal_compact, int16_t *actions_out, int autoreset, void *stream);
 
-/* `plies` lockstep plies of random-legal self-play with auto-reset, state
- * kept in registers across plies (one launch).  Only statistics are
- * produced; increments t by plies. */
+/* `plies` plies of random-legal self-play with auto-reset in ONE launch, the
+ * env record kept in registers across plies.  Every ply's outputs are
+ * streamed to rollout buffers laid out [plies][B][...] with the per-ply
+ * formats of narde_step (each optional, NULL = skip).  Statistics accumulate
+ * as in narde_step.  Equivalent to `plies` narde_step(actions = NULL,
+ * dice = NULL, autoreset = 1) calls. */
+int narde_rollout(narde_env *env, int plies, int32_t *obs, int32_t *reward, uint8_t *terminated,
+                  uint8_t *truncated, uint64_t *legal_compact, int16_t *actions_out, void *stream);
+
+/* narde_rollout with no per-ply outputs (statistics only). */
 int narde_selfplay(narde_env *env, int plies, void *stream);
 
 /* Per-env statistics i32[B][3] = {episodes finished, white points, black

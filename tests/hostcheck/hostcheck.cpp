@@ -19,7 +19,7 @@ static void draw(uint64_t seed, uint32_t t, uint32_t env, uint32_t stream, uint3
 static Side load(const int8_t* board, const uint8_t* off, const uint8_t* ft, int player,
                  uint32_t elapsed) {
   uint4 a, b;
-  record_from_board(board, off[0], off[1], ft[0], ft[1], player, elapsed, a, b);
+  record_from_board(board, off[0], off[1], ft[0], ft[1], player, elapsed, 0u, a, b);
   return side_from_record(a, b);
 }
 

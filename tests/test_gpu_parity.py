@@ -152,6 +152,57 @@ def test_fused_selfplay_vs_oracle():
     assert np.array_equal(np_(env2.get_state()["board"]), ref.board)
 
 
+def test_rollout_vs_oracle_and_step():
+    """k_rollout (P plies per launch, outputs streamed) == the oracle per ply,
+    across launch boundaries of different lengths."""
+    n, seed, env0 = 4096, 0xABCDEF, 777
+    env = vec(n, seed=seed, env_id_offset=env0, max_episode_steps=150)
+    ref = O.SelfPlay(n, seed=seed, env0=env0, max_steps=150)
+    ref.reset(0)
+    for plies in (1, 64, 235):
+        rec = ref.run(plies)
+        bufs = env.rollout(plies)
+        assert np.array_equal(np_(bufs["obs"]), rec["obs"].astype(np.int32))
+        assert np.array_equal(np_(bufs["reward"]), rec["reward"].astype(np.int32))
+        assert np.array_equal(np_(bufs["terminated"]), rec["terminated"])
+        assert np.array_equal(np_(bufs["truncated"]), rec["truncated"])
+        assert np.array_equal(np_(bufs["actions"]), rec["action"])
+        lg = np_(bufs["legal"]).view(np.uint64)
+        cnt = (np.vectorize(lambda x: bin(int(x) & 0xFFFFFFFFFFFF).count("1"))(lg)).astype(np.int16)
+        assert np.array_equal(cnt, rec["count1"])
+    assert np.array_equal(np_(env.stats()), ref.stats)
+    assert env.ply == 300
+
+
+def test_step_graph_replay_vs_oracle():
+    """k_step captured in a hipGraph and replayed advances each env's own RNG
+    counter, so replays reproduce consecutive plies exactly."""
+    n, seed, G, R = 4096, 4242, 20, 5
+    env = vec(n, seed=seed)
+    ref = O.SelfPlay(n, seed=seed)
+    ref.reset(0)
+    graph = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream()
+    cap.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(cap):
+        with torch.cuda.graph(graph, stream=cap):
+            for _ in range(G):
+                env.step()
+    torch.cuda.current_stream().wait_stream(cap)
+    torch.cuda.synchronize()
+    # capture does not execute: state untouched
+    assert np.array_equal(np_(env.get_state()["board"]), ref.board)
+    for _ in range(R):
+        graph.replay()
+    torch.cuda.synchronize()
+    ref.run(G * R, record=False)
+    assert np.array_equal(np_(env.get_state()["board"]), ref.board)
+    assert np.array_equal(np_(env.stats()), ref.stats)
+    rec = ref.run(1)
+    obs, *_ = env.step()
+    assert np.array_equal(np_(obs), rec["obs"][0].astype(np.int32))
+
+
 def test_full_batch_subset_and_invariants():
     """B = 65536 (BASELINE configs[2]): a contiguous window of envs equals the
     oracle run on just those global ids, and the whole batch conserves
