@@ -253,7 +253,9 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
 
 // `plies` plies of random-legal self-play with auto-reset in one launch; the
 // record stays in VGPRs, each ply's outputs (if requested) are streamed to
-// [ply][n] rollout buffers.
+// [ply][n] rollout buffers.  kOut = false: statistics only (a separate
+// instantiation, so profiles tell the two apart).
+template <bool kOut>
 __global__ void __launch_bounds__(kBlock) k_rollout(Planes pl, int n, Rng g, int plies, int max_steps,
                                                     Outs out) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
@@ -264,7 +266,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Planes pl, int n, Rng g, int
     StepOut o;
     int term, trunc;
     ply(s, st, g, (uint32_t)i, nullptr, nullptr, max_steps, true, o, term, trunc);
-    store_outs(out, (size_t)p * n + i, s, o, term, trunc);
+    if (kOut) store_outs(out, (size_t)p * n + i, s, o, term, trunc);
   }
   uint4 ra, rb;
   side_to_record(s, ra, rb);
@@ -603,9 +605,14 @@ int narde_rollout(narde_env* e, int plies, int32_t* obs, int32_t* reward, uint8_
   if (!e || plies < 0) return fail(NARDE_EINVAL, "bad argument");
   if (plies == 0) return NARDE_OK;
   DeviceGuard dg(e->device);
-  k_rollout<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(
-      e->pl, (int)e->n, rng_of(e), plies, e->max_steps,
-      Outs{obs, reward, terminated, truncated, legal_compact, actions_out});
+  const Outs out{obs, reward, terminated, truncated, legal_compact, actions_out};
+  const bool any = obs || reward || terminated || truncated || legal_compact || actions_out;
+  if (any)
+    k_rollout<true><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), plies,
+                                                                   e->max_steps, out);
+  else
+    k_rollout<false><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), plies,
+                                                                    e->max_steps, out);
   return check_launch("k_rollout");
 }
 
