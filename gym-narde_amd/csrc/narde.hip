@@ -312,8 +312,8 @@ __global__ void __launch_bounds__(kBlock) k_observe(Planes pl, int n, int32_t* _
   if (tes) {
     // README.md:42-102 layout, absolute points: [white 24x4, bar, off,
     // black 24x4, bar, off, player one-hot]
-    const Nib w{(uint64_t)a.x | ((uint64_t)a.y << 32), b.x};
-    const Nib k{(uint64_t)a.z | ((uint64_t)a.w << 32), b.y};
+    const Nib w{{a.x, a.y, b.x}};
+    const Nib k{{a.z, a.w, b.y}};
     float2* o = reinterpret_cast<float2*>(tes + (size_t)i * 198);
 #pragma unroll
     for (int side = 0; side < 2; ++side) {

@@ -1,4 +1,4 @@
-// narde_rules.h -- branchless-bitmask Narde rules engine for one env per lane.
+// narde_rules.h -- branch-light bitmask Narde rules engine, one env per lane.
 //
 // MI355X-native restatement of the reference hot path (cites are
 // /root/reference/<path>:<line>):
@@ -11,8 +11,10 @@
 //
 // Representation (all in the MOVER's perspective, mover checkers move toward
 // lower indices, head = 23, home = 0..5, 'off' encoded as to = 24):
-//   * counts: 24 points x 4-bit nibbles per side (Nib: lo = points 0..15,
-//     hi = points 16..23); a side never has more than 15 checkers.
+//   * counts: 24 points x 4-bit nibbles per side in three u32 words
+//     (w[0] = points 0..7, w[1] = 8..15, w[2] = 16..23); a side never has
+//     more than 15 checkers.  A perspective flip is a 48-bit rotation of the
+//     96-bit word triple = three v_alignbit_b32.
 //   * masks: O (own occupied), P (opponent occupied), S1o/S1p (count == 1).
 //   * a legal-move list is a list of per-die 24-bit source masks L[k] with
 //     dice d[k] sorted descending: entry order = die-major, source ascending,
@@ -32,26 +34,31 @@ constexpr int OFF = 24;
 
 // ---------------------------------------------------------------- nibbles
 struct Nib {
-  uint64_t lo;  // points 0..15
-  uint32_t hi;  // points 16..23
+  uint32_t w[3];  // points 0..7, 8..15, 16..23
 };
 
-NARDE_FN uint32_t nib_get(const Nib& b, int p) {
-  return p < 16 ? (uint32_t)(b.lo >> (4 * p)) & 15u : (b.hi >> (4 * (p - 16))) & 15u;
+// (hi:lo) >> 16, low 32 bits: one v_alignbit_b32 on gfx950
+NARDE_FN uint32_t funnel16(uint32_t hi, uint32_t lo) { return (lo >> 16) | (hi << 16); }
+
+NARDE_FN uint32_t nib_word(const Nib& b, int p) {
+  return p < 8 ? b.w[0] : (p < 16 ? b.w[1] : b.w[2]);
 }
-NARDE_FN void nib_inc(Nib& b, int p) {
-  if (p < 16) b.lo += 1ull << (4 * p);
-  else b.hi += 1u << (4 * (p - 16));
+NARDE_FN uint32_t nib_get(const Nib& b, int p) { return (nib_word(b, p) >> (4 * (p & 7))) & 15u; }
+NARDE_FN void nib_add(Nib& b, int p, uint32_t delta /* +1 or 0xFFFFFFFF */) {
+  const uint32_t v = delta << (4 * (p & 7));
+  const int k = p >> 3;
+  b.w[0] += k == 0 ? v : 0u;
+  b.w[1] += k == 1 ? v : 0u;
+  b.w[2] += k == 2 ? v : 0u;
 }
-NARDE_FN void nib_dec(Nib& b, int p) {
-  if (p < 16) b.lo -= 1ull << (4 * p);
-  else b.hi -= 1u << (4 * (p - 16));
-}
+NARDE_FN void nib_inc(Nib& b, int p) { nib_add(b, p, 1u); }
+NARDE_FN void nib_dec(Nib& b, int p) { nib_add(b, p, 0xFFFFFFFFu); }
 // perspective flip: new[p] = old[(p + 12) % 24]  (narde.py:16-17 without the sign)
 NARDE_FN Nib nib_rot12(const Nib& b) {
   Nib r;
-  r.lo = (b.lo >> 48) | ((uint64_t)b.hi << 16) | (b.lo << 48);
-  r.hi = (uint32_t)(b.lo >> 16);
+  r.w[0] = funnel16(b.w[2], b.w[1]);
+  r.w[1] = funnel16(b.w[0], b.w[2]);
+  r.w[2] = funnel16(b.w[1], b.w[0]);
   return r;
 }
 NARDE_FN uint32_t rot12(uint32_t m) { return ((m >> 12) | (m << 12)) & MASK24; }
@@ -69,21 +76,20 @@ NARDE_FN uint32_t fold_nz(uint32_t x) {
   return x & 0x11111111u;
 }
 NARDE_FN uint32_t nz_mask(const Nib& b) {
-  return compact4(fold_nz((uint32_t)b.lo)) | (compact4(fold_nz((uint32_t)(b.lo >> 32))) << 8) |
-         (compact4(fold_nz(b.hi)) << 16);
+  return compact4(fold_nz(b.w[0])) | (compact4(fold_nz(b.w[1])) << 8) |
+         (compact4(fold_nz(b.w[2])) << 16);
 }
 NARDE_FN uint32_t eq1_mask(const Nib& b) {
   const uint32_t k = 0x11111111u;
-  return compact4(~fold_nz((uint32_t)b.lo ^ k) & k) |
-         (compact4(~fold_nz((uint32_t)(b.lo >> 32) ^ k) & k) << 8) |
-         (compact4(~fold_nz(b.hi ^ k) & k) << 16);
+  return compact4(~fold_nz(b.w[0] ^ k) & k) | (compact4(~fold_nz(b.w[1] ^ k) & k) << 8) |
+         (compact4(~fold_nz(b.w[2] ^ k) & k) << 16);
 }
 
 // ------------------------------------------------------------ env record
 // HBM record = two 16-byte planes per env (planar => every load/store of a
 // wave is one contiguous 1 KiB):
-//   plane0 = {white nib lo (u64), black nib lo (u64)}      absolute coords
-//   plane1 = {white nib hi, black nib hi, misc, t}
+//   plane0 = {white w0, white w1, black w0, black w1}   absolute coords
+//   plane1 = {white w2, black w2, misc, t}
 //   misc   = off_w[0:4) | off_b[4:8) | ft_w<<8 | ft_b<<9 | black_to_move<<10
 //            | elapsed[16:32)
 //   t      = the env's RNG ply counter (Philox counter word 0): the dice and
@@ -108,8 +114,8 @@ NARDE_FN void side_masks(Side& s) {
 }
 
 NARDE_FN Side side_from_record(const uint4& a, const uint4& b) {
-  Nib w{(uint64_t)a.x | ((uint64_t)a.y << 32), b.x};
-  Nib k{(uint64_t)a.z | ((uint64_t)a.w << 32), b.y};
+  const Nib w{{a.x, a.y, b.x}};
+  const Nib k{{a.z, a.w, b.y}};
   const uint32_t misc = b.z;
   Side s;
   s.black = (misc >> 10) & 1u;
@@ -138,9 +144,9 @@ NARDE_FN void side_to_record(const Side& s, uint4& a, uint4& b) {
     w = s.own; k = s.opp;
     offw = s.off_own; offb = s.off_opp; ftw = s.ft_own; ftb = s.ft_opp;
   }
-  a.x = (uint32_t)w.lo; a.y = (uint32_t)(w.lo >> 32);
-  a.z = (uint32_t)k.lo; a.w = (uint32_t)(k.lo >> 32);
-  b.x = w.hi; b.y = k.hi;
+  a.x = w.w[0]; a.y = w.w[1];
+  a.z = k.w[0]; a.w = k.w[1];
+  b.x = w.w[2]; b.y = k.w[2];
   b.z = offw | (offb << 4) | (ftw << 8) | (ftb << 9) | (s.black << 10) | (s.elapsed << 16);
   b.w = s.t;
 }
@@ -150,21 +156,16 @@ NARDE_FN void side_to_record(const Side& s, uint4& a, uint4& b) {
 NARDE_FN void record_from_board(const int8_t* board, uint32_t offw, uint32_t offb, uint32_t ftw,
                                 uint32_t ftb, int player, uint32_t elapsed, uint32_t t, uint4& a,
                                 uint4& b) {
-  Nib w{0, 0}, k{0, 0};
+  Nib w{{0, 0, 0}}, k{{0, 0, 0}};
   for (int p = 0; p < 24; ++p) {
     const int v = board[p];
     const uint32_t cw = v > 0 ? (uint32_t)v : 0u, ck = v < 0 ? (uint32_t)(-v) : 0u;
-    if (p < 16) {
-      w.lo |= (uint64_t)(cw & 15u) << (4 * p);
-      k.lo |= (uint64_t)(ck & 15u) << (4 * p);
-    } else {
-      w.hi |= (cw & 15u) << (4 * (p - 16));
-      k.hi |= (ck & 15u) << (4 * (p - 16));
-    }
+    w.w[p >> 3] |= (cw & 15u) << (4 * (p & 7));
+    k.w[p >> 3] |= (ck & 15u) << (4 * (p & 7));
   }
-  a.x = (uint32_t)w.lo; a.y = (uint32_t)(w.lo >> 32);
-  a.z = (uint32_t)k.lo; a.w = (uint32_t)(k.lo >> 32);
-  b.x = w.hi; b.y = k.hi;
+  a.x = w.w[0]; a.y = w.w[1];
+  a.z = k.w[0]; a.w = k.w[1];
+  b.x = w.w[2]; b.y = k.w[2];
   b.z = (offw & 15u) | ((offb & 15u) << 4) | ((ftw ? 1u : 0u) << 8) | ((ftb ? 1u : 0u) << 9) |
         ((player == -1 ? 1u : 0u) << 10) | (elapsed << 16);
   b.w = t;
@@ -172,8 +173,8 @@ NARDE_FN void record_from_board(const int8_t* board, uint32_t offw, uint32_t off
 
 NARDE_FN void board_from_record(const uint4& a, const uint4& b, int8_t* board, uint8_t* off,
                                 uint8_t* ft, int8_t* player, uint16_t* elapsed) {
-  const Nib w{(uint64_t)a.x | ((uint64_t)a.y << 32), b.x};
-  const Nib k{(uint64_t)a.z | ((uint64_t)a.w << 32), b.y};
+  const Nib w{{a.x, a.y, b.x}};
+  const Nib k{{a.z, a.w, b.y}};
   if (board)
     for (int p = 0; p < 24; ++p) board[p] = (int8_t)((int)nib_get(w, p) - (int)nib_get(k, p));
   if (off) { off[0] = b.z & 15u; off[1] = (b.z >> 4) & 15u; }
@@ -186,8 +187,8 @@ NARDE_FN void board_from_record(const uint4& a, const uint4& b, int8_t* board, u
 NARDE_FN Side side_start(uint32_t black_first) {
   Side s;
   // in either perspective the mover has 15 on 23 and the opponent 15 on 11
-  s.own.lo = 0; s.own.hi = 15u << 28;
-  s.opp.lo = 15ull << 44; s.opp.hi = 0;
+  s.own.w[0] = 0; s.own.w[1] = 0; s.own.w[2] = 15u << 28;
+  s.opp.w[0] = 0; s.opp.w[1] = 15u << 12; s.opp.w[2] = 0;
   s.off_own = s.off_opp = 0;
   s.ft_own = s.ft_opp = 1;
   s.black = black_first;
@@ -199,7 +200,7 @@ NARDE_FN Side side_start(uint32_t black_first) {
 
 // mover change (narde_env.py:99-100)
 NARDE_FN void side_flip(Side& s) {
-  Nib t = s.own;
+  const Nib t = s.own;
   s.own = nib_rot12(s.opp);
   s.opp = nib_rot12(t);
   uint32_t m = s.O; s.O = rot12(s.P); s.P = rot12(m);
@@ -224,6 +225,36 @@ NARDE_FN uint32_t block_lowmask(uint32_t P) {
   return P ? ((2u << __builtin_ctz(P)) - 1u) : MASK24;
 }
 
+// What a single move can do to the block rule on this board, for any die:
+//   F = allowed 6-windows already full of own checkers (they violate unless
+//       the move breaks them);
+//   Q = empty/opponent points q whose filling completes an allowed window:
+//       window [q-a, q-a+5] (a = 0..5) needs own q-a..q-1 and q+1..q+5-a and
+//       its start q-a <= lo.
+struct Blocks {
+  uint32_t low, F, Q;
+};
+
+NARDE_FN Blocks block_info(uint32_t O, uint32_t P) {
+  Blocks b;
+  b.low = block_lowmask(P);
+  const uint32_t r2 = O & (O >> 1);
+  const uint32_t r3 = r2 & (O >> 2);
+  const uint32_t r4 = r2 & (r2 >> 2);
+  const uint32_t r5 = r4 & (O >> 4);
+  b.F = r4 & (r2 >> 4) & b.low;
+  const uint32_t lp = b.low + 1u;  // 1 << (lo + 1)
+  // q <= lo + a  <=>  bit q of (lp << a) - 1
+  uint32_t q = (r5 >> 1) & b.low;                               // a = 0
+  q |= (O << 1) & (r4 >> 1) & ((lp << 1) - 1u);                 // a = 1
+  q |= (r2 << 2) & (r3 >> 1) & ((lp << 2) - 1u);                // a = 2
+  q |= (r3 << 3) & (r2 >> 1) & ((lp << 3) - 1u);                // a = 3
+  q |= (r4 << 4) & (O >> 1) & ((lp << 4) - 1u);                 // a = 4
+  q |= (r5 << 5) & ((lp << 5) - 1u);                            // a = 5
+  b.Q = q & ~O & MASK24;
+  return b;
+}
+
 // narde.py:64-77 for one die: sources with a legal single move
 NARDE_FN uint32_t die_candidates(uint32_t O, uint32_t P, int d) {
   const uint32_t normal = O & ~(P << d) & (MASK24 << d) & MASK24;
@@ -231,16 +262,20 @@ NARDE_FN uint32_t die_candidates(uint32_t O, uint32_t P, int d) {
   return normal | off;
 }
 
-// narde.py:78-89 block filter of one die's candidates
-NARDE_FN uint32_t die_filter(uint32_t O, uint32_t S1, uint32_t lowmask, uint32_t C, int d) {
-  if ((runs6(O | (C >> d)) & lowmask) == 0u) return C;  // no candidate can form a block
-  uint32_t L = C, m = C;
+// narde.py:78-89 block filter of one die's candidates C.  A source with >= 2
+// checkers keeps O' = O | {q}: it violates iff F != 0 or q in Q.  Only a
+// single-checker source that would complete (or keep) a window needs the
+// exact per-candidate test, which is rare.
+NARDE_FN uint32_t die_filter(uint32_t O, uint32_t S1, const Blocks& bl, uint32_t C, int d) {
+  const uint32_t hit = bl.F ? MASK24 : (bl.Q << d);
+  uint32_t L = C & ~(hit & ~S1);
+  uint32_t m = C & hit & S1;
   while (m) {
     const int p = __builtin_ctz(m);
     m &= m - 1u;
     const uint32_t bp = 1u << p;
-    const uint32_t Op = (O & ~(S1 & bp)) | (p >= d ? (1u << (p - d)) : 0u);
-    if (runs6(Op) & lowmask) L &= ~bp;
+    const uint32_t Op = (O & ~bp) | (p >= d ? (1u << (p - d)) : 0u);
+    if (runs6(Op) & bl.low) L &= ~bp;
   }
   return L;
 }
@@ -253,15 +288,14 @@ struct Legal {
 };
 
 // Narde.get_valid_moves(roll, mover) for n <= 4 dice already sorted descending.
-// first_turn: mover's first_turn flag (head-rule exception, narde.py:100).
 NARDE_FN void legal_sorted(const Side& s, const int* dd, int n, Legal& l) {
-  const uint32_t low = block_lowmask(s.P);
+  const Blocks bl = block_info(s.O, s.P);
   l.n = n;
   for (int k = 0; k < 4; ++k) { l.L[k] = 0u; l.d[k] = 0; }
   for (int k = 0; k < n; ++k) {
     l.d[k] = dd[k];
     if (k > 0 && dd[k] == dd[k - 1]) { l.L[k] = l.L[k - 1]; continue; }
-    l.L[k] = die_filter(s.O, s.S1o, low, die_candidates(s.O, s.P, dd[k]), dd[k]);
+    l.L[k] = die_filter(s.O, s.S1o, bl, die_candidates(s.O, s.P, dd[k]), dd[k]);
   }
   // head rule (narde.py:94-106,127-137): keep the first max_head entries from 23
   const int max_head =
@@ -278,9 +312,21 @@ NARDE_FN void legal_sorted(const Side& s, const int* dd, int n, Legal& l) {
   l.count = count;
 }
 
+// the two-dice list of NardeEnv.step (roll in any order)
 NARDE_FN void legal2(const Side& s, int d0, int d1, Legal& l) {
-  int dd[2] = {d0 > d1 ? d0 : d1, d0 > d1 ? d1 : d0};
-  legal_sorted(s, dd, 2, l);
+  const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
+  const Blocks bl = block_info(s.O, s.P);
+  l.n = 2;
+  l.d[0] = dh; l.d[1] = dl; l.d[2] = 0; l.d[3] = 0;
+  l.L[2] = 0u; l.L[3] = 0u;
+  uint32_t Lh = die_filter(s.O, s.S1o, bl, die_candidates(s.O, s.P, dh), dh);
+  uint32_t Ll = dl == dh ? Lh : die_filter(s.O, s.S1o, bl, die_candidates(s.O, s.P, dl), dl);
+  // head rule: the second head entry survives only on a first-turn 3-3/4-4/6-6
+  const bool two_heads = s.ft_own && dh == dl && (dh == 3 || dh == 4 || dh == 6);
+  if ((Lh >> 23) && !two_heads) Ll &= ~(1u << 23);
+  l.L[0] = Lh;
+  l.L[1] = Ll;
+  l.count = __builtin_popcount(Lh) + __builtin_popcount(Ll);
 }
 
 // get_valid_moves for an explicit roll of up to 4 dice (0 = unused slot)
@@ -298,10 +344,22 @@ NARDE_FN void legal_roll(const Side& s, const uint8_t* d4, Legal& l) {
   legal_sorted(s, dd, nd, l);
 }
 
-// j-th (0-based) set bit of m (j < popcount(m))
+// j-th (0-based) set bit of a 24-bit m (j < popcount(m)): branch-free
+// binary search on popcounts (12 / 6 / 3 / 1 / 1)
 NARDE_FN int select_bit(uint32_t m, int j) {
-  for (int i = 0; i < j; ++i) m &= m - 1u;
-  return __builtin_ctz(m);
+  int pos = 0;
+  uint32_t c;
+  c = __builtin_popcount(m & 0xFFFu);
+  if ((uint32_t)j >= c) { j -= (int)c; m >>= 12; pos += 12; }
+  c = __builtin_popcount(m & 0x3Fu);
+  if ((uint32_t)j >= c) { j -= (int)c; m >>= 6; pos += 6; }
+  c = __builtin_popcount(m & 0x7u);
+  if ((uint32_t)j >= c) { j -= (int)c; m >>= 3; pos += 3; }
+  c = m & 1u;
+  if ((uint32_t)j >= c) { j -= (int)c; m >>= 1; pos += 1; }
+  c = m & 1u;
+  if ((uint32_t)j >= c) { pos += 1; }
+  return pos;
 }
 
 // list entry i -> (from, to); to = OFF for bear-off
@@ -314,6 +372,16 @@ NARDE_FN void legal_entry(const Legal& l, int i, int& f, int& t) {
   }
   f = select_bit(l.L[k], i);
   t = f - l.d[k] < 0 ? OFF : f - l.d[k];
+}
+
+// entry i of a two-dice list -> (from, to, die)
+NARDE_FN void legal2_entry(const Legal& l, int i, int& f, int& t) {
+  const int c0 = __builtin_popcount(l.L[0]);
+  const bool second = i >= c0;
+  const uint32_t m = second ? l.L[1] : l.L[0];
+  const int d = second ? l.d[1] : l.d[0];
+  f = select_bit(m, second ? i - c0 : i);
+  t = f - d < 0 ? OFF : f - d;
 }
 
 // `move in valid_moves` (narde_env.py:255/281 analogue) in O(n)
@@ -341,16 +409,16 @@ NARDE_FN void apply_move(Side& s, int f, int t) {
   const uint32_t cf = nib_get(s.own, f);
   nib_dec(s.own, f);
   const uint32_t bf = 1u << f;
-  if (cf == 1u) { s.O &= ~bf; s.S1o &= ~bf; }
-  else if (cf == 2u) { s.S1o |= bf; }
+  s.O = cf == 1u ? (s.O & ~bf) : s.O;
+  s.S1o = cf == 1u ? (s.S1o & ~bf) : (cf == 2u ? (s.S1o | bf) : s.S1o);
   if (t == OFF) {
     s.off_own += 1u;
   } else {
     const uint32_t ct = nib_get(s.own, t);
     nib_inc(s.own, t);
     const uint32_t bt = 1u << t;
-    if (ct == 0u) { s.O |= bt; s.S1o |= bt; }
-    else if (ct == 1u) { s.S1o &= ~bt; }
+    s.O |= bt;
+    s.S1o = ct == 0u ? (s.S1o | bt) : (ct == 1u ? (s.S1o & ~bt) : s.S1o);
   }
   s.ft_own = 0u;
 }
@@ -375,42 +443,51 @@ NARDE_FN void env_step(Side& s, int d0, int d1, int code1, int code2, bool polic
   legal2(s, d0, d1, o.l1);
   o.L2 = 0u; o.d2 = 0; o.count2 = -1;
   const int n1 = o.l1.count;
+  int f1 = -1, t1 = -1;
+  bool play1;
   if (policy) {
-    code1 = 0; code2 = 0;
-    if (n1 >= 2) {
-      int f, t;
-      legal_entry(o.l1, (int)mulhi_u32(r1, (uint32_t)n1), f, t);
-      code1 = encode_move(f, t);
+    // the drawn entry is its own code; decode(encode(f, t)) differs from (f, t)
+    // only for a normal move (f, 0) with f <= 5, which decodes to (f, 'off')
+    legal2_entry(o.l1, n1 >= 2 ? (int)mulhi_u32(r1, (uint32_t)n1) : 0, f1, t1);
+    code1 = n1 >= 2 ? encode_move(f1, t1) : 0;
+    code2 = 0;
+    play1 = n1 >= 1;
+    if (n1 >= 2 && t1 == 0 && f1 <= 5) {
+      t1 = OFF;
+      play1 = legal_contains(o.l1, f1, t1);
     }
-  }
-  if (n1 == 1) {
-    int f, t;
-    legal_entry(o.l1, 0, f, t);
-    apply_move(s, f, t);  // narde_env.py:41-43, action ignored
-  } else if (n1 >= 2) {
-    int f1, t1;
+  } else if (n1 == 1) {
+    legal2_entry(o.l1, 0, f1, t1);  // narde_env.py:41-43, action ignored
+    play1 = true;
+  } else {
     decode_action(code1, f1, t1);
-    if (legal_contains(o.l1, f1, t1)) {
-      apply_move(s, f1, t1);
-      // die bookkeeping, narde_env.py:63-83: remove dist if rolled, else pop(0)
-      const int dist = t1 == OFF ? f1 + 1 : (f1 > t1 ? f1 - t1 : t1 - f1);
-      const int rem = (d0 == dist) ? d1 : ((d1 == dist) ? d0 : d1);
-      // second get_valid_moves([rem]) (:88): one die, first_turn already cleared
-      const uint32_t low = block_lowmask(s.P);
-      o.L2 = die_filter(s.O, s.S1o, low, die_candidates(s.O, s.P, rem), rem);
-      o.d2 = rem;
-      o.count2 = __builtin_popcount(o.L2);
-      if (policy) {
-        if (o.count2 > 0) {
-          const int f = select_bit(o.L2, (int)mulhi_u32(r2, (uint32_t)o.count2));
-          code2 = encode_move(f, f - rem < 0 ? OFF : f - rem);
-        }
-      }
-      int f2, t2;
+    play1 = n1 >= 2 && legal_contains(o.l1, f1, t1);
+  }
+  if (play1) apply_move(s, f1, t1);
+  if (n1 >= 2 && play1) {
+    // die bookkeeping, narde_env.py:63-83: remove dist if rolled, else pop(0)
+    const int dist = t1 == OFF ? f1 + 1 : (f1 > t1 ? f1 - t1 : t1 - f1);
+    const int rem = (d0 == dist) ? d1 : ((d1 == dist) ? d0 : d1);
+    // second get_valid_moves([rem]) (:88): one die, first_turn already cleared
+    const Blocks bl = block_info(s.O, s.P);
+    const uint32_t L2 = die_filter(s.O, s.S1o, bl, die_candidates(s.O, s.P, rem), rem);
+    o.L2 = L2;
+    o.d2 = rem;
+    o.count2 = __builtin_popcount(L2);
+    int f2, t2;
+    bool play2;
+    if (policy) {
+      f2 = select_bit(L2, (int)mulhi_u32(r2, (uint32_t)o.count2));
+      t2 = f2 - rem < 0 ? OFF : f2 - rem;
+      code2 = o.count2 > 0 ? encode_move(f2, t2) : 0;
+      // a drawn (f, 0) with f <= 5 decodes to (f, 'off'), never in a one-die
+      // list (it needs f < rem = f); code 0 = (0, 'off') on an empty list
+      play2 = o.count2 > 0 && !(t2 == 0 && f2 <= 5);
+    } else {
       decode_action(code2, f2, t2);
-      if (f2 >= 0 && ((o.L2 >> f2) & 1u) && (t2 == OFF ? (f2 < rem) : (f2 - t2 == rem)))
-        apply_move(s, f2, t2);
+      play2 = f2 >= 0 && ((L2 >> f2) & 1u) && (t2 == OFF ? (f2 < rem) : (f2 - t2 == rem));
     }
+    if (play2) apply_move(s, f2, t2);
   }
   o.code1 = code1;
   o.code2 = code2;
