@@ -192,25 +192,79 @@ struct StepArgs {
   Outs out;
 };
 
+// Output store strategy (tuning knob, tools/diag/variants.sh):
+//   0: each lane stores its own 96-B obs row (6 x 16 B at a 96-B lane stride:
+//      every wave-instruction touches ~48 partial 128-B lines);
+//   1: the wave transposes its 64 rows (6 KiB) through LDS so each
+//      wave-instruction stores one contiguous 1 KiB (8 whole lines);
+//   2: as 1 with non-temporal (streaming) stores for every per-ply output.
+#ifndef NARDE_OBS_STORE
+#define NARDE_OBS_STORE 2
+#endif
+
+template <class T>
+__device__ __forceinline__ void st_out(T* p, T v) {
+#if NARDE_OBS_STORE == 2
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ void st_out(int4* p, int4 v) {
+#if NARDE_OBS_STORE == 2
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  const v4i x = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(x, reinterpret_cast<v4i*>(p));
+#else
+  *p = v;
+#endif
+}
+
+__device__ __forceinline__ int4 obs_quad(const Side& s, int q) {
+  return make_int4(obs_point(s, 4 * q), obs_point(s, 4 * q + 1), obs_point(s, 4 * q + 2),
+                   obs_point(s, 4 * q + 3));
+}
+
 __device__ __forceinline__ void store_obs(int32_t* __restrict__ obs, size_t ix, const Side& s) {
   int4* o = reinterpret_cast<int4*>(obs + ix * 24);
 #pragma unroll
-  for (int q = 0; q < 6; ++q)
-    o[q] = make_int4(obs_point(s, 4 * q), obs_point(s, 4 * q + 1), obs_point(s, 4 * q + 2),
-                     obs_point(s, 4 * q + 3));
+  for (int q = 0; q < 6; ++q) st_out(o + q, obs_quad(s, q));
+}
+
+// whole-wave obs store through the wave's 6-KiB LDS slice (all 64 lanes
+// active, rows ix - lane .. ix - lane + 63 contiguous)
+__device__ __forceinline__ void store_obs_wave(int32_t* __restrict__ obs, size_t ix, const Side& s,
+                                               int4* __restrict__ lds) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) lds[lane * 6 + q] = obs_quad(s, q);
+  __builtin_amdgcn_wave_barrier();  // LDS ops of one wave retire in issue order
+  int4* dst = reinterpret_cast<int4*>(obs + (ix - lane) * 24);
+#pragma unroll
+  for (int q = 0; q < 6; ++q) st_out(dst + q * 64 + lane, lds[q * 64 + lane]);
+  __builtin_amdgcn_wave_barrier();
 }
 
 __device__ __forceinline__ void store_outs(const Outs& out, size_t ix, const Side& s,
-                                           const StepOut& o, int term, int trunc) {
-  if (out.obs) store_obs(out.obs, ix, s);
-  if (out.reward) out.reward[ix] = o.reward;
-  if (out.term) out.term[ix] = (uint8_t)term;
-  if (out.trunc) out.trunc[ix] = (uint8_t)trunc;
-  if (out.legal) out.legal[ix] = compact_legal(o.l1);
+                                           const StepOut& o, int term, int trunc, int4* lds,
+                                           bool wave_full) {
+  if (out.obs) {
+    if (NARDE_OBS_STORE != 0 && wave_full) store_obs_wave(out.obs, ix, s, lds);
+    else store_obs(out.obs, ix, s);
+  }
+  if (out.reward) st_out(out.reward + ix, (int32_t)o.reward);
+  if (out.term) st_out(out.term + ix, (uint8_t)term);
+  if (out.trunc) st_out(out.trunc + ix, (uint8_t)trunc);
+  if (out.legal) st_out(out.legal + ix, (uint64_t)compact_legal(o.l1));
   if (out.act_out)
-    reinterpret_cast<uint32_t*>(out.act_out)[ix] =
-        ((uint32_t)(uint16_t)o.code1) | ((uint32_t)(uint16_t)o.code2 << 16);
+    st_out(reinterpret_cast<uint32_t*>(out.act_out) + ix,
+           ((uint32_t)(uint16_t)o.code1) | ((uint32_t)(uint16_t)o.code2 << 16));
 }
+
+// this wave's slice of the block's obs staging buffer (6 KiB per wave)
+#define OBS_LDS_DECL                                   \
+  __shared__ int4 obs_lds[kBlock * 6];                 \
+  int4* const wave_lds = obs_lds + (threadIdx.x & ~63) * 6;
 
 // one ply for env i: draw with the env's own counter, then the shared
 // host/device ply (narde_rules.h)
@@ -236,6 +290,7 @@ __device__ __forceinline__ void add_stats(int4* __restrict__ stats, int i, const
 
 // NardeEnv.step for every env (API step; one ply of self-play when actions == NULL)
 __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
+  OBS_LDS_DECL
   const int i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= a.n) return;
   Side s = side_from_record(a.pl.p0[i], a.pl.p1[i]);
@@ -248,7 +303,7 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
   a.pl.p0[i] = ra;
   a.pl.p1[i] = rb;
   add_stats(a.pl.stats, i, st);
-  store_outs(a.out, (size_t)i, s, o, term, trunc);
+  store_outs(a.out, (size_t)i, s, o, term, trunc, wave_lds, i - (int)(threadIdx.x & 63) + 64 <= a.n);
 }
 
 // `plies` plies of random-legal self-play with auto-reset in one launch; the
@@ -258,15 +313,17 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
 template <bool kOut>
 __global__ void __launch_bounds__(kBlock) k_rollout(Planes pl, int n, Rng g, int plies, int max_steps,
                                                     Outs out) {
+  OBS_LDS_DECL
   const int i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
+  const bool wave_full = i - (int)(threadIdx.x & 63) + 64 <= n;
   Side s = side_from_record(pl.p0[i], pl.p1[i]);
   int4 st = make_int4(0, 0, 0, 0);
   for (int p = 0; p < plies; ++p) {
     StepOut o;
     int term, trunc;
     ply(s, st, g, (uint32_t)i, nullptr, nullptr, max_steps, true, o, term, trunc);
-    if (kOut) store_outs(out, (size_t)p * n + i, s, o, term, trunc);
+    if (kOut) store_outs(out, (size_t)p * n + i, s, o, term, trunc, wave_lds, wave_full);
   }
   uint4 ra, rb;
   side_to_record(s, ra, rb);

@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""Time k_rollout (outputs on/off) for the libnarde.so named by $NARDE_LIB."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(ROOT, "gym-narde_amd"))
+import torch  # noqa: E402
+
+from gym_narde.vector import VecNardeEnv  # noqa: E402
+
+
+def timed(fn, reps):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def main():
+    n, P, reps = 65536, 100, 30
+    env = VecNardeEnv(n, device="cuda:0", seed=0)
+    bufs = env.rollout_buffers(P)
+    env.selfplay(300)
+    out = {"lib": os.path.basename(os.environ.get("NARDE_LIB", "libnarde.so")),
+           "rollout_ms": round(timed(lambda: env.rollout(P, bufs), reps), 4),
+           "selfplay_ms": round(timed(lambda: env.selfplay(P), reps), 4)}
+    out["rollout_steps_per_s"] = round(n * P / (out["rollout_ms"] * 1e-3))
+    out["rollout_TBps"] = round(n * (114 * P + 64) / (out["rollout_ms"] * 1e-3) / 1e12, 3)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
