@@ -1,0 +1,38 @@
+#!/bin/bash
+# One gpurun call's worth of evidence (run on the MI355X box from the repo root):
+#   gpurun --timeout 1100 -- bash tools/gpu_round.sh [tag]
+# GPU parity tests, smoke, the bench line, the rocprofv3 kernel-trace summary of
+# the same bench command, and two separate PMC passes (FETCH_SIZE, WRITE_SIZE)
+# over k_rollout at the bench shape.  Every GPU step has its own time limit
+# and the steps are chained with && so the first failure ends the call.
+set -o pipefail
+TAG=${1:-r01}
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+echo "[gpu_round] $(date +%T) pytest -m gpu"
+timeout -k 10 420 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1 \
+  && echo "pytest rc=0" >> "$OUT/pytest_gpu.log" \
+  && echo "[gpu_round] $(date +%T) smoke" \
+  && timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
+  && echo "[gpu_round] $(date +%T) bench" \
+  && timeout -k 10 300 python bench.py > "$OUT/bench_n1.json" 2> "$OUT/bench_n1.err" \
+  && echo "[gpu_round] $(date +%T) rocprof kernel trace" \
+  && (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$OUT/rocprof" -o bench -- python3 "$ROOT/bench.py" --no-cpu-baseline \
+        > "$OUT/rocprof_bench.log" 2>&1) \
+  && echo "[gpu_round] $(date +%T) pmc FETCH_SIZE" \
+  && (cd /tmp && timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+        -d "$OUT/pmc/fetch" -o pmc -- python3 "$ROOT/tools/pmc_target.py" > "$OUT/pmc_fetch.log" 2>&1) \
+  && echo "[gpu_round] $(date +%T) pmc WRITE_SIZE" \
+  && (cd /tmp && timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+        -d "$OUT/pmc/write" -o pmc -- python3 "$ROOT/tools/pmc_target.py" > "$OUT/pmc_write.log" 2>&1) \
+  && python3 tools/pmc_summary.py --fetch "$OUT/pmc/fetch" --write "$OUT/pmc/write" \
+        --out "$OUT/pmc_k_rollout.json" \
+  && echo "[gpu_round] $(date +%T) done"
+rc=$?
+echo "[gpu_round] rc=$rc"
+tail -3 "$OUT/pytest_gpu.log" 2>/dev/null
+cat "$OUT/bench_n1.json" 2>/dev/null
+exit $rc
