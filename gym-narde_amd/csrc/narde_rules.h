@@ -235,9 +235,9 @@ struct Blocks {
   uint32_t low, F, Q;
 };
 
-NARDE_FN Blocks block_info(uint32_t O, uint32_t P) {
+NARDE_FN Blocks block_info_low(uint32_t O, uint32_t low) {
   Blocks b;
-  b.low = block_lowmask(P);
+  b.low = low;
   const uint32_t r2 = O & (O >> 1);
   const uint32_t r3 = r2 & (O >> 2);
   const uint32_t r4 = r2 & (r2 >> 2);
@@ -254,6 +254,7 @@ NARDE_FN Blocks block_info(uint32_t O, uint32_t P) {
   b.Q = q & ~O & MASK24;
   return b;
 }
+NARDE_FN Blocks block_info(uint32_t O, uint32_t P) { return block_info_low(O, block_lowmask(P)); }
 
 // narde.py:64-77 for one die: sources with a legal single move
 NARDE_FN uint32_t die_candidates(uint32_t O, uint32_t P, int d) {
@@ -497,6 +498,206 @@ NARDE_FN void env_step(Side& s, int d0, int d1, int code1, int code2, bool polic
   if (!o.term) side_flip(s);
 }
 
+// ============================================================ FULL4 turns
+// Build extension: one
+// step = the mover's WHOLE turn -- four sub-moves on doubles, the
+// max-dice-used rule (README.md:27-30), the higher die when only one of two
+// can be played.  Every sub-move is the reference's single-die primitive
+// (get_valid_moves([d]) = legal1 below, execute_rotated_move = apply_die);
+// the composition is restated independently in oracle/narde_oracle.c
+// (or_full4_turn) and pinned to tests/golden/full4.npz.
+//   H = 2 head moves on a first-turn 3-3/4-4/6-6 (narde.py:94-106's
+//   condition), else 1, for the whole turn.
+//   M = the longest playable sequence; C_k = the sub-moves that keep M
+//   reachable; list order die-descending, source-ascending.
+// The opponent never changes during a turn, so the block rule's low mask is
+// computed once per turn.
+constexpr uint32_t HEAD = 1u << 23;
+
+// get_valid_moves([d], mover) (narde.py:58-92 with one die: the head filter
+// is a no-op, a one-die list has at most one head entry)
+NARDE_FN uint32_t legal1(const Side& s, uint32_t low, int d) {
+  return die_filter(s.O, s.S1o, block_info_low(s.O, low), die_candidates(s.O, s.P, d), d);
+}
+
+NARDE_FN void apply_die(Side& s, int p, int d) { apply_move(s, p, p - d < 0 ? OFF : p - d); }
+
+// can N more sub-moves of die d be played (hl head moves still allowed)?
+template <int N>
+NARDE_FN bool f4_reach(const Side& s, uint32_t low, int d, int hl) {
+  uint32_t L = legal1(s, low, d);
+  if (hl <= 0) L &= ~HEAD;
+  if constexpr (N == 1) {
+    return L != 0u;
+  } else {
+    while (L) {
+      const int p = __builtin_ctz(L);
+      L &= L - 1u;
+      Side c = s;
+      apply_die(c, p, d);
+      if (f4_reach<N - 1>(c, low, d, hl - (p == 23 ? 1 : 0))) return true;
+    }
+    return false;
+  }
+}
+
+// the sources of L (die d) after which NEED more sub-moves stay playable
+template <int NEED>
+NARDE_FN uint32_t f4_keep(const Side& s, uint32_t low, int d, int hl, uint32_t L) {
+  if constexpr (NEED == 0) {
+    return L;
+  } else {
+    uint32_t C = 0u, m = L;
+    while (m) {
+      const int p = __builtin_ctz(m);
+      m &= m - 1u;
+      Side c = s;
+      apply_die(c, p, d);
+      C |= f4_reach<NEED>(c, low, d, hl - (p == 23 ? 1 : 0)) ? (1u << p) : 0u;
+    }
+    return C;
+  }
+}
+
+NARDE_FN uint32_t f4_keep_rt(const Side& s, uint32_t low, int d, int hl, uint32_t L, int need) {
+  switch (need) {
+    case 1: return f4_keep<1>(s, low, d, hl, L);
+    case 2: return f4_keep<2>(s, low, d, hl, L);
+    case 3: return f4_keep<3>(s, low, d, hl, L);
+    default: return L;
+  }
+}
+
+// two different dice: the first sub-move's options of die a whose child can
+// still play die b (a head move used up the turn's single head move)
+NARDE_FN uint32_t f4_keep_pair(const Side& s, uint32_t low, int a, int b, uint32_t L) {
+  uint32_t C = 0u, m = L;
+  while (m) {
+    const int p = __builtin_ctz(m);
+    m &= m - 1u;
+    Side c = s;
+    apply_die(c, p, a);
+    uint32_t L2 = legal1(c, low, b);
+    if (p == 23) L2 &= ~HEAD;
+    C |= L2 ? (1u << p) : 0u;
+  }
+  return C;
+}
+
+struct TurnOut {
+  uint64_t legal;   // C_0: C_hi | C_lo<<24 | d_hi<<48 | d_lo<<52 | M<<56
+  uint64_t played;  // byte 2k = from, 2k+1 = die of sub-move k; 0xFF = none
+  int max_dice;
+  int reward;
+  int term;
+};
+
+NARDE_FN uint64_t played_set(uint64_t pl, int k, int p, int d) {
+  const int sh = 16 * k;
+  return (pl & ~(0xFFFFull << sh)) | ((uint64_t)(((uint32_t)d << 8) | (uint32_t)p) << sh);
+}
+
+// One FULL4 turn with dice (d0, d1).  play == nullptr: sub-move k is entry
+// mulhi(w[k], |C_k|) of C_k (the random-legal policy); else play = int8
+// (from, die)[4] and sub-moves are applied while each is in C_k (the first
+// one that is not ends the turn -- illegal actions are ignored, as in
+// narde_env.py:56-93).  Then _check_game_ended and the flip (narde_env.py:
+// 95-103, 134-141).
+NARDE_FN void env_turn_full(Side& s, int d0, int d1, const int8_t* play, const uint32_t w[4],
+                            TurnOut& o) {
+  const uint32_t low = block_lowmask(s.P);
+  const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
+  uint64_t played = ~0ull;
+  int M = 0;
+  if (dh != dl) {
+    const uint32_t Lh = legal1(s, low, dh), Ll = legal1(s, low, dl);
+    uint32_t Ch = f4_keep_pair(s, low, dh, dl, Lh);
+    uint32_t Cl = f4_keep_pair(s, low, dl, dh, Ll);
+    if (Ch | Cl) {
+      M = 2;
+    } else {
+      M = (Lh | Ll) ? 1 : 0;
+      Ch = Lh;              // only one die playable: the higher one if it can
+      Cl = Lh ? 0u : Ll;
+    }
+    o.legal = (uint64_t)Ch | ((uint64_t)Cl << 24) | ((uint64_t)dh << 48) | ((uint64_t)dl << 52) |
+              ((uint64_t)M << 56);
+    if (M >= 1) {
+      const int nh = __builtin_popcount(Ch), n = nh + __builtin_popcount(Cl);
+      int p, d;
+      bool ok;
+      if (play) {
+        p = play[0];
+        d = play[1];
+        ok = p >= 0 && p < 24 && ((d == dh && ((Ch >> p) & 1u)) || (d == dl && ((Cl >> p) & 1u)));
+      } else {
+        const int idx = (int)mulhi_u32(w[0], (uint32_t)n);
+        const bool hi = idx < nh;
+        d = hi ? dh : dl;
+        p = select_bit(hi ? Ch : Cl, hi ? idx : idx - nh);
+        ok = true;
+      }
+      if (ok) {
+        apply_die(s, p, d);
+        played = played_set(played, 0, p, d);
+        if (M == 2) {
+          const int d2 = d == dh ? dl : dh;
+          uint32_t L2 = legal1(s, low, d2);
+          if (p == 23) L2 &= ~HEAD;
+          int p2;
+          bool ok2;
+          if (play) {
+            p2 = play[2];
+            ok2 = play[3] == d2 && p2 >= 0 && p2 < 24 && ((L2 >> p2) & 1u);
+          } else {
+            p2 = select_bit(L2, (int)mulhi_u32(w[1], (uint32_t)__builtin_popcount(L2)));
+            ok2 = true;
+          }
+          if (ok2) {
+            apply_die(s, p2, d2);
+            played = played_set(played, 1, p2, d2);
+          }
+        }
+      }
+    }
+  } else {
+    const int d = dh;
+    int hl = (s.ft_own && (d == 3 || d == 4 || d == 6)) ? 2 : 1;
+    uint32_t L = legal1(s, low, d);
+    uint32_t C = 0u;
+    if (L) {
+      C = f4_keep<3>(s, low, d, hl, L);
+      M = 4;
+      if (!C) { C = f4_keep<2>(s, low, d, hl, L); M = 3; }
+      if (!C) { C = f4_keep<1>(s, low, d, hl, L); M = 2; }
+      if (!C) { C = L; M = 1; }
+    }
+    o.legal = (uint64_t)C | ((uint64_t)d << 48) | ((uint64_t)d << 52) | ((uint64_t)M << 56);
+    for (int k = 0; k < M; ++k) {
+      if (k > 0) {
+        L = legal1(s, low, d);
+        if (hl <= 0) L &= ~HEAD;
+        C = f4_keep_rt(s, low, d, hl, L, M - k - 1);
+      }
+      int p;
+      if (play) {
+        p = play[2 * k];
+        if (!(play[2 * k + 1] == d && p >= 0 && p < 24 && ((C >> p) & 1u))) break;
+      } else {
+        p = select_bit(C, (int)mulhi_u32(w[k], (uint32_t)__builtin_popcount(C)));
+      }
+      apply_die(s, p, d);
+      hl -= p == 23 ? 1 : 0;
+      played = played_set(played, k, p, d);
+    }
+  }
+  o.played = played;
+  o.max_dice = M;
+  o.term = s.off_own == 15u;
+  o.reward = o.term ? (s.off_opp > 0u ? 1 : 2) : 0;
+  if (!o.term) side_flip(s);
+}
+
 // obs = get_perspective_board(current_player) (narde.py:31-34): int32[24]
 NARDE_FN int obs_point(const Side& s, int p) { return (int)nib_get(s.own, p) - (int)nib_get(s.opp, p); }
 
@@ -553,6 +754,41 @@ NARDE_FN void env_ply(Side& s, int4& st, const uint32_t r[4], bool have_dice, in
   if (!have_dice) dice_from(r[0], dice_mode, d0, d1);
   const uint32_t mover_black = s.black;
   env_step(s, d0, d1, c1, c2, policy, r[1], r[2], o);
+  s.elapsed += 1u;
+  term = o.term;
+  trunc = max_steps > 0 && s.elapsed >= (uint32_t)max_steps;
+  if (term | trunc) {
+    st.x += 1;
+    if (term) {
+      if (mover_black) st.z += o.reward;
+      else st.y += o.reward;
+    }
+    if (autoreset) {
+      const uint32_t t = s.t;
+      s = side_reset(r[3]);
+      s.t = t;
+    }
+  }
+  s.t += 1u;
+}
+
+// One FULL4 ply: env_ply with a whole turn per step.  Pick words w = {r1,
+// r2, q0, q1}, q = Philox4x32-10(ctr = {t, env, 0, 2}) drawn only on doubles
+// (the only turns with more than two sub-moves).
+NARDE_FN void env_ply_full(Side& s, int4& st, const uint32_t r[4], uint32_t env, uint32_t k0,
+                           uint32_t k1, bool have_dice, int d0, int d1, int dice_mode,
+                           const int8_t* play, int max_steps, bool autoreset, TurnOut& o, int& term,
+                           int& trunc) {
+  if (!have_dice) dice_from(r[0], dice_mode, d0, d1);
+  uint32_t w[4] = {r[1], r[2], 0u, 0u};
+  if (d0 == d1 && !play) {
+    uint32_t q[4];
+    philox4x32_10(s.t, env, 0u, 2u, k0, k1, q);
+    w[2] = q[0];
+    w[3] = q[1];
+  }
+  const uint32_t mover_black = s.black;
+  env_turn_full(s, d0, d1, play, w, o);
   s.elapsed += 1u;
   term = o.term;
   trunc = max_steps > 0 && s.elapsed >= (uint32_t)max_steps;

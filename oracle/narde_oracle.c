@@ -36,6 +36,8 @@
 #define OR_OFF 24
 #define OR_MAXM 64
 
+static uint32_t mulhi_n(uint32_t r, uint32_t n) { return (uint32_t)(((uint64_t)r * n) >> 32); }
+
 typedef struct {
     int32_t board[24]; /* absolute: white > 0, black < 0 */
     int32_t off_w, off_b;
@@ -341,6 +343,134 @@ void or_step_batch(int64_t n, int8_t *board, uint8_t *off, uint8_t *ft, int8_t *
     }
 }
 
+/* ================= FULL4 rules mode (build extension) =================
+ * Whole turns with 4-move doubles and the max-dice-used rule (SURVEY.md
+ * section 8 row f-2; spec README.md:27-30).  The reference env never plays
+ * them, so the composition rule is the build's; every
+ * sub-move is the reference's own single-die primitive: or_get_valid_moves
+ * with ONE die (narde.py:58-92 incl. the block filter :139-184) applied with
+ * or_execute_rotated_move (narde.py:36-56).  Pinned to tests/golden/full4.npz
+ * (tools/capture_full4.py: the same composition over the imported
+ * reference's Narde objects).
+ *   D = [a]*4 if a == b else [max, min];  H = 2 if first_turn and a == b in
+ *   {3,4,6} else 1 (narde.py:94-106's condition) = head moves allowed;
+ *   options = (v, p) for each distinct remaining die v descending, each entry
+ *   of get_valid_moves([v]) ascending, except a head move beyond H;
+ *   M = max sub-moves over all sequences; C_k = options whose child still
+ *   reaches M; two different dice with M == 1: the higher die if it has an
+ *   option; sub-move k plays entry mulhi(w[k], |C_k|) of C_k.
+ */
+typedef struct { int32_t v, from, to; } or_opt;
+
+static int or_f4_options(const or_state *s, const int32_t *R, int nR, int h, int H, or_opt *opt) {
+    int vals[4], nv = 0;
+    for (int i = 0; i < nR; ++i) {
+        int dup = 0;
+        for (int j = 0; j < nv; ++j) dup |= vals[j] == R[i];
+        if (!dup) vals[nv++] = R[i];
+    }
+    for (int i = 1; i < nv; ++i)
+        for (int j = i; j > 0 && vals[j] > vals[j - 1]; --j) { int t = vals[j]; vals[j] = vals[j - 1]; vals[j - 1] = t; }
+    int no = 0;
+    for (int i = 0; i < nv; ++i) {
+        int32_t die = vals[i], list[OR_MAXM][2];
+        int c = or_get_valid_moves(s->board, s->ft_w, s->ft_b, &die, 1, s->player, list);
+        for (int k = 0; k < c; ++k) {
+            if (list[k][0] == 23 && h >= H) continue;
+            opt[no].v = die; opt[no].from = list[k][0]; opt[no].to = list[k][1]; no++;
+        }
+    }
+    return no;
+}
+
+static void or_f4_child(const or_state *s, const int32_t *R, int nR, int h, const or_opt *o,
+                        or_state *c, int32_t *R2, int *nR2, int *h2) {
+    *c = *s;
+    or_execute_rotated_move(c, o->from, o->to, s->player);
+    int removed = 0, n = 0;
+    for (int i = 0; i < nR; ++i) {
+        if (!removed && R[i] == o->v) { removed = 1; continue; }
+        R2[n++] = R[i];
+    }
+    *nR2 = n;
+    *h2 = h + (o->from == 23);
+}
+
+static int or_f4_depth(const or_state *s, const int32_t *R, int nR, int h, int H) {
+    if (nR == 0) return 0;
+    or_opt opt[64];
+    int no = or_f4_options(s, R, nR, h, H, opt), best = 0;
+    for (int i = 0; i < no && best < nR; ++i) {
+        or_state c; int32_t R2[4]; int nR2, h2;
+        or_f4_child(s, R, nR, h, &opt[i], &c, R2, &nR2, &h2);
+        int d = 1 + or_f4_depth(&c, R2, nR2, h2, H);
+        if (d > best) best = d;
+    }
+    return best;
+}
+
+/* One FULL4 turn of the mover, in place.  cm[k][0/1] = C_k source masks of
+ * the higher/lower die (doubles: column 0); played[k] = (from, die), -1 pad. */
+static int or_full4_turn(or_state *s, const int32_t dice[2], const uint32_t w[4],
+                         uint32_t cm[4][2], int8_t played[4][2]) {
+    int32_t a = dice[0], b = dice[1], hi = a > b ? a : b, lo = a > b ? b : a;
+    int32_t R[4];
+    int nR;
+    if (a == b) { R[0] = R[1] = R[2] = R[3] = a; nR = 4; }
+    else { R[0] = hi; R[1] = lo; nR = 2; }
+    int ft = s->player == 1 ? s->ft_w : s->ft_b;
+    int H = (ft && a == b && (a == 3 || a == 4 || a == 6)) ? 2 : 1, h = 0;
+    int M = or_f4_depth(s, R, nR, h, H);
+    for (int k = 0; k < 4; ++k) { cm[k][0] = cm[k][1] = 0; played[k][0] = played[k][1] = -1; }
+    for (int k = 0; k < M; ++k) {
+        or_opt opt[64], C[64];
+        int no = or_f4_options(s, R, nR, h, H, opt), nc = 0;
+        for (int i = 0; i < no; ++i) {
+            or_state c; int32_t R2[4]; int nR2, h2;
+            or_f4_child(s, R, nR, h, &opt[i], &c, R2, &nR2, &h2);
+            if (or_f4_depth(&c, R2, nR2, h2, H) == M - k - 1) C[nc++] = opt[i];
+        }
+        if (k == 0 && M == 1 && a != b) {
+            int any_hi = 0;
+            for (int i = 0; i < nc; ++i) any_hi |= C[i].v == hi;
+            if (any_hi) {
+                int m = 0;
+                for (int i = 0; i < nc; ++i) if (C[i].v == hi) C[m++] = C[i];
+                nc = m;
+            }
+        }
+        if (nc == 0) return M; /* unreachable: C_k is non-empty below M */
+        for (int i = 0; i < nc; ++i) cm[k][C[i].v == hi ? 0 : 1] |= 1u << C[i].from;
+        const or_opt *o = &C[mulhi_n(w[k], (uint32_t)nc)];
+        played[k][0] = (int8_t)o->from; played[k][1] = (int8_t)o->v;
+        or_state c; int32_t R2[4]; int nR2, h2;
+        or_f4_child(s, R, nR, h, o, &c, R2, &nR2, &h2);
+        *s = c; memcpy(R, R2, sizeof R2); nR = nR2; h = h2;
+    }
+    return M;
+}
+
+/* FULL4 turns over a batch with given dice and pick words; state updated in
+ * place (no player flip: the caller sees the post-turn board). */
+void or_full4_batch(int64_t n, int8_t *board, uint8_t *off, uint8_t *ft, const int8_t *player,
+                    const uint8_t *dice, const uint32_t *words, int8_t *max_dice, uint32_t *cmask,
+                    int8_t *played, int8_t *reward, uint8_t *done) {
+    for (int64_t i = 0; i < n; ++i) {
+        or_state s;
+        load_state(&s, board + i * 24, off + i * 2, ft + i * 2, player[i]);
+        int32_t d[2] = {dice[i * 2], dice[i * 2 + 1]};
+        uint32_t cm[4][2];
+        int8_t pl[4][2];
+        max_dice[i] = (int8_t)or_full4_turn(&s, d, words + i * 4, cm, pl);
+        memcpy(cmask + i * 8, cm, sizeof cm);
+        memcpy(played + i * 8, pl, sizeof pl);
+        int dn, rw;
+        or_check_game_ended(&s, &dn, &rw);
+        reward[i] = (int8_t)rw; done[i] = (uint8_t)dn;
+        store_state(&s, board + i * 24, off + i * 2, ft + i * 2, NULL);
+    }
+}
+
 /* 198-float Tesauro-style observation, README.md:42-102 (spec only; the
  * reference has no implementation -> parity unpinned).  Absolute points,
  * white block [0..97], black block [98..195], player one-hot [196..197]. */
@@ -388,7 +518,6 @@ void or_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
-static uint32_t mulhi_n(uint32_t r, uint32_t n) { return (uint32_t)(((uint64_t)r * n) >> 32); }
 
 /* dice_mode 0: all 36 ordered pairs; 1: the 30 non-double ordered pairs. */
 static void or_dice_from(uint32_t r, int dice_mode, int32_t d[2]) {
@@ -480,6 +609,80 @@ void or_selfplay(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int plies,
             if (dice_out) { dice_out[ix * 2] = (uint8_t)d[0]; dice_out[ix * 2 + 1] = (uint8_t)d[1]; }
             if (action_out) { action_out[ix * 2] = (int16_t)o.code1; action_out[ix * 2 + 1] = (int16_t)o.code2; }
             if (count1_out) count1_out[ix] = (int16_t)o.count1;
+        }
+        store_state(&s, board + i * 24, off + i * 2, ft + i * 2, player + i);
+        elapsed[i] = (uint16_t)s.elapsed;
+    }
+}
+
+
+/*
+ * FULL4 self-play driver restatement: as or_selfplay
+ * with a whole FULL4 turn per step.  Pick words w = {r1, r2, q0, q1} with
+ * q = Philox4x32-10(ctr = {t, e, 0, 2}) (drawn on doubles only).  Per-ply
+ * outputs (optional): obs, reward, terminated, truncated, dice, legal u64
+ * (C_0 masks | d_hi<<48 | d_lo<<52 | M<<56), played u64 (bytes 2k/2k+1 =
+ * from/die of sub-move k, 0xFF = none).
+ */
+void or_selfplay_full(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int plies,
+                      int dice_mode, int max_steps,
+                      int8_t *board, uint8_t *off, uint8_t *ft, int8_t *player, uint16_t *elapsed,
+                      int32_t *stats,
+                      int8_t *obs, int8_t *reward, uint8_t *terminated, uint8_t *truncated,
+                      uint8_t *dice_out, uint64_t *legal_out, uint64_t *played_out) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    for (int64_t i = 0; i < n; ++i) {
+        or_state s;
+        load_state(&s, board + i * 24, off + i * 2, ft + i * 2, player[i]);
+        s.elapsed = elapsed[i];
+        for (int p = 0; p < plies; ++p) {
+            uint32_t ctr[4] = {t0 + (uint32_t)p, (uint32_t)(env0 + i), 0, 0}, r[4];
+            or_philox4x32_10(ctr, key, r);
+            int32_t d[2];
+            or_dice_from(r[0], dice_mode, d);
+            uint32_t w[4] = {r[1], r[2], 0, 0};
+            if (d[0] == d[1]) {
+                uint32_t c2[4] = {t0 + (uint32_t)p, (uint32_t)(env0 + i), 0, 2}, q[4];
+                or_philox4x32_10(c2, key, q);
+                w[2] = q[0]; w[3] = q[1];
+            }
+            int mover = s.player;
+            uint32_t cm[4][2];
+            int8_t pl[4][2];
+            int M = or_full4_turn(&s, d, w, cm, pl);
+            int term, rew;
+            or_check_game_ended(&s, &term, &rew);
+            if (!term) s.player = -s.player;
+            s.elapsed += 1;
+            int trunc = max_steps > 0 && s.elapsed >= max_steps;
+            if (term) {
+                stats[i * 3 + 0] += 1;
+                stats[i * 3 + (mover == 1 ? 1 : 2)] += rew;
+            } else if (trunc) {
+                stats[i * 3 + 0] += 1;
+            }
+            if (term || trunc) or_reset_state(&s, r[3]);
+            int64_t ix = (int64_t)p * n + i;
+            if (obs) {
+                int32_t o[24];
+                or_perspective(&s, s.player, o);
+                for (int k = 0; k < 24; ++k) obs[ix * 24 + k] = (int8_t)o[k];
+            }
+            if (reward) reward[ix] = (int8_t)rew;
+            if (terminated) terminated[ix] = (uint8_t)term;
+            if (truncated) truncated[ix] = (uint8_t)trunc;
+            if (dice_out) { dice_out[ix * 2] = (uint8_t)d[0]; dice_out[ix * 2 + 1] = (uint8_t)d[1]; }
+            if (legal_out) {
+                uint32_t hi = d[0] > d[1] ? d[0] : d[1], lo = d[0] > d[1] ? d[1] : d[0];
+                legal_out[ix] = (uint64_t)cm[0][0] | ((uint64_t)cm[0][1] << 24) |
+                                ((uint64_t)hi << 48) | ((uint64_t)lo << 52) | ((uint64_t)M << 56);
+            }
+            if (played_out) {
+                uint64_t v = 0;
+                for (int k = 0; k < 4; ++k)
+                    v |= (uint64_t)(((uint32_t)(uint8_t)pl[k][1] << 8) | (uint8_t)pl[k][0]) << (16 * k);
+                played_out[ix] = v;
+            }
         }
         store_state(&s, board + i * 24, off + i * 2, ft + i * 2, player + i);
         elapsed[i] = (uint16_t)s.elapsed;

@@ -103,6 +103,27 @@ def step(board, off, ft, player, dice, action, with_lists=True):
                 roll2=roll2)
 
 
+def full4_turn(board, off, ft, player, dice, words):
+    """FULL4 turns with given dice and pick words.
+    Returns post-turn state (no flip) + max_dice, cmask [n,4,2] (C_k source
+    masks of the higher / lower die), played [n,4,2] (from, die), reward, done."""
+    board = _c(board, np.int8).copy()
+    off = _c(off, np.uint8).copy()
+    ft = _c(ft, np.uint8).copy()
+    player = _c(player, np.int8)
+    n = board.shape[0]
+    M = np.empty(n, np.int8)
+    cm = np.empty((n, 4, 2), np.uint32)
+    played = np.empty((n, 4, 2), np.int8)
+    reward = np.empty(n, np.int8)
+    done = np.empty(n, np.uint8)
+    lib().or_full4_batch(ctypes.c_int64(n), _p(board), _p(off), _p(ft), _p(player),
+                         _p(_c(dice, np.uint8)), _p(_c(words, np.uint32)), _p(M), _p(cm),
+                         _p(played), _p(reward), _p(done))
+    return dict(board=board, off=off, first_turn=ft, max_dice=M, cmask=cm, played=played,
+                reward=reward, done=done)
+
+
 def tesauro198(board, off, player):
     board = _c(board, np.int8)
     n = board.shape[0]
@@ -162,4 +183,31 @@ class SelfPlay:
         if record:
             return dict(obs=obs, reward=reward, terminated=term, truncated=trunc, dice=dice,
                         action=action, count1=count1)
+        return None
+
+
+    def run_full(self, plies, record=True):
+        """FULL4 self-play, same state as run()."""
+        n = self.n
+        if record:
+            obs = np.empty((plies, n, 24), np.int8)
+            reward = np.empty((plies, n), np.int8)
+            term = np.empty((plies, n), np.uint8)
+            trunc = np.empty((plies, n), np.uint8)
+            dice = np.empty((plies, n, 2), np.uint8)
+            legal = np.empty((plies, n), np.uint64)
+            played = np.empty((plies, n), np.uint64)
+        else:
+            obs = reward = term = trunc = dice = legal = played = None
+        lib().or_selfplay_full(ctypes.c_int64(n), ctypes.c_int64(self.env0),
+                               ctypes.c_uint64(self.seed), ctypes.c_uint32(self.t),
+                               ctypes.c_int(plies), ctypes.c_int(self.dice_mode),
+                               ctypes.c_int(self.max_steps), _p(self.board), _p(self.off),
+                               _p(self.ft), _p(self.player), _p(self.elapsed), _p(self.stats),
+                               _p(obs), _p(reward), _p(term), _p(trunc), _p(dice), _p(legal),
+                               _p(played))
+        self.t += plies
+        if record:
+            return dict(obs=obs, reward=reward, terminated=term, truncated=trunc, dice=dice,
+                        legal=legal, played=played)
         return None

@@ -120,4 +120,67 @@ void hc_selfplay(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int plies,
   }
 }
 
+// FULL4 turns with given dice and pick words (mirror of or_full4_batch):
+// post-turn state without the flip, C_0 compact, played sub-moves.
+void hc_full4_batch(int64_t n, int8_t* board, uint8_t* off, uint8_t* ft, const int8_t* player,
+                    const uint8_t* dice, const uint32_t* words, uint64_t* legal, uint64_t* played,
+                    int8_t* reward, uint8_t* done) {
+  for (int64_t i = 0; i < n; ++i) {
+    Side s = load(board + i * 24, off + 2 * i, ft + 2 * i, player[i], 0);
+    TurnOut o;
+    env_turn_full(s, dice[2 * i], dice[2 * i + 1], nullptr, words + 4 * i, o);
+    if (!o.term) side_flip(s);  // undo the flip: compare the mover's post-turn board
+    legal[i] = o.legal;
+    played[i] = o.played;
+    reward[i] = (int8_t)o.reward;
+    done[i] = (uint8_t)o.term;
+    store(s, board + i * 24, off + 2 * i, ft + 2 * i, nullptr, nullptr);
+  }
+}
+
+// FULL4 turns with explicit plays int8 (from, die)[4] (the narde_step_full
+// action path).
+void hc_full4_play_batch(int64_t n, int8_t* board, uint8_t* off, uint8_t* ft, int8_t* player,
+                         const uint8_t* dice, const int8_t* play, uint64_t* played) {
+  for (int64_t i = 0; i < n; ++i) {
+    Side s = load(board + i * 24, off + 2 * i, ft + 2 * i, player[i], 0);
+    TurnOut o;
+    const uint32_t w[4] = {0, 0, 0, 0};
+    env_turn_full(s, dice[2 * i], dice[2 * i + 1], play + 8 * i, w, o);
+    played[i] = o.played;
+    store(s, board + i * 24, off + 2 * i, ft + 2 * i, player + i, nullptr);
+  }
+}
+
+void hc_selfplay_full(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int plies, int dice_mode,
+                      int max_steps, int8_t* board, uint8_t* off, uint8_t* ft, int8_t* player,
+                      uint16_t* elapsed, int32_t* stats, int8_t* obs, int8_t* reward, uint8_t* term,
+                      uint8_t* trunc, uint64_t* legal_out, uint64_t* played_out) {
+  for (int64_t i = 0; i < n; ++i) {
+    Side s = load(board + i * 24, off + 2 * i, ft + 2 * i, player[i], elapsed[i]);
+    s.t = t0;
+    int4 st = make_int4(0, 0, 0, 0);
+    for (int p = 0; p < plies; ++p) {
+      uint32_t r[4];
+      draw(seed, s.t, (uint32_t)(env0 + i), 0u, r);
+      TurnOut o;
+      int tm, tr;
+      env_ply_full(s, st, r, (uint32_t)(env0 + i), (uint32_t)seed, (uint32_t)(seed >> 32), false, 0,
+                   0, dice_mode, nullptr, max_steps, true, o, tm, tr);
+      const int64_t ix = (int64_t)p * n + i;
+      if (obs)
+        for (int q = 0; q < 24; ++q) obs[ix * 24 + q] = (int8_t)obs_point(s, q);
+      if (reward) reward[ix] = (int8_t)o.reward;
+      if (term) term[ix] = (uint8_t)tm;
+      if (trunc) trunc[ix] = (uint8_t)tr;
+      if (legal_out) legal_out[ix] = o.legal;
+      if (played_out) played_out[ix] = o.played;
+    }
+    stats[3 * i] += st.x;
+    stats[3 * i + 1] += st.y;
+    stats[3 * i + 2] += st.z;
+    store(s, board + i * 24, off + 2 * i, ft + 2 * i, player + i, elapsed + i);
+  }
+}
+
 }  // extern "C"

@@ -1,0 +1,182 @@
+"""FULL4 rules mode (4-move doubles + max dice used) on CPU.
+
+1. The C oracle's composition (oracle/narde_oracle.c or_full4_turn) against
+   tests/golden/full4.npz, which tools/capture_full4.py made by composing the
+   imported reference's own primitives (Narde.get_valid_moves([die]) and
+   execute_rotated_move, narde.py:36-92) -- parity of every sub-move is
+   pinned to the reference; the whole-turn rule is the build's (the
+   reference env never plays 4 moves: narde_env.py:45-93).
+2. The test-only host build of the device engine (tests/hostcheck, the same
+   narde_rules.h the HIP kernels compile) against the same fixtures, the
+   explicit-play path, and the oracle's FULL4 self-play driver.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+from conftest import golden
+
+import oracle as O
+
+P = lambda a: a.ctypes.data_as(ctypes.c_void_p) if a is not None else None  # noqa: E731
+
+
+def compact_c0(d):
+    """golden C_0 masks + dice + M -> the device's u64 legal word."""
+    hi = np.maximum(d["dice"][:, 0], d["dice"][:, 1]).astype(np.uint64)
+    lo = np.minimum(d["dice"][:, 0], d["dice"][:, 1]).astype(np.uint64)
+    c = d["cmask"][:, 0, :].astype(np.uint64)
+    return (c[:, 0] | (c[:, 1] << np.uint64(24)) | (hi << np.uint64(48)) | (lo << np.uint64(52))
+            | (d["max_dice"].astype(np.uint64) << np.uint64(56)))
+
+
+def played_u64(played):
+    """[n,4,2] int8 (from, die) -> u64 (bytes 2k, 2k+1)."""
+    b = played.astype(np.uint8).astype(np.uint64)
+    v = np.zeros(len(played), np.uint64)
+    for k in range(4):
+        v |= (b[:, k, 0] | (b[:, k, 1] << np.uint64(8))) << np.uint64(16 * k)
+    return v
+
+
+def test_oracle_full4_golden():
+    d = golden("full4.npz")
+    r = O.full4_turn(d["board"], d["off"], d["ft"], d["player"], d["dice"], d["words"])
+    assert np.array_equal(r["max_dice"], d["max_dice"])
+    assert np.array_equal(r["cmask"], d["cmask"])
+    assert np.array_equal(r["played"], d["played"])
+    assert np.array_equal(r["board"], d["board_after"])
+    assert np.array_equal(r["off"], d["off_after"])
+    assert np.array_equal(r["first_turn"], d["ft_after"])
+    assert np.array_equal(r["reward"], d["reward"])
+    assert np.array_equal(r["done"], d["done"])
+
+
+def test_full4_golden_coverage():
+    d = golden("full4.npz")
+    M = d["max_dice"]
+    dbl = d["dice"][:, 0] == d["dice"][:, 1]
+    assert set(np.unique(M).tolist()) == {0, 1, 2, 3, 4}
+    assert ((M == 4) & dbl).sum() > 1000 and ((M == 3) & dbl).sum() > 100
+    # the higher-die rule (two dice, only one playable, the higher one can)
+    one = (M == 1) & ~dbl
+    assert one.sum() > 50
+    # two head moves on a first-turn 6-6 / 4-4 / 3-3
+    heads = (d["played"][:, :, 0] == 23).sum(1)
+    assert (heads == 2).any() and heads.max() <= 2
+    assert d["done"].sum() > 100
+
+
+def test_full4_known_answers():
+    """Start position turns: hand-checked FULL4 answers."""
+    d = golden("full4.npz")
+    start = (d["board"][:, 23] == 15) & (d["board"][:, 11] == -15) & (d["ft"] == 1).all(1)
+    idx = np.nonzero(start)[0]
+    by_roll = {}
+    for i in idx:
+        by_roll.setdefault((int(d["player"][i]), *map(int, d["dice"][i])), i)
+    for pl in (1, -1):
+        # 6-6 first turn: two head checkers to 17; 17->11 is blocked by the
+        # opponent's head, so only 2 of the 4 dice can be used
+        i = by_roll[(pl, 6, 6)]
+        assert d["max_dice"][i] == 2
+        assert d["played"][i][:2].tolist() == [[23, 6], [23, 6]]
+        # 4-4 first turn: 23->19 twice, then 19->15 twice (4 dice)
+        i = by_roll[(pl, 4, 4)]
+        assert d["max_dice"][i] == 4
+        # 5-5: only one head move (5-5 is not a head exception), then that
+        # checker moves on: 23->18->13->8 (13 is empty: the opponent is on 11)
+        i = by_roll[(pl, 5, 5)]
+        assert d["max_dice"][i] == 4 and (d["played"][i][:, 0] == 23).sum() == 1
+        # 6-5 from the start: one head move, then the same checker continues
+        i = by_roll[(pl, 6, 5)]
+        assert d["max_dice"][i] == 2
+
+
+def test_hostcheck_full4_golden(hostcheck):
+    d = golden("full4.npz")
+    n = len(d["dice"])
+    b, off, ft = d["board"].copy(), d["off"].copy(), d["ft"].copy()
+    legal = np.empty(n, np.uint64)
+    played = np.empty(n, np.uint64)
+    rw = np.empty(n, np.int8)
+    dn = np.empty(n, np.uint8)
+    hostcheck.hc_full4_batch(ctypes.c_int64(n), P(b), P(off), P(ft), P(d["player"]), P(d["dice"]),
+                             P(np.ascontiguousarray(d["words"])), P(legal), P(played), P(rw), P(dn))
+    assert np.array_equal(legal, compact_c0(d))
+    assert np.array_equal(played, played_u64(d["played"]))
+    assert np.array_equal(b, d["board_after"])
+    assert np.array_equal(off, d["off_after"])
+    assert np.array_equal(ft, d["ft_after"])
+    assert np.array_equal(rw, d["reward"]) and np.array_equal(dn, d["done"])
+
+
+def test_hostcheck_full4_explicit_play(hostcheck):
+    """Replaying the golden plays as explicit actions gives the same turn;
+    an illegal sub-move ends the turn there (actions are never forced)."""
+    d = golden("full4.npz")
+    n = len(d["dice"])
+    b, off, ft, pl = d["board"].copy(), d["off"].copy(), d["ft"].copy(), d["player"].copy()
+    played = np.empty(n, np.uint64)
+    play = np.ascontiguousarray(d["played"])
+    hostcheck.hc_full4_play_batch(ctypes.c_int64(n), P(b), P(off), P(ft), P(pl), P(d["dice"]),
+                                  P(play), P(played))
+    assert np.array_equal(played, played_u64(d["played"]))
+    assert np.array_equal(off, d["off_after"])
+    # truncate every play after its first sub-move with a bogus second one
+    bad = play.copy()
+    bad[:, 1:, :] = -1
+    bad[:, 1, 0] = 30
+    b2, off2, ft2, pl2 = d["board"].copy(), d["off"].copy(), d["ft"].copy(), d["player"].copy()
+    hostcheck.hc_full4_play_batch(ctypes.c_int64(n), P(b2), P(off2), P(ft2), P(pl2), P(d["dice"]),
+                                  P(bad), P(played))
+    first = played_u64(d["played"]) & np.uint64(0xFFFF)
+    assert np.array_equal(played & np.uint64(0xFFFF), first)
+    assert ((played >> np.uint64(16)) == np.uint64(0xFFFFFFFFFFFF)).all()
+
+
+@pytest.mark.parametrize("dice_mode", [0, 1])
+def test_hostcheck_selfplay_full_vs_oracle(hostcheck, dice_mode):
+    n, plies, seed, env0 = 384, 300, 0x5EED0F11, 77
+    sp = O.SelfPlay(n, seed=seed, env0=env0, dice_mode=dice_mode, max_steps=1000)
+    sp.reset(0)
+    ro = sp.run_full(plies)
+    b = np.zeros((n, 24), np.int8)
+    off = np.zeros((n, 2), np.uint8)
+    ft = np.zeros((n, 2), np.uint8)
+    pl = np.zeros(n, np.int8)
+    el = np.zeros(n, np.uint16)
+    st = np.zeros((n, 3), np.int32)
+    hostcheck.hc_reset_batch(ctypes.c_int64(n), ctypes.c_int64(env0), ctypes.c_uint64(seed),
+                             ctypes.c_uint32(0), P(b), P(off), P(ft), P(pl), P(el))
+    out = {k: np.empty_like(v) for k, v in ro.items() if k != "dice"}
+    hostcheck.hc_selfplay_full(ctypes.c_int64(n), ctypes.c_int64(env0), ctypes.c_uint64(seed),
+                               ctypes.c_uint32(0), ctypes.c_int(plies), ctypes.c_int(dice_mode),
+                               ctypes.c_int(1000), P(b), P(off), P(ft), P(pl), P(el), P(st),
+                               P(out["obs"]), P(out["reward"]), P(out["terminated"]),
+                               P(out["truncated"]), P(out["legal"]), P(out["played"]))
+    for k in out:
+        assert np.array_equal(out[k], ro[k]), k
+    assert np.array_equal(st, sp.stats) and np.array_equal(b, sp.board)
+    assert sp.stats[:, 0].sum() > 0
+    if dice_mode == 0:
+        M = (ro["legal"] >> np.uint64(56)).astype(np.int64)
+        assert (M == 4).any() and (M == 3).any()
+
+
+def test_oracle_full4_selfplay_invariants():
+    n = 256
+    sp = O.SelfPlay(n, seed=3, max_steps=100)
+    sp.reset(0)
+    r = sp.run_full(400)
+    assert r["terminated"].any() and r["truncated"].any()
+    w = np.where(sp.board > 0, sp.board, 0).sum(1) + sp.off[:, 0]
+    k = np.where(sp.board < 0, -sp.board, 0).sum(1) + sp.off[:, 1]
+    assert (w == 15).all() and (k == 15).all()
+    # the number of sub-moves played equals max dice used, every ply
+    M = (r["legal"] >> np.uint64(56)).astype(np.int64)
+    nplayed = sum(((r["played"] >> np.uint64(16 * k)) & np.uint64(0xFF)) != np.uint64(0xFF)
+                  for k in range(4))
+    assert np.array_equal(nplayed.astype(np.int64), M)
+    # FULL4 games are shorter than REF2 ones (doubles move 4 checkers)
+    assert sp.stats[:, 0].sum() > 0

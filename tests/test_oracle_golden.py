@@ -205,3 +205,4 @@ def test_oracle_tesauro_bounds():
     cnt = w[..., 0] + w[..., 1] + w[..., 2] + 2 * w[..., 3]
     assert np.array_equal(cnt.astype(np.int64), np.where(d["post_board"] > 0, d["post_board"], 0))
     random.seed(0)
+
