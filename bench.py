@@ -34,10 +34,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 # actions 4 = 114 B; per env and launch the 32-B record read + written = 64 B
 OUT_BYTES_PER_STEP = 114
 RECORD_BYTES = 64
+# FULL4: the same per-ply outputs with the 8-B played
+# sub-moves instead of the 4-B action codes = 118 B
+OUT_BYTES_PER_STEP_FULL = 118
 
 
-def launch_bytes(envs, plies):
-    return envs * (OUT_BYTES_PER_STEP * plies + RECORD_BYTES)
+def launch_bytes(envs, plies, full=False):
+    return envs * ((OUT_BYTES_PER_STEP_FULL if full else OUT_BYTES_PER_STEP) * plies + RECORD_BYTES)
 
 
 def _port_worker(args):
@@ -114,6 +117,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--cpu-cores", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--rules", choices=("ref2", "full4"), default="ref2",
+                    help="rules of the timed path (value); the other mode is reported beside it")
+    ap.add_argument("--other-launches", type=int, default=20,
+                    help="k_rollout launches of the other rules mode, timed beside the headline")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_k_rollout.json"))
     args = ap.parse_args()
 
@@ -133,7 +140,9 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     first, per = D.env_shard(world * args.envs, rank, world)
-    env = VecNardeEnv(per, device=dev, seed=args.seed, env_id_offset=first, max_episode_steps=1000)
+    full = args.rules == "full4"
+    env = VecNardeEnv(per, device=dev, seed=args.seed, env_id_offset=first, max_episode_steps=1000,
+                      rules=args.rules)
 
     def barrier():
         if world > 1:
@@ -225,10 +234,41 @@ def main():
     torch.cuda.synchronize()
     fused = per * F * args.fused_launches / (time.perf_counter() - f0)
 
+    # secondary 3: the other rules mode through the same rollout kernel shape
+    other_rules = "ref2" if full else "full4"
+    env_o = VecNardeEnv(per, device=dev, seed=args.seed, env_id_offset=first, max_episode_steps=1000,
+                        rules=other_rules)
+    bufs_o = env_o.rollout_buffers(P)
+    env_o.rollout(P, bufs_o)
+    env_o.rollout(P, bufs_o)
+    torch.cuda.synchronize()
+    ev_o = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            for _ in range(args.other_launches)]
+    o0 = time.perf_counter()
+    for s_, e_ in ev_o:
+        s_.record()
+        env_o.rollout(P, bufs_o)
+        e_.record()
+    torch.cuda.synchronize()
+    other_rate = per * P * args.other_launches / (time.perf_counter() - o0)
+    other_ms = sum(s_.elapsed_time(e_) for s_, e_ in ev_o) / len(ev_o)
+    other_M = None
+    if other_rules == "full4":
+        M = ((bufs_o["legal"] >> 56) & 7).flatten()
+        other_M = [round(float(x), 4) for x in (torch.bincount(M, minlength=5).double() / M.numel()).tolist()]
+    env_o.close()
+
     if rank == 0:
-        nbytes = launch_bytes(per, P)
+        nbytes = launch_bytes(per, P, full)
         achieved = nbytes / (kern_ms * 1e-3) / 1e9
-        traffic = load_traffic(args.traffic_json, per, P)
+        traffic = load_traffic(args.traffic_json, per, P) if not full else None
+        obytes = launch_bytes(per, P, not full)
+        rules_txt = {
+            "ref2": ("reference NardeEnv.step (REF2: <=2 checker moves per step, also on doubles; "
+                     "legal sets bit-exact vs the reference)"),
+            "full4": ("FULL4 whole turns (4-move doubles, max dice used, higher-die rule; DESIGN.md "
+                      "section 10; every sub-move is the reference's single-die primitive)"),
+        }
         line = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -243,12 +283,12 @@ def main():
             "dtype": "u32",
             "data": "synthetic (Philox dice, random legal policy, start position + auto-reset)",
             "config": {
-                "workload": ("configs[2]: batch=65536 random-policy self-play per GPU; rules = "
-                             "reference NardeEnv.step (REF2: <=2 checker moves per step, also on "
-                             "doubles); dice uniform over 36 ordered pairs; TimeLimit 1000; every "
-                             "ply writes obs/reward/terminated/truncated/legal set/actions for "
-                             "every env"),
-                "kernel": f"k_rollout, {P} plies per launch",
+                "workload": (f"configs[2]: batch=65536 random-policy self-play per GPU; rules = "
+                             f"{rules_txt[args.rules]}; dice uniform over 36 ordered pairs; "
+                             f"TimeLimit 1000; every ply writes obs/reward/terminated/truncated/"
+                             f"legal set/actions for every env"),
+                "rules": args.rules,
+                "kernel": f"k_rollout<{'full' if full else 'ref2'}>, {P} plies per launch",
                 "envs_per_gpu": per,
                 "global_envs": world * per,
                 "parallelism": f"dp{world} (env-id shards, 1 RCCL all-gather of stats)",
@@ -256,7 +296,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_rollout",
+                "kernel": f"k_rollout<true, {'true' if full else 'false'}>",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -272,7 +312,20 @@ def main():
                 "hipgraph": round(api_graph, 1),
                 "unit": "env steps/s",
                 "kernel_ms": round(step_ms, 5),
-                "achieved_GBps": round((OUT_BYTES_PER_STEP + RECORD_BYTES) * per / (step_ms * 1e-3) / 1e9, 2),
+                "achieved_GBps": round(((OUT_BYTES_PER_STEP_FULL if full else OUT_BYTES_PER_STEP) + RECORD_BYTES)
+                                       * per / (step_ms * 1e-3) / 1e9, 2),
+            },
+            "other_rules": {
+                "rules": other_rules,
+                "workload": rules_txt[other_rules],
+                "kernel": f"k_rollout<{'full' if other_rules == 'full4' else 'ref2'}>, {P} plies per launch, all outputs",
+                "value": round(other_rate, 1),
+                "unit": "env steps/s",
+                "kernel_ms": round(other_ms, 5),
+                "bytes_per_launch": obytes,
+                "achieved_GBps": round(obytes / (other_ms * 1e-3) / 1e9, 2),
+                "frac": round(obytes / (other_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                "max_dice_hist": other_M,
             },
             "selfplay_stats_only": {
                 "kernel": f"k_rollout without per-ply outputs, {F} plies per launch",

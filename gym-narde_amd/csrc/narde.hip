@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <type_traits>
 
 #include "../../include/narde.h"
 #include "narde_rules.h"
@@ -171,14 +172,40 @@ __global__ void __launch_bounds__(kBlock) k_legal(Planes pl, int n, Rng g,
   }
 }
 
+// FULL4 first-sub-move set C_0 and max dice M for the given (or the next
+// device) dice: the turn engine run on a copy with a play whose first
+// sub-move is invalid, so nothing is applied.
+__global__ void __launch_bounds__(kBlock) k_legal_full(Planes pl, int n, Rng g,
+                                                       const uint8_t* __restrict__ dice2,
+                                                       uint64_t* __restrict__ out) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  Side s = side_from_record(pl.p0[i], pl.p1[i]);
+  int d0, d1;
+  if (dice2) {
+    d0 = dice2[2 * i];
+    d1 = dice2[2 * i + 1];
+  } else {
+    uint32_t r[4];
+    draw(g, s.t, (uint32_t)i, 0u, r);
+    dice_from(r[0], g.dice_mode, d0, d1);
+  }
+  const int8_t none[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
+  const uint32_t w[4] = {0u, 0u, 0u, 0u};
+  TurnOut o;
+  env_turn_full(s, d0, d1, none, w, o);
+  out[i] = o.legal;
+}
+
 // per-ply outputs; a rollout writes ply p of env i at [p * n + i]
 struct Outs {
   int32_t* __restrict__ obs;      // [.][n][24]
   int32_t* __restrict__ reward;   // [.][n]
   uint8_t* __restrict__ term;     // [.][n]
   uint8_t* __restrict__ trunc;    // [.][n]
-  uint64_t* __restrict__ legal;   // [.][n] compact list #1
-  int16_t* __restrict__ act_out;  // [.][n][2]
+  uint64_t* __restrict__ legal;   // [.][n] compact list #1 (FULL4: C_0 | M<<56)
+  int16_t* __restrict__ act_out;  // [.][n][2] REF2 codes used
+  uint64_t* __restrict__ played;  // [.][n] FULL4 sub-moves (from, die) x 4
 };
 
 struct StepArgs {
@@ -187,7 +214,8 @@ struct StepArgs {
   Rng g;
   int max_steps;
   int autoreset;
-  const int16_t* __restrict__ actions;
+  const int16_t* __restrict__ actions;  // REF2: i16[n][2] codes
+  const int8_t* __restrict__ play;      // FULL4: i8[n][4][2] (from, die)
   const uint8_t* __restrict__ dice;
   Outs out;
 };
@@ -245,20 +273,33 @@ __device__ __forceinline__ void store_obs_wave(int32_t* __restrict__ obs, size_t
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ void store_outs(const Outs& out, size_t ix, const Side& s,
-                                           const StepOut& o, int term, int trunc, int4* lds,
-                                           bool wave_full) {
+__device__ __forceinline__ void store_common(const Outs& out, size_t ix, const Side& s, int reward,
+                                             int term, int trunc, int4* lds, bool wave_full) {
   if (out.obs) {
     if (NARDE_OBS_STORE != 0 && wave_full) store_obs_wave(out.obs, ix, s, lds);
     else store_obs(out.obs, ix, s);
   }
-  if (out.reward) st_out(out.reward + ix, (int32_t)o.reward);
+  if (out.reward) st_out(out.reward + ix, (int32_t)reward);
   if (out.term) st_out(out.term + ix, (uint8_t)term);
   if (out.trunc) st_out(out.trunc + ix, (uint8_t)trunc);
+}
+
+__device__ __forceinline__ void store_outs(const Outs& out, size_t ix, const Side& s,
+                                           const StepOut& o, int term, int trunc, int4* lds,
+                                           bool wave_full) {
+  store_common(out, ix, s, o.reward, term, trunc, lds, wave_full);
   if (out.legal) st_out(out.legal + ix, (uint64_t)compact_legal(o.l1));
   if (out.act_out)
     st_out(reinterpret_cast<uint32_t*>(out.act_out) + ix,
            ((uint32_t)(uint16_t)o.code1) | ((uint32_t)(uint16_t)o.code2 << 16));
+}
+
+__device__ __forceinline__ void store_outs(const Outs& out, size_t ix, const Side& s,
+                                           const TurnOut& o, int term, int trunc, int4* lds,
+                                           bool wave_full) {
+  store_common(out, ix, s, o.reward, term, trunc, lds, wave_full);
+  if (out.legal) st_out(out.legal + ix, o.legal);
+  if (out.played) st_out(out.played + ix, o.played);
 }
 
 // this wave's slice of the block's obs staging buffer (6 KiB per wave)
@@ -280,6 +321,18 @@ __device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t i,
           autoreset, o, term, trunc);
 }
 
+// one FULL4 ply (a whole turn per step)
+__device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t i, const int8_t* play,
+                                    const uint8_t* dice, int max_steps, bool autoreset, TurnOut& o,
+                                    int& term, int& trunc) {
+  uint32_t r[4];
+  draw(g, s.t, i, 0u, r);
+  int d0 = 0, d1 = 0;
+  if (dice) { d0 = dice[2 * i]; d1 = dice[2 * i + 1]; }
+  env_ply_full(s, st, r, g.env0 + i, g.k0, g.k1, dice != nullptr, d0, d1, g.dice_mode,
+               play ? play + 8 * (size_t)i : nullptr, max_steps, autoreset, o, term, trunc);
+}
+
 __device__ __forceinline__ void add_stats(int4* __restrict__ stats, int i, const int4& st) {
   if (st.x) {
     int4 cur = stats[i];
@@ -288,16 +341,21 @@ __device__ __forceinline__ void add_stats(int4* __restrict__ stats, int i, const
   }
 }
 
-// NardeEnv.step for every env (API step; one ply of self-play when actions == NULL)
+// NardeEnv.step for every env (API step; one ply of self-play when the
+// actions are NULL).  kFull: FULL4 whole turns (TurnOut), else REF2 (StepOut).
+template <bool kFull>
 __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
   OBS_LDS_DECL
   const int i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= a.n) return;
   Side s = side_from_record(a.pl.p0[i], a.pl.p1[i]);
   int4 st = make_int4(0, 0, 0, 0);
-  StepOut o;
+  typename std::conditional<kFull, TurnOut, StepOut>::type o;
   int term, trunc;
-  ply(s, st, a.g, (uint32_t)i, a.actions, a.dice, a.max_steps, a.autoreset != 0, o, term, trunc);
+  if constexpr (kFull)
+    ply(s, st, a.g, (uint32_t)i, a.play, a.dice, a.max_steps, a.autoreset != 0, o, term, trunc);
+  else
+    ply(s, st, a.g, (uint32_t)i, a.actions, a.dice, a.max_steps, a.autoreset != 0, o, term, trunc);
   uint4 ra, rb;
   side_to_record(s, ra, rb);
   a.pl.p0[i] = ra;
@@ -310,7 +368,7 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
 // record stays in VGPRs, each ply's outputs (if requested) are streamed to
 // [ply][n] rollout buffers.  kOut = false: statistics only (a separate
 // instantiation, so profiles tell the two apart).
-template <bool kOut>
+template <bool kOut, bool kFull>
 __global__ void __launch_bounds__(kBlock) k_rollout(Planes pl, int n, Rng g, int plies, int max_steps,
                                                     Outs out) {
   OBS_LDS_DECL
@@ -320,9 +378,12 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Planes pl, int n, Rng g, int
   Side s = side_from_record(pl.p0[i], pl.p1[i]);
   int4 st = make_int4(0, 0, 0, 0);
   for (int p = 0; p < plies; ++p) {
-    StepOut o;
+    typename std::conditional<kFull, TurnOut, StepOut>::type o;
     int term, trunc;
-    ply(s, st, g, (uint32_t)i, nullptr, nullptr, max_steps, true, o, term, trunc);
+    if constexpr (kFull)
+      ply(s, st, g, (uint32_t)i, (const int8_t*)nullptr, nullptr, max_steps, true, o, term, trunc);
+    else
+      ply(s, st, g, (uint32_t)i, (const int16_t*)nullptr, nullptr, max_steps, true, o, term, trunc);
     if (kOut) store_outs(out, (size_t)p * n + i, s, o, term, trunc, wave_lds, wave_full);
   }
   uint4 ra, rb;
@@ -652,9 +713,29 @@ int narde_step(narde_env* e, const int16_t* actions, const uint8_t* dice, int32_
   a.autoreset = autoreset;
   a.actions = actions;
   a.dice = dice;
-  a.out = Outs{obs, reward, terminated, truncated, legal_compact, actions_out};
-  k_step<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(a);
+  a.play = nullptr;
+  a.out = Outs{obs, reward, terminated, truncated, legal_compact, actions_out, nullptr};
+  k_step<false><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(a);
   return check_launch("k_step");
+}
+
+int narde_step_full(narde_env* e, const int8_t* play, const uint8_t* dice, int32_t* obs, int32_t* reward,
+                    uint8_t* terminated, uint8_t* truncated, uint64_t* legal_first, uint64_t* played,
+                    int autoreset, void* stream) {
+  if (!e) return fail(NARDE_EINVAL, "NULL handle");
+  DeviceGuard dg(e->device);
+  StepArgs a;
+  a.pl = e->pl;
+  a.n = (int)e->n;
+  a.g = rng_of(e);
+  a.max_steps = e->max_steps;
+  a.autoreset = autoreset;
+  a.actions = nullptr;
+  a.play = play;
+  a.dice = dice;
+  a.out = Outs{obs, reward, terminated, truncated, legal_first, nullptr, played};
+  k_step<true><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(a);
+  return check_launch("k_step<full>");
 }
 
 int narde_rollout(narde_env* e, int plies, int32_t* obs, int32_t* reward, uint8_t* terminated,
@@ -662,19 +743,47 @@ int narde_rollout(narde_env* e, int plies, int32_t* obs, int32_t* reward, uint8_
   if (!e || plies < 0) return fail(NARDE_EINVAL, "bad argument");
   if (plies == 0) return NARDE_OK;
   DeviceGuard dg(e->device);
-  const Outs out{obs, reward, terminated, truncated, legal_compact, actions_out};
+  const Outs out{obs, reward, terminated, truncated, legal_compact, actions_out, nullptr};
   const bool any = obs || reward || terminated || truncated || legal_compact || actions_out;
   if (any)
-    k_rollout<true><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), plies,
-                                                                   e->max_steps, out);
+    k_rollout<true, false><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e),
+                                                                          plies, e->max_steps, out);
   else
-    k_rollout<false><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), plies,
-                                                                    e->max_steps, out);
+    k_rollout<false, false><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e),
+                                                                           plies, e->max_steps, out);
   return check_launch("k_rollout");
 }
 
 int narde_selfplay(narde_env* e, int plies, void* stream) {
   return narde_rollout(e, plies, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+int narde_rollout_full(narde_env* e, int plies, int32_t* obs, int32_t* reward, uint8_t* terminated,
+                       uint8_t* truncated, uint64_t* legal_first, uint64_t* played, void* stream) {
+  if (!e || plies < 0) return fail(NARDE_EINVAL, "bad argument");
+  if (plies == 0) return NARDE_OK;
+  DeviceGuard dg(e->device);
+  const Outs out{obs, reward, terminated, truncated, legal_first, nullptr, played};
+  const bool any = obs || reward || terminated || truncated || legal_first || played;
+  if (any)
+    k_rollout<true, true><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e),
+                                                                         plies, e->max_steps, out);
+  else
+    k_rollout<false, true><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e),
+                                                                          plies, e->max_steps, out);
+  return check_launch("k_rollout<full>");
+}
+
+int narde_selfplay_full(narde_env* e, int plies, void* stream) {
+  return narde_rollout_full(e, plies, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
+}
+
+int narde_legal_full(narde_env* e, const uint8_t* dice, uint64_t* legal_first, void* stream) {
+  if (!e || !legal_first) return fail(NARDE_EINVAL, "NULL argument");
+  DeviceGuard dg(e->device);
+  k_legal_full<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), dice,
+                                                               legal_first);
+  return check_launch("k_legal_full");
 }
 
 int narde_get_stats(narde_env* e, int32_t* stats, void* stream) {
@@ -821,8 +930,9 @@ int narde_host_step(narde_env* e, int64_t n, int8_t* board, uint8_t* off, uint8_
   a.autoreset = 0;
   a.actions = da;
   a.dice = dd;
-  a.out = Outs{dobs, dr, dt, nullptr, nullptr, nullptr};
-  k_step<<<grid(n), kBlock, 0, e->hstream>>>(a);
+  a.play = nullptr;
+  a.out = Outs{dobs, dr, dt, nullptr, nullptr, nullptr, nullptr};
+  k_step<false><<<grid(n), kBlock, 0, e->hstream>>>(a);
   k_get_state<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, db2, doff2, dft2, dp2, nullptr);
   if ((rc = check_launch("host step"))) return rc;
   HIP_TRY(hipMemcpyAsync(e->h_out, e->d_out, dq.off, hipMemcpyDeviceToHost, e->hstream));

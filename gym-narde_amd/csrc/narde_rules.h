@@ -40,8 +40,12 @@ struct Nib {
 // (hi:lo) >> 16, low 32 bits: one v_alignbit_b32 on gfx950
 NARDE_FN uint32_t funnel16(uint32_t hi, uint32_t lo) { return (lo >> 16) | (hi << 16); }
 
+// (value selects, never an address computed from p: a select between the
+// words' addresses would keep the record out of VGPRs, in scratch)
 NARDE_FN uint32_t nib_word(const Nib& b, int p) {
-  return p < 8 ? b.w[0] : (p < 16 ? b.w[1] : b.w[2]);
+  const uint32_t w0 = b.w[0], w1 = b.w[1], w2 = b.w[2];
+  const int k = p >> 3;
+  return (k == 0 ? w0 : 0u) | (k == 1 ? w1 : 0u) | (k == 2 ? w2 : 0u);
 }
 NARDE_FN uint32_t nib_get(const Nib& b, int p) { return (nib_word(b, p) >> (4 * (p & 7))) & 15u; }
 NARDE_FN void nib_add(Nib& b, int p, uint32_t delta /* +1 or 0xFFFFFFFF */) {
@@ -684,7 +688,9 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, const int8_t* play, const u
         p = play[2 * k];
         if (!(play[2 * k + 1] == d && p >= 0 && p < 24 && ((C >> p) & 1u))) break;
       } else {
-        p = select_bit(C, (int)mulhi_u32(w[k], (uint32_t)__builtin_popcount(C)));
+        // w[k] with a runtime k as selects (a dynamic index would put w in scratch)
+        const uint32_t wk = k == 0 ? w[0] : (k == 1 ? w[1] : (k == 2 ? w[2] : w[3]));
+        p = select_bit(C, (int)mulhi_u32(wk, (uint32_t)__builtin_popcount(C)));
       }
       apply_die(s, p, d);
       hl -= p == 23 ? 1 : 0;

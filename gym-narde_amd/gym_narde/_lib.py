@@ -39,6 +39,10 @@ SIGNATURES = {
     "narde_step": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
     "narde_rollout": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "narde_selfplay": (_i32, [_vp, _i32, _vp]),
+    "narde_step_full": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
+    "narde_rollout_full": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "narde_selfplay_full": (_i32, [_vp, _i32, _vp]),
+    "narde_legal_full": (_i32, [_vp, _vp, _vp, _vp]),
     "narde_get_stats": (_i32, [_vp, _vp, _vp]),
     "narde_apply_moves": (_i32, [_vp, _vp, _vp, _vp]),
     "narde_observe": (_i32, [_vp, _vp, _vp, _vp]),

@@ -11,6 +11,14 @@ Dice of ply t for global env e are Philox4x32-10({t, e, 0, 0}, seed), so
 `step()` will use (the reference's callers peek/roll their own dice instead,
 train_deepq_pytorch.py:866).  Actions are the reference's codes
 (from*24 + to, (from<=5, to==0) = bear-off).
+
+rules="ref2" (default) is the reference's NardeEnv.step: at most two checker
+moves per step, quirks included.  rules="full4" is the build's whole-turn
+mode (include/narde.h): four sub-moves on doubles, max
+dice used, the higher die when only one can be used.  Its actions are plays,
+(B,4,2) int8 (from, die) sub-moves; info["legal"] is the first sub-move's
+set with the max dice usable in bits 56-58, info["played"] the sub-moves
+played (bytes 2k/2k+1 = from/die, 0xFF unused).
 """
 import ctypes
 
@@ -19,6 +27,7 @@ import numpy as np
 from . import _lib
 
 DICE_MODES = {"all36": _lib.DICE_ALL36, "nodoubles": _lib.DICE_NODOUBLES}
+RULES = ("ref2", "full4")
 
 
 def decode_compact(compact):
@@ -40,10 +49,39 @@ def decode_compact(compact):
     return out if np.ndim(compact) else out[0]
 
 
+def decode_full_legal(word):
+    """FULL4 legal word (u64) -> (max_dice, [(from, die), ...]) in list
+    order (higher die first, ascending source)."""
+    c = int(np.uint64(word))
+    ch, cl = c & 0xFFFFFF, (c >> 24) & 0xFFFFFF
+    dh, dl, m = (c >> 48) & 0xF, (c >> 52) & 0xF, (c >> 56) & 0x7
+    opts = [(p, dh) for p in range(24) if (ch >> p) & 1]
+    if dl != dh:
+        opts += [(p, dl) for p in range(24) if (cl >> p) & 1]
+    return m, opts
+
+
+def decode_played(word):
+    """FULL4 played word (u64) -> [(from, die), ...] sub-moves in order."""
+    c = int(np.uint64(word))
+    out = []
+    for k in range(4):
+        f, d = (c >> (16 * k)) & 0xFF, (c >> (16 * k + 8)) & 0xFF
+        if f == 0xFF:
+            break
+        out.append((f, d))
+    return out
+
+
 class VecNardeEnv:
     def __init__(self, num_envs, device=None, seed=0, env_id_offset=0, dice_mode="all36",
-                 max_episode_steps=1000, autoreset=True):
+                 max_episode_steps=1000, autoreset=True, rules="ref2"):
         import torch
+
+        if rules not in RULES:
+            raise ValueError(f"rules must be one of {RULES}")
+        self.rules = rules
+        self.full = rules == "full4"
 
         self.torch = torch
         dev = torch.device(device if device is not None else "cuda")
@@ -64,6 +102,7 @@ class VecNardeEnv:
         self.truncated = torch.zeros(B, dtype=torch.uint8, **z)
         self.legal = torch.zeros(B, dtype=torch.int64, **z)
         self.actions_used = torch.zeros((B, 2), dtype=torch.int16, **z)
+        self.played = torch.zeros(B, dtype=torch.int64, **z)
 
     # ------------------------------------------------------------ plumbing
     def _s(self):
@@ -133,12 +172,33 @@ class VecNardeEnv:
         self.handle.call("narde_legal_mask576", _lib.ptr(out), self._s())
         return out
 
-    def step(self, actions=None, dice=None):
-        """NardeEnv.step for all envs.  actions (B,2) codes or None for the
-        in-kernel random legal policy; dice (B,2) or None for device dice.
-        Returns (obs, reward, terminated, truncated, info) device tensors;
-        info = {'legal': compact list #1, 'actions': codes used}."""
+    def legal_full(self, dice=None):
+        """FULL4: (B,) int64 legal words (first sub-move set | max dice << 56)
+        for dice (B,2) or the next step's device dice."""
         B = self.num_envs
+        d = None if dice is None else self._dev(dice, self.torch.uint8, (B, 2))
+        out = self.torch.empty(B, dtype=self.torch.int64, device=self.device)
+        self.handle.call("narde_legal_full", _lib.ptr(d), _lib.ptr(out), self._s())
+        return out
+
+    def step(self, actions=None, dice=None):
+        """NardeEnv.step for all envs.  actions (B,2) codes (rules="full4":
+        (B,4,2) int8 (from, die) plays) or None for the in-kernel random
+        legal policy; dice (B,2) or None for device dice.  Returns (obs,
+        reward, terminated, truncated, info) device tensors; info =
+        {'legal': compact list #1, 'actions': codes used} (rules="full4":
+        {'legal': first sub-move set + max dice, 'played': sub-moves})."""
+        B = self.num_envs
+        if self.full:
+            a = None if actions is None else self._dev(actions, self.torch.int8, (B, 4, 2))
+            d = None if dice is None else self._dev(dice, self.torch.uint8, (B, 2))
+            self.handle.call("narde_step_full", _lib.ptr(a), _lib.ptr(d), _lib.ptr(self.obs),
+                             _lib.ptr(self.reward), _lib.ptr(self.terminated),
+                             _lib.ptr(self.truncated), _lib.ptr(self.legal), _lib.ptr(self.played),
+                             int(self.autoreset), self._s())
+            self._keep = (a, d)
+            return (self.obs, self.reward, self.terminated, self.truncated,
+                    {"legal": self.legal, "played": self.played})
         a = None if actions is None else self._dev(actions, self.torch.int16, (B, 2))
         d = None if dice is None else self._dev(dice, self.torch.uint8, (B, 2))
         self.handle.call("narde_step", _lib.ptr(a), _lib.ptr(d), _lib.ptr(self.obs),
@@ -150,17 +210,20 @@ class VecNardeEnv:
 
     def selfplay(self, plies):
         """plies plies of random-legal self-play in ONE launch (statistics only)."""
-        self.handle.call("narde_selfplay", int(plies), self._s())
+        self.handle.call("narde_selfplay_full" if self.full else "narde_selfplay", int(plies),
+                         self._s())
 
     def rollout_buffers(self, plies, obs=True, reward=True, terminated=True, truncated=True,
                         legal=True, actions=True):
-        """Allocate [plies][B] rollout buffers for rollout()."""
+        """Allocate [plies][B] rollout buffers for rollout() (rules="full4":
+        'actions' holds the played sub-moves, (plies, B) int64)."""
         t, B, dev = self.torch, self.num_envs, self.device
         mk = lambda on, shape, dt: t.empty(shape, dtype=dt, device=dev) if on else None  # noqa: E731
+        act = mk(actions, (plies, B), t.int64) if self.full else mk(actions, (plies, B, 2), t.int16)
         return dict(obs=mk(obs, (plies, B, 24), t.int32), reward=mk(reward, (plies, B), t.int32),
                     terminated=mk(terminated, (plies, B), t.uint8),
                     truncated=mk(truncated, (plies, B), t.uint8),
-                    legal=mk(legal, (plies, B), t.int64), actions=mk(actions, (plies, B, 2), t.int16))
+                    legal=mk(legal, (plies, B), t.int64), actions=act)
 
     def rollout(self, plies, bufs=None):
         """plies plies of random-legal self-play (auto-reset) in ONE launch,
@@ -171,7 +234,8 @@ class VecNardeEnv:
         for v in bufs.values():
             if v is not None and v.shape[0] < plies:
                 raise ValueError("rollout buffer shorter than plies")
-        self.handle.call("narde_rollout", int(plies), _lib.ptr(bufs["obs"]), _lib.ptr(bufs["reward"]),
+        self.handle.call("narde_rollout_full" if self.full else "narde_rollout", int(plies),
+                         _lib.ptr(bufs["obs"]), _lib.ptr(bufs["reward"]),
                          _lib.ptr(bufs["terminated"]), _lib.ptr(bufs["truncated"]),
                          _lib.ptr(bufs["legal"]), _lib.ptr(bufs["actions"]), self._s())
         return bufs

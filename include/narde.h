@@ -132,6 +132,36 @@ int narde_rollout(narde_env *env, int plies, int32_t *obs, int32_t *reward, uint
 /* narde_rollout with no per-ply outputs (statistics only). */
 int narde_selfplay(narde_env *env, int plies, void *stream);
 
+/* ---- FULL4 rules mode (build extension) -------------
+ * One step = the mover's WHOLE turn: four sub-moves on doubles, the
+ * max-dice-used rule, the higher die when only one of two dice can be used,
+ * at most one checker off the head per turn (two on a first-turn 3-3, 4-4 or
+ * 6-6).  Every sub-move is the reference's single-die primitive
+ * (Narde.get_valid_moves([die]) narde.py:58-92, execute_rotated_move
+ * narde.py:36-56); the reference env itself stops after two checker moves
+ * (narde_env.py:45-93), so whole-turn parity is against the build's oracle,
+ * which is pinned sub-move by sub-move to the reference (tests/golden/full4.npz).
+ * A sub-move is (from, die), from in the mover's perspective; the landing
+ * point is from - die, or 'off' when negative.
+ *   legal_first u64[B] = C_hi | C_lo<<24 | d_hi<<48 | d_lo<<52 | M<<56: the
+ *     sources playable as the FIRST sub-move with the higher / lower die
+ *     (doubles: C_lo = 0, d_lo = d_hi) and M = max dice usable (0..4).
+ *   played u64[B]: bytes 2k / 2k+1 = from / die of sub-move k, 0xFF unused.
+ *   play i8[B][4][2] (from, die): applied while each sub-move keeps M
+ *     reachable; the first one that does not ends the turn (illegal actions
+ *     are ignored, as in narde_env.py:56-93).  NULL = in-kernel random policy
+ *     (sub-move k uniform over its legal set). */
+int narde_step_full(narde_env *env, const int8_t *play, const uint8_t *dice, int32_t *obs,
+                    int32_t *reward, uint8_t *terminated, uint8_t *truncated,
+                    uint64_t *legal_first, uint64_t *played, int autoreset, void *stream);
+/* `plies` FULL4 random-policy turns per env in ONE launch (outputs [plies][B]). */
+int narde_rollout_full(narde_env *env, int plies, int32_t *obs, int32_t *reward,
+                       uint8_t *terminated, uint8_t *truncated, uint64_t *legal_first,
+                       uint64_t *played, void *stream);
+int narde_selfplay_full(narde_env *env, int plies, void *stream);
+/* C_0 and M for dice u8[B][2] (NULL = the next step's device dice). */
+int narde_legal_full(narde_env *env, const uint8_t *dice, uint64_t *legal_first, void *stream);
+
 /* Per-env statistics i32[B][3] = {episodes finished, white points, black
  * points} since the last reset of that env. */
 int narde_get_stats(narde_env *env, int32_t *stats, void *stream);

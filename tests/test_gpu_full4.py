@@ -1,0 +1,177 @@
+"""GPU parity of the FULL4 rules mode (whole turns: 4-move doubles, max dice
+used) through libnarde.so's C ABI.
+
+Against tests/golden/full4.npz (turns composed of the reference's own
+single-die primitives by tools/capture_full4.py) and against the C oracle's
+FULL4 self-play driver.  Bit-exact (integer work).  Whole-turn semantics have
+no reference arithmetic (the reference env stops after two checker moves,
+narde_env.py:45-93): parity of each sub-move is pinned, the composition rule
+is the build's.
+"""
+import numpy as np
+import pytest
+from conftest import golden
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def vec(n, **kw):
+    from gym_narde.vector import VecNardeEnv
+
+    return VecNardeEnv(n, device="cuda:0", rules="full4", **kw)
+
+
+def np_(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def golden_legal_word(d):
+    hi = np.maximum(d["dice"][:, 0], d["dice"][:, 1]).astype(np.uint64)
+    lo = np.minimum(d["dice"][:, 0], d["dice"][:, 1]).astype(np.uint64)
+    c = d["cmask"][:, 0, :].astype(np.uint64)
+    return (c[:, 0] | (c[:, 1] << np.uint64(24)) | (hi << np.uint64(48)) | (lo << np.uint64(52))
+            | (d["max_dice"].astype(np.uint64) << np.uint64(56)))
+
+
+def played_word(played):
+    b = played.astype(np.uint8).astype(np.uint64)
+    v = np.zeros(len(played), np.uint64)
+    for k in range(4):
+        v |= (b[:, k, 0] | (b[:, k, 1] << np.uint64(8))) << np.uint64(16 * k)
+    return v
+
+
+def set_golden(env, d):
+    env.set_state(torch.from_numpy(d["board"]), torch.from_numpy(d["off"]),
+                  torch.from_numpy(d["ft"]), torch.from_numpy(d["player"]))
+
+
+def test_full4_legal_first_golden():
+    d = golden("full4.npz")
+    env = vec(len(d["dice"]))
+    set_golden(env, d)
+    w = env.legal_full(torch.from_numpy(d["dice"]))
+    assert np.array_equal(np_(w).view(np.uint64), golden_legal_word(d))
+    # the query applies nothing
+    assert np.array_equal(np_(env.get_state()["board"]), d["board"])
+
+
+def test_full4_step_replays_golden_plays():
+    """Explicit plays = the golden sub-moves: same post-turn state."""
+    d = golden("full4.npz")
+    n = len(d["dice"])
+    env = vec(n, max_episode_steps=0, autoreset=False)
+    set_golden(env, d)
+    obs, rew, term, trunc, info = env.step(torch.from_numpy(d["played"]),
+                                           torch.from_numpy(d["dice"]))
+    assert np.array_equal(np_(info["legal"]).view(np.uint64), golden_legal_word(d))
+    assert np.array_equal(np_(info["played"]).view(np.uint64), played_word(d["played"]))
+    assert np.array_equal(np_(rew), d["reward"].astype(np.int32))
+    assert np.array_equal(np_(term), d["done"])
+    st = env.get_state()
+    assert np.array_equal(np_(st["board"]), d["board_after"])
+    assert np.array_equal(np_(st["off"]), d["off_after"])
+    assert np.array_equal(np_(st["first_turn"]), d["ft_after"])
+    # the mover flips unless the game ended (narde_env.py:96-100)
+    exp_player = np.where(d["done"] == 1, d["player"], -d["player"]).astype(np.int8)
+    assert np.array_equal(np_(st["player"]), exp_player)
+
+
+def test_full4_illegal_play_is_ignored():
+    d = golden("full4.npz")
+    n = len(d["dice"])
+    env = vec(n, max_episode_steps=0, autoreset=False)
+    set_golden(env, d)
+    bad = np.full((n, 4, 2), -1, np.int8)
+    bad[:, 0, 0] = 30  # not a point: the turn ends before any sub-move
+    _, _, term, _, info = env.step(torch.from_numpy(bad), torch.from_numpy(d["dice"]))
+    assert (np_(info["played"]).view(np.uint64) == np.uint64(0xFFFFFFFFFFFFFFFF)).all()
+    st = env.get_state()
+    assert np.array_equal(np_(st["board"]), d["board"])
+    assert not np_(term).any()
+
+
+@pytest.mark.parametrize("dice_mode,max_steps", [("all36", 1000), ("nodoubles", 1000), ("all36", 80)])
+def test_full4_selfplay_trajectory_vs_oracle(dice_mode, max_steps):
+    n, plies, seed, env0 = 4096, 200, 0xF4F4F4, 999
+    dm = 0 if dice_mode == "all36" else 1
+    env = vec(n, seed=seed, env_id_offset=env0, dice_mode=dice_mode, max_episode_steps=max_steps)
+    ref = O.SelfPlay(n, seed=seed, env0=env0, dice_mode=dm, max_steps=max_steps)
+    ref.reset(0)
+    rec = ref.run_full(plies)
+    for p in range(plies):
+        assert np.array_equal(np_(env.dice()), rec["dice"][p]), p
+        obs, rew, term, trunc, info = env.step()
+        assert np.array_equal(np_(obs), rec["obs"][p].astype(np.int32)), p
+        assert np.array_equal(np_(rew), rec["reward"][p].astype(np.int32)), p
+        assert np.array_equal(np_(term), rec["terminated"][p]), p
+        assert np.array_equal(np_(trunc), rec["truncated"][p]), p
+        assert np.array_equal(np_(info["legal"]).view(np.uint64), rec["legal"][p]), p
+        assert np.array_equal(np_(info["played"]).view(np.uint64), rec["played"][p]), p
+    st = env.get_state()
+    assert np.array_equal(np_(st["board"]), ref.board)
+    assert np.array_equal(np_(env.stats()), ref.stats)
+
+
+def test_full4_rollout_equals_steps():
+    """k_rollout<full> over launch boundaries == per-ply k_step<full>."""
+    n, seed = 2048, 31337
+    a = vec(n, seed=seed)
+    b = vec(n, seed=seed)
+    bufs = a.rollout_buffers(70)
+    got = {k: [] for k in bufs}
+    for plies in (1, 29, 70):
+        a.rollout(plies, bufs)
+        for k, v in bufs.items():
+            got[k].append(np_(v[:plies]).copy())
+    got = {k: np.concatenate(v) for k, v in got.items()}
+    for p in range(100):
+        obs, rew, term, trunc, info = b.step()
+        assert np.array_equal(got["obs"][p], np_(obs)), p
+        assert np.array_equal(got["reward"][p], np_(rew)), p
+        assert np.array_equal(got["terminated"][p], np_(term)), p
+        assert np.array_equal(got["truncated"][p], np_(trunc)), p
+        assert np.array_equal(got["legal"][p], np_(info["legal"])), p
+        assert np.array_equal(got["actions"][p], np_(info["played"])), p
+    assert np.array_equal(np_(a.stats()), np_(b.stats()))
+
+
+def test_full4_full_batch_window_and_invariants():
+    """B = 65,536 (the bench shape): a 2,048-env window equals the oracle run
+    on those global ids; checker conservation and played == max dice
+    everywhere."""
+    n, plies, seed = 65536, 120, 7
+    env = vec(n, seed=seed)
+    bufs = env.rollout_buffers(plies)
+    env.rollout(plies, bufs)
+    lo = 40000
+    ref = O.SelfPlay(2048, seed=seed, env0=lo)
+    ref.reset(0)
+    rec = ref.run_full(plies)
+    sl = slice(lo, lo + 2048)
+    assert np.array_equal(np_(bufs["obs"][:, sl]), rec["obs"].astype(np.int32))
+    assert np.array_equal(np_(bufs["legal"][:, sl]).view(np.uint64), rec["legal"])
+    assert np.array_equal(np_(bufs["actions"][:, sl]).view(np.uint64), rec["played"])
+    st = env.get_state()
+    b = np_(st["board"]).astype(np.int64)
+    off = np_(st["off"]).astype(np.int64)
+    assert ((np.where(b > 0, b, 0).sum(1) + off[:, 0]) == 15).all()
+    assert ((np.where(b < 0, -b, 0).sum(1) + off[:, 1]) == 15).all()
+    legal = np_(bufs["legal"]).view(np.uint64)
+    played = np_(bufs["actions"]).view(np.uint64)
+    M = (legal >> np.uint64(56)).astype(np.int64)
+    nplayed = sum((((played >> np.uint64(16 * k)) & np.uint64(0xFF)) != np.uint64(0xFF)).astype(np.int64)
+                  for k in range(4))
+    assert np.array_equal(nplayed, M)
+    assert (M == 4).mean() > 0.1

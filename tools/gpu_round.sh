@@ -30,9 +30,21 @@ timeout -k 10 420 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>
         -d "$OUT/pmc/write" -o pmc -- python3 "$ROOT/tools/pmc_target.py" > "$OUT/pmc_write.log" 2>&1) \
   && python3 tools/pmc_summary.py --fetch "$OUT/pmc/fetch" --write "$OUT/pmc/write" \
         --out "$OUT/pmc_k_rollout.json" \
+  && echo "[gpu_round] $(date +%T) pmc FETCH_SIZE full4" \
+  && (cd /tmp && timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+        -d "$OUT/pmc_full/fetch" -o pmc -- python3 "$ROOT/tools/pmc_target.py" --rules full4 \
+        > "$OUT/pmc_full_fetch.log" 2>&1) \
+  && echo "[gpu_round] $(date +%T) pmc WRITE_SIZE full4" \
+  && (cd /tmp && timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+        -d "$OUT/pmc_full/write" -o pmc -- python3 "$ROOT/tools/pmc_target.py" --rules full4 \
+        > "$OUT/pmc_full_write.log" 2>&1) \
+  && python3 tools/pmc_summary.py --fetch "$OUT/pmc_full/fetch" --write "$OUT/pmc_full/write" \
+        --kernel "k_rollout<true, true>" --bytes-per-ply 118 --out "$OUT/pmc_k_rollout_full.json" \
+  && echo "[gpu_round] $(date +%T) bench --rules full4" \
+  && timeout -k 10 300 python bench.py --rules full4 --no-cpu-baseline > "$OUT/bench_full4.json" 2> "$OUT/bench_full4.err" \
   && echo "[gpu_round] $(date +%T) done"
 rc=$?
 echo "[gpu_round] rc=$rc"
 tail -3 "$OUT/pytest_gpu.log" 2>/dev/null
-cat "$OUT/bench_n1.json" 2>/dev/null
+cat "$OUT/bench_n1.json" "$OUT/bench_full4.json" 2>/dev/null
 exit $rc

@@ -32,9 +32,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", required=True, help="dir of the FETCH_SIZE pass")
     ap.add_argument("--write", required=True, help="dir of the WRITE_SIZE pass")
-    ap.add_argument("--kernel", default="k_rollout<true>")
+    ap.add_argument("--kernel", default="k_rollout<true, false>")
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--plies", type=int, default=100)
+    ap.add_argument("--bytes-per-ply", type=int, default=114, help="114 REF2, 118 FULL4")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles",
                                                   "pmc_k_rollout.json"))
     a = ap.parse_args()
@@ -45,7 +46,7 @@ def main():
     f, w = f[1:], w[1:]
     fetch_kib = sum(f) / len(f)
     write_kib = sum(w) / len(w)
-    algo = a.envs * (114 * a.plies + 64)
+    algo = a.envs * (a.bytes_per_ply * a.plies + 64)
     hbm = (2 * fetch_kib + write_kib) * 1024
     out = {
         "kernel": a.kernel, "envs": a.envs, "plies": a.plies, "dispatches": len(f),

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""rocprofv3 --pmc target: k_rollout<true> at the bench shape.
+"""rocprofv3 --pmc target: k_rollout<true, *> at the bench shape.
 
 Runs `--launches` launches of `--plies` plies over `--envs` envs with every
 per-ply output written (exactly bench.py's timed kernel), after one warm-up
@@ -25,8 +25,9 @@ def main():
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--plies", type=int, default=100)
     ap.add_argument("--launches", type=int, default=5)
+    ap.add_argument("--rules", choices=("ref2", "full4"), default="ref2")
     a = ap.parse_args()
-    env = VecNardeEnv(a.envs, device="cuda:0", seed=0)
+    env = VecNardeEnv(a.envs, device="cuda:0", seed=0, rules=a.rules)
     bufs = env.rollout_buffers(a.plies)
     for _ in range(a.launches + 1):
         env.rollout(a.plies, bufs)
