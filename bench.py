@@ -121,7 +121,8 @@ def main():
                     help="rules of the timed path (value); the other mode is reported beside it")
     ap.add_argument("--other-launches", type=int, default=20,
                     help="k_rollout launches of the other rules mode, timed beside the headline")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_k_rollout.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC summary (tools/pmc_summary.py); default profiles/pmc_k_rollout[_full].json")
     args = ap.parse_args()
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -140,7 +141,7 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     first, per = D.env_shard(world * args.envs, rank, world)
-    full = args.rules == "full4"
+    is_full4 = args.rules == "full4"
     env = VecNardeEnv(per, device=dev, seed=args.seed, env_id_offset=first, max_episode_steps=1000,
                       rules=args.rules)
 
@@ -235,7 +236,7 @@ def main():
     fused = per * F * args.fused_launches / (time.perf_counter() - f0)
 
     # secondary 3: the other rules mode through the same rollout kernel shape
-    other_rules = "ref2" if full else "full4"
+    other_rules = "ref2" if is_full4 else "full4"
     env_o = VecNardeEnv(per, device=dev, seed=args.seed, env_id_offset=first, max_episode_steps=1000,
                         rules=other_rules)
     bufs_o = env_o.rollout_buffers(P)
@@ -259,10 +260,12 @@ def main():
     env_o.close()
 
     if rank == 0:
-        nbytes = launch_bytes(per, P, full)
+        nbytes = launch_bytes(per, P, is_full4)
         achieved = nbytes / (kern_ms * 1e-3) / 1e9
-        traffic = load_traffic(args.traffic_json, per, P) if not full else None
-        obytes = launch_bytes(per, P, not full)
+        tj = args.traffic_json or os.path.join(
+            ROOT, "profiles", "pmc_k_rollout_full.json" if is_full4 else "pmc_k_rollout.json")
+        traffic = load_traffic(tj, per, P)
+        obytes = launch_bytes(per, P, not is_full4)
         rules_txt = {
             "ref2": ("reference NardeEnv.step (REF2: <=2 checker moves per step, also on doubles; "
                      "legal sets bit-exact vs the reference)"),
@@ -288,7 +291,7 @@ def main():
                              f"TimeLimit 1000; every ply writes obs/reward/terminated/truncated/"
                              f"legal set/actions for every env"),
                 "rules": args.rules,
-                "kernel": f"k_rollout<{'full' if full else 'ref2'}>, {P} plies per launch",
+                "kernel": f"k_rollout<{'full' if is_full4 else 'ref2'}>, {P} plies per launch",
                 "envs_per_gpu": per,
                 "global_envs": world * per,
                 "parallelism": f"dp{world} (env-id shards, 1 RCCL all-gather of stats)",
@@ -296,7 +299,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": f"k_rollout<true, {'true' if full else 'false'}>",
+                "kernel": f"k_rollout<true, {'true' if is_full4 else 'false'}>",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -312,7 +315,7 @@ def main():
                 "hipgraph": round(api_graph, 1),
                 "unit": "env steps/s",
                 "kernel_ms": round(step_ms, 5),
-                "achieved_GBps": round(((OUT_BYTES_PER_STEP_FULL if full else OUT_BYTES_PER_STEP) + RECORD_BYTES)
+                "achieved_GBps": round(((OUT_BYTES_PER_STEP_FULL if is_full4 else OUT_BYTES_PER_STEP) + RECORD_BYTES)
                                        * per / (step_ms * 1e-3) / 1e9, 2),
             },
             "other_rules": {

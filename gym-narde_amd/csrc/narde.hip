@@ -190,10 +190,9 @@ __global__ void __launch_bounds__(kBlock) k_legal_full(Planes pl, int n, Rng g,
     draw(g, s.t, (uint32_t)i, 0u, r);
     dice_from(r[0], g.dice_mode, d0, d1);
   }
-  const int8_t none[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
   const uint32_t w[4] = {0u, 0u, 0u, 0u};
   TurnOut o;
-  env_turn_full(s, d0, d1, none, w, o);
+  env_turn_full(s, d0, d1, true, ~0ull, w, o);  // play word of -1s: nothing is applied
   out[i] = o.legal;
 }
 
@@ -329,8 +328,10 @@ __device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t i,
   draw(g, s.t, i, 0u, r);
   int d0 = 0, d1 = 0;
   if (dice) { d0 = dice[2 * i]; d1 = dice[2 * i + 1]; }
+  // one 8-B load per env: the play's four (from, die) pairs
+  const uint64_t pw = play ? reinterpret_cast<const uint64_t*>(play)[i] : 0ull;
   env_ply_full(s, st, r, g.env0 + i, g.k0, g.k1, dice != nullptr, d0, d1, g.dice_mode,
-               play ? play + 8 * (size_t)i : nullptr, max_steps, autoreset, o, term, trunc);
+               play != nullptr, pw, max_steps, autoreset, o, term, trunc);
 }
 
 __device__ __forceinline__ void add_stats(int4* __restrict__ stats, int i, const int4& st) {

@@ -601,13 +601,16 @@ NARDE_FN uint64_t played_set(uint64_t pl, int k, int p, int d) {
   return (pl & ~(0xFFFFull << sh)) | ((uint64_t)(((uint32_t)d << 8) | (uint32_t)p) << sh);
 }
 
-// One FULL4 turn with dice (d0, d1).  play == nullptr: sub-move k is entry
-// mulhi(w[k], |C_k|) of C_k (the random-legal policy); else play = int8
-// (from, die)[4] and sub-moves are applied while each is in C_k (the first
-// one that is not ends the turn -- illegal actions are ignored, as in
-// narde_env.py:56-93).  Then _check_game_ended and the flip (narde_env.py:
-// 95-103, 134-141).
-NARDE_FN void env_turn_full(Side& s, int d0, int d1, const int8_t* play, const uint32_t w[4],
+// byte j of a play word, sign-extended (plays are int8 (from, die)[4])
+NARDE_FN int play_byte(uint64_t pw, int j) { return (int)(int8_t)(uint8_t)(pw >> (8 * j)); }
+
+// One FULL4 turn with dice (d0, d1).  !play: sub-move k is entry
+// mulhi(w[k], |C_k|) of C_k (the random-legal policy); else pw holds the
+// caller's int8 (from, die)[4] little-endian and sub-moves are applied while
+// each is in C_k (the first one that is not ends the turn -- illegal actions
+// are ignored, as in narde_env.py:56-93).  Then _check_game_ended and the
+// flip (narde_env.py:95-103, 134-141).
+NARDE_FN void env_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, const uint32_t w[4],
                             TurnOut& o) {
   const uint32_t low = block_lowmask(s.P);
   const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
@@ -631,8 +634,8 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, const int8_t* play, const u
       int p, d;
       bool ok;
       if (play) {
-        p = play[0];
-        d = play[1];
+        p = play_byte(pw, 0);
+        d = play_byte(pw, 1);
         ok = p >= 0 && p < 24 && ((d == dh && ((Ch >> p) & 1u)) || (d == dl && ((Cl >> p) & 1u)));
       } else {
         const int idx = (int)mulhi_u32(w[0], (uint32_t)n);
@@ -651,8 +654,8 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, const int8_t* play, const u
           int p2;
           bool ok2;
           if (play) {
-            p2 = play[2];
-            ok2 = play[3] == d2 && p2 >= 0 && p2 < 24 && ((L2 >> p2) & 1u);
+            p2 = play_byte(pw, 2);
+            ok2 = play_byte(pw, 3) == d2 && p2 >= 0 && p2 < 24 && ((L2 >> p2) & 1u);
           } else {
             p2 = select_bit(L2, (int)mulhi_u32(w[1], (uint32_t)__builtin_popcount(L2)));
             ok2 = true;
@@ -685,8 +688,8 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, const int8_t* play, const u
       }
       int p;
       if (play) {
-        p = play[2 * k];
-        if (!(play[2 * k + 1] == d && p >= 0 && p < 24 && ((C >> p) & 1u))) break;
+        p = play_byte(pw, 2 * k);
+        if (!(play_byte(pw, 2 * k + 1) == d && p >= 0 && p < 24 && ((C >> p) & 1u))) break;
       } else {
         // w[k] with a runtime k as selects (a dynamic index would put w in scratch)
         const uint32_t wk = k == 0 ? w[0] : (k == 1 ? w[1] : (k == 2 ? w[2] : w[3]));
@@ -782,8 +785,8 @@ NARDE_FN void env_ply(Side& s, int4& st, const uint32_t r[4], bool have_dice, in
 // r2, q0, q1}, q = Philox4x32-10(ctr = {t, env, 0, 2}) drawn only on doubles
 // (the only turns with more than two sub-moves).
 NARDE_FN void env_ply_full(Side& s, int4& st, const uint32_t r[4], uint32_t env, uint32_t k0,
-                           uint32_t k1, bool have_dice, int d0, int d1, int dice_mode,
-                           const int8_t* play, int max_steps, bool autoreset, TurnOut& o, int& term,
+                           uint32_t k1, bool have_dice, int d0, int d1, int dice_mode, bool play,
+                           uint64_t pw, int max_steps, bool autoreset, TurnOut& o, int& term,
                            int& trunc) {
   if (!have_dice) dice_from(r[0], dice_mode, d0, d1);
   uint32_t w[4] = {r[1], r[2], 0u, 0u};
@@ -794,7 +797,7 @@ NARDE_FN void env_ply_full(Side& s, int4& st, const uint32_t r[4], uint32_t env,
     w[3] = q[1];
   }
   const uint32_t mover_black = s.black;
-  env_turn_full(s, d0, d1, play, w, o);
+  env_turn_full(s, d0, d1, play, pw, w, o);
   s.elapsed += 1u;
   term = o.term;
   trunc = max_steps > 0 && s.elapsed >= (uint32_t)max_steps;

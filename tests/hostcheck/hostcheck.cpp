@@ -128,7 +128,7 @@ void hc_full4_batch(int64_t n, int8_t* board, uint8_t* off, uint8_t* ft, const i
   for (int64_t i = 0; i < n; ++i) {
     Side s = load(board + i * 24, off + 2 * i, ft + 2 * i, player[i], 0);
     TurnOut o;
-    env_turn_full(s, dice[2 * i], dice[2 * i + 1], nullptr, words + 4 * i, o);
+    env_turn_full(s, dice[2 * i], dice[2 * i + 1], false, 0ull, words + 4 * i, o);
     if (!o.term) side_flip(s);  // undo the flip: compare the mover's post-turn board
     legal[i] = o.legal;
     played[i] = o.played;
@@ -146,7 +146,9 @@ void hc_full4_play_batch(int64_t n, int8_t* board, uint8_t* off, uint8_t* ft, in
     Side s = load(board + i * 24, off + 2 * i, ft + 2 * i, player[i], 0);
     TurnOut o;
     const uint32_t w[4] = {0, 0, 0, 0};
-    env_turn_full(s, dice[2 * i], dice[2 * i + 1], play + 8 * i, w, o);
+    uint64_t pw;
+    memcpy(&pw, play + 8 * i, 8);
+    env_turn_full(s, dice[2 * i], dice[2 * i + 1], true, pw, w, o);
     played[i] = o.played;
     store(s, board + i * 24, off + 2 * i, ft + 2 * i, player + i, nullptr);
   }
@@ -166,7 +168,7 @@ void hc_selfplay_full(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int p
       TurnOut o;
       int tm, tr;
       env_ply_full(s, st, r, (uint32_t)(env0 + i), (uint32_t)seed, (uint32_t)(seed >> 32), false, 0,
-                   0, dice_mode, nullptr, max_steps, true, o, tm, tr);
+                   0, dice_mode, false, 0ull, max_steps, true, o, tm, tr);
       const int64_t ix = (int64_t)p * n + i;
       if (obs)
         for (int q = 0; q < 24; ++q) obs[ix * 24 + q] = (int8_t)obs_point(s, q);
