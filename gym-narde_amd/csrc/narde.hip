@@ -225,6 +225,18 @@ struct StepArgs {
 //   1: the wave transposes its 64 rows (6 KiB) through LDS so each
 //      wave-instruction stores one contiguous 1 KiB (8 whole lines);
 //   2: as 1 with non-temporal (streaming) stores for every per-ply output.
+// REF2 rollout kernel: 1 = producer/consumer k_rollout_pc (default),
+// 0 = one wave per 64 envs (k_rollout; A/B diagnostic builds only)
+#ifndef NARDE_ROLLOUT_PC
+#define NARDE_ROLLOUT_PC 1
+#endif
+
+// wave priority in k_rollout_pc (diagnostic knob): 0 none (age decides),
+// 1 consumers first, 2 producers first
+#ifndef NARDE_PC_PRIO
+#define NARDE_PC_PRIO 0
+#endif
+
 #ifndef NARDE_OBS_STORE
 #define NARDE_OBS_STORE 2
 #endif
@@ -392,6 +404,159 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Planes pl, int n, Rng g, int
   pl.p0[i] = ra;
   pl.p1[i] = rb;
   add_stats(pl.stats, i, st);
+}
+
+// ---------------------------------------------------------------------------
+// k_rollout_pc: the REF2 rollout as a producer/consumer workgroup.
+//
+// At B = 65,536 one lane per env gives exactly one wave per SIMD, and one wave
+// alone issues a VALU instruction only every 4 cycles (MI355X_MICROARCH.md,
+// constants table) -- half of what the SIMD can issue.  So each workgroup
+// (one per CU) holds 256 envs on 8 waves, two per SIMD:
+//   waves 0-3 (producers, the older waves, which win VALU arbitration) run
+//     the rules for their env with the record in VGPRs;
+//   waves 4-7 (consumers) do the work that does not depend on the state:
+//     the Philox draws of the NEXT block of plies (counter-based, so known
+//     in advance), and the per-ply outputs of the PREVIOUS block, expanded
+//     from the ply results the producers left in LDS and stored so that
+//     every wave-wide store is one contiguous 1 KiB.
+// Plies go in blocks of kPcR with one workgroup barrier per block; LDS holds
+// two slots of each ring (draws and results), 32 + 96 KiB.
+// Equivalent, bit for bit, to `plies` narde_step(NULL, NULL, autoreset=1).
+constexpr int kPcEnvs = 256;                  // envs per workgroup
+constexpr int kPcThreads = 2 * kPcEnvs;       // producers + consumers
+constexpr int kPcR = 4;                       // plies per barrier block
+
+struct PcLds {
+  uint4 draw[2][kPcR][kPcEnvs];               // Philox r0..r3 per env and ply
+  uint4 res[2][kPcR][3][kPcEnvs];             // ply results (kOut only)
+};
+
+// results of one ply of one env, as the consumers read them:
+//   res[.][.][0] = {own w0, own w1, own w2, opp w0}  (next mover's view)
+//   res[.][.][1] = {opp w1, opp w2, legal lo, legal hi}
+//   res[.][.][2] = {code1 | code2 << 16, reward | term << 8 | trunc << 16, 0, 0}
+__device__ __forceinline__ void pc_put(PcLds& L, int slot, int k, int le, const Side& s,
+                                       const StepOut& o, int term, int trunc) {
+  const uint64_t lg = compact_legal(o.l1);
+  L.res[slot][k][0][le] = make_uint4(s.own.w[0], s.own.w[1], s.own.w[2], s.opp.w[0]);
+  L.res[slot][k][1][le] = make_uint4(s.opp.w[1], s.opp.w[2], (uint32_t)lg, (uint32_t)(lg >> 32));
+  L.res[slot][k][2][le] =
+      make_uint4(((uint32_t)(uint16_t)o.code1) | ((uint32_t)(uint16_t)o.code2 << 16),
+                 (uint32_t)o.reward | ((uint32_t)term << 8) | ((uint32_t)trunc << 16), 0u, 0u);
+}
+
+// consumer: outputs of plies p0 .. p0+np-1 for the 64 envs of consumer wave cw
+__device__ __forceinline__ void pc_emit(const PcLds& L, int slot, int np, int p0, int n, int wg_env0,
+                                        int cw, int lane, const Outs& out) {
+  const int e0 = cw * 64;          // first env of this wave, workgroup-local
+  const int g0 = wg_env0 + e0;     // ... global (handle) index
+  const bool mine = g0 + lane < n;
+  for (int k = 0; k < np; ++k) {
+    const size_t row0 = (size_t)(p0 + k) * n + g0;
+    if (out.obs) {
+      // the wave's 64 obs rows are 384 contiguous int4 quads: lane takes
+      // quads lane + 64 q, so every store instruction covers 1 KiB
+      int4* dst = reinterpret_cast<int4*>(out.obs + row0 * 24);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const int j = lane + 64 * q;
+        const int el = j / 6, qq = j - 6 * el;
+        if (g0 + el >= n) continue;
+        const int wi = qq >> 1, sh = (qq & 1) * 16;
+        const uint4 a = L.res[slot][k][0][e0 + el];
+        const uint4 b = L.res[slot][k][1][e0 + el];
+        const uint32_t own = wi == 0 ? a.x : (wi == 1 ? a.y : a.z);
+        const uint32_t opp = wi == 0 ? a.w : (wi == 1 ? b.x : b.y);
+        int4 v;
+        v.x = (int)((own >> sh) & 15u) - (int)((opp >> sh) & 15u);
+        v.y = (int)((own >> (sh + 4)) & 15u) - (int)((opp >> (sh + 4)) & 15u);
+        v.z = (int)((own >> (sh + 8)) & 15u) - (int)((opp >> (sh + 8)) & 15u);
+        v.w = (int)((own >> (sh + 12)) & 15u) - (int)((opp >> (sh + 12)) & 15u);
+        st_out(dst + j, v);
+      }
+    }
+    if (mine) {
+      const uint4 b = L.res[slot][k][1][e0 + lane];
+      const uint4 c = L.res[slot][k][2][e0 + lane];
+      const size_t ix = row0 + lane;
+      if (out.reward) st_out(out.reward + ix, (int32_t)(c.y & 0xFFu));
+      if (out.term) st_out(out.term + ix, (uint8_t)((c.y >> 8) & 1u));
+      if (out.trunc) st_out(out.trunc + ix, (uint8_t)((c.y >> 16) & 1u));
+      if (out.legal) st_out(out.legal + ix, (uint64_t)b.z | ((uint64_t)b.w << 32));
+      if (out.act_out) st_out(reinterpret_cast<uint32_t*>(out.act_out) + ix, c.x);
+    }
+  }
+}
+
+template <bool kOut>
+__global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng g, int plies,
+                                                           int max_steps, Outs out) {
+  __shared__ PcLds L;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool producer = wave < 4;
+#if NARDE_PC_PRIO == 1
+  if (!producer) __builtin_amdgcn_s_setprio(1);
+#elif NARDE_PC_PRIO == 2
+  if (producer) __builtin_amdgcn_s_setprio(1);
+#endif
+  const int le = (wave & 3) * 64 + lane;            // workgroup-local env
+  const int wg_env0 = blockIdx.x * kPcEnvs;
+  const int i = wg_env0 + le;
+  const bool valid = i < n;
+  const int nb = (plies + kPcR - 1) / kPcR;
+
+  Side s;
+  int4 st = make_int4(0, 0, 0, 0);
+  uint32_t t0 = 0;
+  if (producer) {
+    if (valid) s = side_from_record(pl.p0[i], pl.p1[i]);
+  } else if (valid) {
+    t0 = pl.p1[i].w;
+  }
+  // consumer: draws of block b into slot b & 1 (Philox ctr {t, env, 0, 0})
+  auto draw_block = [&](int b) {
+    const int p0 = b * kPcR;
+    const int np = min(kPcR, plies - p0);
+    for (int k = 0; k < np; ++k) {
+      uint32_t r[4];
+      draw(g, t0 + (uint32_t)(p0 + k), (uint32_t)i, 0u, r);
+      L.draw[b & 1][k][le] = make_uint4(r[0], r[1], r[2], r[3]);
+    }
+  };
+  if (!producer) draw_block(0);
+  __syncthreads();
+  for (int b = 0; b < nb; ++b) {
+    const int p0 = b * kPcR;
+    const int np = min(kPcR, plies - p0);
+    if (producer) {
+      if (valid) {
+        for (int k = 0; k < np; ++k) {
+          const uint4 rv = L.draw[b & 1][k][le];
+          const uint32_t r[4] = {rv.x, rv.y, rv.z, rv.w};
+          StepOut o;
+          int term, trunc;
+          env_ply(s, st, r, false, 0, 0, g.dice_mode, true, 0, 0, max_steps, true, o, term, trunc);
+          if (kOut) pc_put(L, b & 1, k, le, s, o, term, trunc);
+        }
+      }
+    } else {
+      if (b + 1 < nb) draw_block(b + 1);
+      if (kOut && b > 0) pc_emit(L, (b - 1) & 1, kPcR, p0 - kPcR, n, wg_env0, wave & 3, lane, out);
+    }
+    __syncthreads();
+  }
+  if (kOut && !producer && nb > 0) {
+    const int p0 = (nb - 1) * kPcR;
+    pc_emit(L, (nb - 1) & 1, plies - p0, p0, n, wg_env0, wave & 3, lane, out);
+  }
+  if (producer && valid) {
+    uint4 ra, rb;
+    side_to_record(s, ra, rb);
+    pl.p0[i] = ra;
+    pl.p1[i] = rb;
+    add_stats(pl.stats, i, st);
+  }
 }
 
 __global__ void __launch_bounds__(kBlock) k_get_stats(Planes pl, int n, int32_t* __restrict__ out) {
@@ -746,12 +911,23 @@ int narde_rollout(narde_env* e, int plies, int32_t* obs, int32_t* reward, uint8_
   DeviceGuard dg(e->device);
   const Outs out{obs, reward, terminated, truncated, legal_compact, actions_out, nullptr};
   const bool any = obs || reward || terminated || truncated || legal_compact || actions_out;
+  const int pc_grid = (int)((e->n + kPcEnvs - 1) / kPcEnvs);
+#if NARDE_ROLLOUT_PC
+  if (any)
+    k_rollout_pc<true><<<pc_grid, kPcThreads, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), plies,
+                                                                      e->max_steps, out);
+  else
+    k_rollout_pc<false><<<pc_grid, kPcThreads, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e),
+                                                                       plies, e->max_steps, out);
+#else
+  (void)pc_grid;
   if (any)
     k_rollout<true, false><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e),
                                                                           plies, e->max_steps, out);
   else
     k_rollout<false, false><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e),
                                                                            plies, e->max_steps, out);
+#endif
   return check_launch("k_rollout");
 }
 

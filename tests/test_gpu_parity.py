@@ -130,8 +130,9 @@ def test_selfplay_trajectory_vs_oracle(dice_mode, max_steps):
         assert rec["truncated"].any()
 
 
-def test_fused_selfplay_vs_oracle():
-    n, seed = 8192, 99
+@pytest.mark.parametrize("n", [8192, 1337])
+def test_fused_selfplay_vs_oracle(n):
+    seed = 99
     env = vec(n, seed=seed)
     ref = O.SelfPlay(n, seed=seed)
     ref.reset(0)
@@ -152,10 +153,12 @@ def test_fused_selfplay_vs_oracle():
     assert np.array_equal(np_(env2.get_state()["board"]), ref.board)
 
 
-def test_rollout_vs_oracle_and_step():
+@pytest.mark.parametrize("n", [4096, 1000, 37])
+def test_rollout_vs_oracle_and_step(n):
     """k_rollout (P plies per launch, outputs streamed) == the oracle per ply,
-    across launch boundaries of different lengths."""
-    n, seed, env0 = 4096, 0xABCDEF, 777
+    across launch boundaries of different lengths, also for env counts that
+    leave partial workgroups and waves (ragged tails)."""
+    seed, env0 = 0xABCDEF, 777
     env = vec(n, seed=seed, env_id_offset=env0, max_episode_steps=150)
     ref = O.SelfPlay(n, seed=seed, env0=env0, max_steps=150)
     ref.reset(0)

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Time k_rollout (outputs on/off) for the libnarde.so named by $NARDE_LIB."""
+"""Time k_rollout (outputs on/off) for the libnarde.so named by $NARDE_LIB.
+Optional argv[1] = number of envs (default 65,536)."""
 import json
 import os
 import sys
@@ -24,14 +25,18 @@ def timed(fn, reps):
 
 
 def main():
-    n, P, reps = 65536, 100, 30
-    env = VecNardeEnv(n, device="cuda:0", seed=0)
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+    rules = sys.argv[2] if len(sys.argv) > 2 else "ref2"
+    P, reps = 100, 30
+    env = VecNardeEnv(n, device="cuda:0", seed=0, rules=rules)
     bufs = env.rollout_buffers(P)
     env.selfplay(300)
-    out = {"lib": os.path.basename(os.environ.get("NARDE_LIB", "libnarde.so")),
+    out = {"lib": os.path.basename(os.environ.get("NARDE_LIB", "libnarde.so")), "envs": n,
+           "rules": rules,
            "rollout_ms": round(timed(lambda: env.rollout(P, bufs), reps), 4),
            "selfplay_ms": round(timed(lambda: env.selfplay(P), reps), 4)}
     out["rollout_steps_per_s"] = round(n * P / (out["rollout_ms"] * 1e-3))
+    out["selfplay_steps_per_s"] = round(n * P / (out["selfplay_ms"] * 1e-3))
     out["rollout_TBps"] = round(n * (114 * P + 64) / (out["rollout_ms"] * 1e-3) / 1e12, 3)
     print(json.dumps(out))
 
