@@ -119,6 +119,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rules", choices=("ref2", "full4"), default="ref2",
                     help="rules of the timed path (value); the other mode is reported beside it")
+    ap.add_argument("--dqn-steps", type=int, default=30,
+                    help="timed steps of the config-4 DQN driver leg (0 = skip)")
+    ap.add_argument("--dqn-train-batch", type=int, default=4096)
     ap.add_argument("--other-launches", type=int, default=20,
                     help="k_rollout launches of the other rules mode, timed beside the headline")
     ap.add_argument("--traffic-json", default=None,
@@ -259,6 +262,49 @@ def main():
         other_M = [round(float(x), 4) for x in (torch.bincount(M, minlength=5).double() / M.numel()).tolist()]
     env_o.close()
 
+    # secondary 4: configs[3] -- the batched DQN driver (198-d obs + legal
+    # masks -> DecomposedDQN -> env step -> device replay -> one PER update)
+    dqn = None
+    if args.dqn_steps > 0 and not is_full4:
+        from gym_narde.dqn import BatchedDQNDriver
+
+        env_q = VecNardeEnv(per, device=dev, seed=args.seed + 1, env_id_offset=first,
+                            max_episode_steps=1000)
+        drv = BatchedDQNDriver(env_q, obs="tesauro198", train_batch=args.dqn_train_batch,
+                               capacity=max(1 << 20, 4 * per))
+        for _ in range(5):
+            drv.step()
+        torch.cuda.synchronize()
+        q0 = time.perf_counter()
+        for _ in range(args.dqn_steps):
+            drv.step()
+        torch.cuda.synchronize()
+        q_el = time.perf_counter() - q0
+        # split: action selection + env step vs the learner update
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record()
+        x = drv.state
+        a = drv.act(x)
+        env_q.step(a.to(torch.int16))
+        ev[1].record()
+        drv.update()
+        ev[2].record()
+        torch.cuda.synchronize()
+        dqn = {
+            "config": "configs[3]: batch=65536, legal-action masks + 198-d obs -> DecomposedDQN "
+                      "(train_deepq_pytorch.py:184-277) on PyTorch-ROCm, fp32",
+            "value": round(world * per * args.dqn_steps / q_el, 1),
+            "unit": "env steps/s",
+            "ms_per_step": round(q_el / args.dqn_steps * 1e3, 4),
+            "act_plus_env_ms": round(ev[0].elapsed_time(ev[1]), 4),
+            "update_ms": round(ev[1].elapsed_time(ev[2]), 4),
+            "train_batch": args.dqn_train_batch,
+            "updates_per_step": 1,
+            "dtype": "f32",
+            "final_loss": float(drv.last_loss) if drv.last_loss is not None else None,
+        }
+        env_q.close()
+
     if rank == 0:
         nbytes = launch_bytes(per, P, is_full4)
         achieved = nbytes / (kern_ms * 1e-3) / 1e9
@@ -330,6 +376,7 @@ def main():
                 "frac": round(obytes / (other_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
                 "max_dice_hist": other_M,
             },
+            "config4_dqn": dqn,
             "selfplay_stats_only": {
                 "kernel": f"k_rollout without per-ply outputs, {F} plies per launch",
                 "value": round(fused, 1),

@@ -643,6 +643,50 @@ __global__ void __launch_bounds__(kBlock) k_mask576(Planes pl, int n, Rng g,
   for (int q = 0; q < 9; ++q) mask[(size_t)i * 9 + q] = m[q];
 }
 
+// move-2 acceptance mask given each env's move-1 code, for the next step's
+// device dice: what NardeEnv.step would accept as move2 after move1
+// (narde_env.py:56-93: move1 must be in list #1 with >= 2 entries; the die
+// bookkeeping picks the second die; list #2 = get_valid_moves([die]) on the
+// post-move1 board; the decode quirk makes (f, 0), f <= 5, unrequestable).
+// All zero when move1 would not be played.
+__global__ void __launch_bounds__(kBlock) k_mask576_move2(Planes pl, int n, Rng g,
+                                                          const int16_t* __restrict__ move1,
+                                                          const uint8_t* __restrict__ dice,
+                                                          uint64_t* __restrict__ mask) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  Side s = side_from_record(pl.p0[i], pl.p1[i]);
+  int d0, d1;
+  if (dice) {
+    d0 = dice[2 * i];
+    d1 = dice[2 * i + 1];
+  } else {
+    uint32_t r[4];
+    draw(g, s.t, (uint32_t)i, 0u, r);
+    dice_from(r[0], g.dice_mode, d0, d1);
+  }
+  Legal l;
+  legal2(s, d0, d1, l);
+  uint64_t m[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int f1, t1;
+  decode_action(move1[i], f1, t1);
+  if (l.count >= 2 && legal_contains(l, f1, t1)) {
+    apply_move(s, f1, t1);
+    const int dist = t1 == OFF ? f1 + 1 : (f1 > t1 ? f1 - t1 : t1 - f1);
+    const int rem = (d0 == dist) ? d1 : ((d1 == dist) ? d0 : d1);
+    uint32_t L2 = die_filter(s.O, s.S1o, block_info(s.O, s.P), die_candidates(s.O, s.P, rem), rem);
+    while (L2) {
+      const int f = __builtin_ctz(L2);
+      L2 &= L2 - 1u;
+      const int to = f - rem < 0 ? OFF : f - rem;
+      if (to == 0 && f <= 5) continue;  // (f, 0) cannot be requested by a code
+      const int c = encode_move(f, to);
+      m[c >> 6] |= 1ull << (c & 63);
+    }
+  }
+  for (int q = 0; q < 9; ++q) mask[(size_t)i * 9 + q] = m[q];
+}
+
 __global__ void __launch_bounds__(kBlock) k_block(const int8_t* __restrict__ boards, int n,
                                                   uint8_t* __restrict__ out) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
@@ -990,6 +1034,15 @@ int narde_legal_mask576(narde_env* e, uint64_t* mask, void* stream) {
   DeviceGuard dg(e->device);
   k_mask576<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), mask);
   return check_launch("k_mask576");
+}
+
+int narde_legal_mask576_move2(narde_env* e, const int16_t* move1, const uint8_t* dice, uint64_t* mask,
+                              void* stream) {
+  if (!e || !move1 || !mask) return fail(NARDE_EINVAL, "NULL argument");
+  DeviceGuard dg(e->device);
+  k_mask576_move2<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), move1, dice,
+                                                                  mask);
+  return check_launch("k_mask576_move2");
 }
 
 int narde_violates_block_rule(int device, const int8_t* boards, int64_t n, uint8_t* out, void* stream) {

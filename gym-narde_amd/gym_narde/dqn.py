@@ -1,0 +1,247 @@
+"""Batched DQN self-play driver on the device env (SURVEY.md section 8 row f-1,
+BASELINE.json configs[3]: batch 65,536 with the legal-action mask and the
+198-float observation feeding the reference trainer's DQN).
+
+The reference trainer (train_deepq_pytorch.py) plays ONE env on the host:
+per step it rolls dice, lists moves, runs DQNAgent.act over Python lists of
+(move1, move2) combinations (:411-600), steps the env, shapes the reward
+(:885-908), stores the transition and trains on a 64-sample prioritized
+minibatch (:279-342, :602-750).  Here every piece works on B envs at once
+without leaving the GPU:
+
+  observation   VecNardeEnv.tesauro198()  (k_observe, README.md:42-102) or
+                the reference's int32[24] perspective board (state_size 24)
+  move-1 mask   VecNardeEnv.legal_mask()        (k_mask576: exactly the codes
+                                                 NardeEnv.step accepts)
+  move-2 mask   VecNardeEnv.legal_mask_move2()  (k_mask576_move2: the codes
+                step accepts after the chosen move 1 -- the reference's act()
+                guesses them from the pre-move board, :452-503)
+  Q-values      DecomposedDQN, the reference's architecture and parameter
+                names (:184-277), so its checkpoints load; move-2 Q-values
+                use the column-gather identity below instead of a one-hot
+                concat GEMM
+  policy        masked epsilon-greedy (explore: uniform over legal codes)
+  env step      VecNardeEnv.step(actions)  (k_step, auto-reset)
+  replay        DeviceReplay: prioritized replay with the reference's
+                alpha/beta/epsilon rules on device tensors (:279-342)
+  update        the reference's decomposed double-head DQN loss (:653-720),
+                Adam, grad-norm clip 10, target sync every 10 updates,
+                epsilon decay per update
+
+move2_head(cat(features, onehot(m1))) = features @ Wf^T + Wm[:, m1] + b with
+W = [Wf | Wm]: mathematically identical to the reference's one-hot concat,
+equal in fp32 up to summation order (tests/test_dqn_cpu.py).
+"""
+import torch
+import torch.nn as nn
+
+MOVES = 576
+
+
+class DecomposedDQN(nn.Module):
+    """train_deepq_pytorch.py:184-222 (same layers, same parameter names)."""
+
+    def __init__(self, state_size, move_space_size=MOVES):
+        super().__init__()
+        self.move_space_size = move_space_size
+        self.feature_network = nn.Sequential(
+            nn.Linear(state_size, 256), nn.ReLU(), nn.Linear(256, 256), nn.ReLU())
+        self.move1_head = nn.Linear(256, move_space_size)
+        self.move2_head = nn.Linear(256 + move_space_size, move_space_size)
+
+    def features(self, x):
+        return self.feature_network(x)
+
+    def move2_from_features(self, f, move1):
+        """move2 Q-values given move-1 codes, without materialising the
+        one-hot concat: W[:, :256] f + W[:, 256 + m1] + b."""
+        w = self.move2_head.weight
+        out = torch.nn.functional.linear(f, w[:, :256], self.move2_head.bias)
+        return out + w[:, 256:].t().index_select(0, move1)
+
+    def forward(self, x, selected_move1=None):
+        f = self.features(x)
+        if selected_move1 is None:
+            return self.move1_head(f)
+        return self.move2_from_features(f, selected_move1)
+
+
+def expand_mask(mask576):
+    """(B,9) int64 bit masks -> (B,576) bool."""
+    shifts = torch.arange(64, device=mask576.device, dtype=torch.int64)
+    bits = (mask576.unsqueeze(-1) >> shifts) & 1
+    return bits.view(mask576.shape[0], MOVES).bool()
+
+
+def masked_argmax(scores, mask):
+    """argmax over legal entries; 0 where nothing is legal (the reference's
+    'no move' code, train_deepq_pytorch.py:504-505)."""
+    neg = torch.finfo(scores.dtype).min
+    best = scores.masked_fill(~mask, neg).argmax(1)
+    return torch.where(mask.any(1), best, torch.zeros_like(best))
+
+
+class DeviceReplay:
+    """PrioritizedReplayBuffer (train_deepq_pytorch.py:279-342) on device
+    tensors: new transitions get the running max priority, sampling is
+    proportional to priority**alpha, importance weights (N p)^-beta / max,
+    beta anneals by beta_increment per sample, priorities = |td| + epsilon."""
+
+    def __init__(self, capacity, state_size, device, alpha=0.6, beta=0.4, beta_increment=0.001,
+                 epsilon=0.01):
+        self.capacity, self.device = int(capacity), device
+        self.alpha, self.beta, self.beta_increment, self.epsilon = alpha, beta, beta_increment, epsilon
+        z = dict(device=device)
+        self.obs = torch.zeros((self.capacity, state_size), dtype=torch.float32, **z)
+        self.next_obs = torch.zeros((self.capacity, state_size), dtype=torch.float32, **z)
+        self.action = torch.zeros((self.capacity, 2), dtype=torch.int64, **z)
+        self.reward = torch.zeros(self.capacity, dtype=torch.float32, **z)
+        self.done = torch.zeros(self.capacity, dtype=torch.float32, **z)
+        self.prio = torch.ones(self.capacity, dtype=torch.float32, **z)
+        self.max_prio = torch.ones((), dtype=torch.float32, **z)
+        self.pos = 0
+        self.size = 0
+
+    def add(self, obs, action, reward, next_obs, done):
+        n = obs.shape[0]
+        if n > self.capacity:
+            raise ValueError("batch larger than the replay capacity")
+        idx = (torch.arange(n, device=self.device) + self.pos) % self.capacity
+        self.obs.index_copy_(0, idx, obs)
+        self.next_obs.index_copy_(0, idx, next_obs)
+        self.action.index_copy_(0, idx, action)
+        self.reward.index_copy_(0, idx, reward)
+        self.done.index_copy_(0, idx, done)
+        self.prio.index_copy_(0, idx, self.max_prio.expand(n))
+        self.pos = (self.pos + n) % self.capacity
+        self.size = min(self.size + n, self.capacity)
+
+    def sample(self, batch, generator=None):
+        p = self.prio[: self.size] ** self.alpha
+        probs = p / p.sum()
+        idx = torch.multinomial(probs, batch, replacement=True, generator=generator)
+        w = (self.size * probs[idx]) ** (-self.beta)
+        w = w / w.max()
+        self.beta = min(1.0, self.beta + self.beta_increment)
+        return idx, w
+
+    def update(self, idx, td):
+        pr = td + self.epsilon
+        self.prio.index_copy_(0, idx, pr)
+        self.max_prio = torch.maximum(self.max_prio, pr.max())
+
+
+class BatchedDQNDriver:
+    """B envs of DQN self-play on one GPU; one call of step() = one env step
+    for every env + `updates_per_step` prioritized DQN updates."""
+
+    def __init__(self, env, obs="tesauro198", train_batch=4096, capacity=1 << 20,
+                 learning_rate=1e-4, gamma=0.99, epsilon=1.0, epsilon_min=0.01,
+                 epsilon_decay=0.995, target_update=10, updates_per_step=1, shaping=True,
+                 seed=0):
+        if env.full:
+            raise ValueError("the DQN driver plays the reference's (move1, move2) actions: rules='ref2'")
+        self.env, self.dev = env, env.device
+        self.obs_kind = obs
+        self.state_size = 198 if obs == "tesauro198" else 24
+        torch.manual_seed(seed)
+        self.gen = torch.Generator(device=self.dev)
+        self.gen.manual_seed(seed)
+        self.model = DecomposedDQN(self.state_size).to(self.dev)
+        self.target = DecomposedDQN(self.state_size).to(self.dev)
+        self.target.load_state_dict(self.model.state_dict())
+        self.opt = torch.optim.Adam(self.model.parameters(), lr=learning_rate)
+        self.replay = DeviceReplay(capacity, self.state_size, self.dev)
+        self.train_batch, self.gamma = int(train_batch), gamma
+        self.epsilon, self.epsilon_min, self.epsilon_decay = epsilon, epsilon_min, epsilon_decay
+        self.target_update, self.updates_per_step = target_update, updates_per_step
+        self.shaping = shaping
+        self.train_steps = 0
+        B = env.num_envs
+        self.off_seen = torch.zeros((B, 2), dtype=torch.float32, device=self.dev)
+        self.state = self._observe()
+        self.last_loss = None
+
+    # ---------------------------------------------------------------- env side
+    def _observe(self):
+        if self.obs_kind == "tesauro198":
+            return self.env.tesauro198().clone()
+        return self.env.observe().to(torch.float32)
+
+    def _off_counts(self):
+        """(B,2) borne-off counts (white, black) and the current player (+1/-1)."""
+        st = self.env.get_state()
+        return st["off"].to(torch.float32), st["player"].to(torch.float32)
+
+    @torch.no_grad()
+    def act(self, x):
+        """Masked epsilon-greedy (move1, move2) codes for the next step."""
+        B = x.shape[0]
+        m1 = expand_mask(self.env.legal_mask())
+        f = self.model.features(x)
+        q1 = self.model.move1_head(f)
+        explore = torch.rand(B, device=self.dev, generator=self.gen) < self.epsilon
+        rnd1 = torch.rand((B, MOVES), device=self.dev, generator=self.gen)
+        a1 = masked_argmax(torch.where(explore.unsqueeze(1), rnd1, q1), m1)
+        m2 = expand_mask(self.env.legal_mask_move2(a1.to(torch.int16)))
+        q2 = self.model.move2_from_features(f, a1)
+        rnd2 = torch.rand((B, MOVES), device=self.dev, generator=self.gen)
+        a2 = masked_argmax(torch.where(explore.unsqueeze(1), rnd2, q2), m2)
+        return torch.stack([a1, a2], 1)
+
+    def step(self):
+        x = self.state
+        actions = self.act(x)
+        _, reward, term, trunc, _ = self.env.step(actions.to(torch.int16))
+        r = reward.to(torch.float32)
+        done = (term | trunc).to(torch.float32)
+        if self.shaping:
+            # train_deepq_pytorch.py:885-908: +1 per checker newly borne off
+            # and +0.1 x total off, for env.unwrapped.current_player read AFTER
+            # the step (the reference reads the post-flip player)
+            off, player = self._off_counts()
+            col = (player < 0).long()
+            now = off.gather(1, col.unsqueeze(1)).squeeze(1)
+            before = self.off_seen.gather(1, col.unsqueeze(1)).squeeze(1)
+            r = r + (now - before).clamp(min=0) + 0.1 * now
+            self.off_seen.scatter_(1, col.unsqueeze(1), now.unsqueeze(1))
+            self.off_seen.mul_((1.0 - done).unsqueeze(1))  # new episode: trackers restart at 0
+        nxt = self._observe()
+        self.replay.add(x, actions, r, nxt, done)
+        self.state = nxt
+        loss = None
+        for _ in range(self.updates_per_step):
+            loss = self.update()
+        return loss
+
+    # ------------------------------------------------------------ learner side
+    def update(self):
+        """DQNAgent.replay (train_deepq_pytorch.py:602-750), decomposed branch."""
+        if self.replay.size < self.train_batch:
+            return None
+        idx, w = self.replay.sample(self.train_batch, generator=self.gen)
+        s, ns = self.replay.obs[idx], self.replay.next_obs[idx]
+        a, r, d = self.replay.action[idx], self.replay.reward[idx], self.replay.done[idx]
+        f = self.model.features(s)
+        q1 = self.model.move1_head(f).gather(1, a[:, :1]).squeeze(1)
+        q2 = self.model.move2_from_features(f, a[:, 0]).gather(1, a[:, 1:]).squeeze(1)
+        with torch.no_grad():
+            tf = self.target.features(ns)
+            nq1 = self.target.move1_head(tf)
+            t1 = r + (1 - d) * self.gamma * nq1.max(1)[0]
+            nq2 = self.target.move2_from_features(tf, nq1.argmax(1))
+            t2 = r + (1 - d) * self.gamma * nq2.max(1)[0]
+        td = torch.clamp((t1 - q1).abs() + (t2 - q2).abs(), 0.0, 100.0).detach()
+        loss = (w * (q1 - t1) ** 2).mean() + (w * (q2 - t2) ** 2).mean()
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=10.0)
+        self.opt.step()
+        self.replay.update(idx, td)
+        self.train_steps += 1
+        if self.train_steps % self.target_update == 0:
+            self.target.load_state_dict(self.model.state_dict())
+        if self.epsilon > self.epsilon_min:
+            self.epsilon *= self.epsilon_decay
+        self.last_loss = loss.detach()
+        return self.last_loss

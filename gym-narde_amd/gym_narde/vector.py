@@ -172,6 +172,20 @@ class VecNardeEnv:
         self.handle.call("narde_legal_mask576", _lib.ptr(out), self._s())
         return out
 
+    def legal_mask_move2(self, move1, dice=None, out=None):
+        """(B,9) int64 = 576-bit mask of move2 codes step() accepts after the
+        move1 codes (B,), for dice (B,2) or the next step's device dice (all
+        zero where move1 would not be played)."""
+        B = self.num_envs
+        m1 = self._dev(move1, self.torch.int16, (B,))
+        d = None if dice is None else self._dev(dice, self.torch.uint8, (B, 2))
+        if out is None:
+            out = self.torch.empty((B, 9), dtype=self.torch.int64, device=self.device)
+        self.handle.call("narde_legal_mask576_move2", _lib.ptr(m1), _lib.ptr(d), _lib.ptr(out),
+                         self._s())
+        self._keep = (m1, d)
+        return out
+
     def legal_full(self, dice=None):
         """FULL4: (B,) int64 legal words (first sub-move set | max dice << 56)
         for dice (B,2) or the next step's device dice."""

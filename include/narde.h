@@ -179,6 +179,15 @@ int narde_observe(narde_env *env, int32_t *obs, float *tesauro198, void *stream)
  * u64[B][9], bit c set iff the reference would accept code c as move1. */
 int narde_legal_mask576(narde_env *env, uint64_t *mask, void *stream);
 
+/* Move-2 acceptance mask u64[B][9] given each env's move-1 code i16[B] and
+ * dice u8[B][2] in roll order (NULL = the next step's device dice): bit c
+ * set iff NardeEnv.step would play code c as move2 after move1
+ * (narde_env.py:56-93); all zero when move1 would not be played.  With
+ * narde_legal_mask576 it gives a policy the exact legal set of (move1,
+ * move2) codes (train_deepq_pytorch.py:411-600 approximates it). */
+int narde_legal_mask576_move2(narde_env *env, const int16_t *move1, const uint8_t *dice,
+                              uint64_t *mask, void *stream);
+
 /* Stateless: Narde._violates_block_rule on n perspective boards i8[n][24]. */
 int narde_violates_block_rule(int device, const int8_t *boards, int64_t n, uint8_t *out,
                               void *stream);

@@ -1,0 +1,84 @@
+"""The batched DQN driver (gym_narde/dqn.py, config 4) on the GPU: every
+chosen action is legal per the env's own masks, greedy actions are the masked
+argmax of the network, and learning updates run (finite loss, replay grows,
+target sync, epsilon decay)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def make(n=4096, **kw):
+    from gym_narde.dqn import BatchedDQNDriver
+    from gym_narde.vector import VecNardeEnv
+
+    env = VecNardeEnv(n, device="cuda:0", seed=17)
+    return env, BatchedDQNDriver(env, capacity=1 << 16, train_batch=1024, **kw)
+
+
+@pytest.mark.parametrize("obs", ["tesauro198", "int24"])
+def test_driver_actions_are_legal_and_learning_runs(obs):
+    from gym_narde.dqn import expand_mask
+
+    env, drv = make(obs=obs)
+    n = env.num_envs
+    for step in range(12):
+        x = drv.state
+        m1 = expand_mask(env.legal_mask())
+        a = drv.act(x)
+        m2 = expand_mask(env.legal_mask_move2(a[:, 0].to(torch.int16)))
+        rows = torch.arange(n, device=a.device)
+        has1 = m1.any(1)
+        assert bool(m1[rows, a[:, 0]][has1].all())
+        assert bool((a[:, 0][~has1] == 0).all())
+        has2 = m2.any(1)
+        assert bool(m2[rows, a[:, 1]][has2].all())
+        drv.step()  # (draws its own actions; the env advances)
+    torch.cuda.synchronize()
+    assert drv.replay.size == 12 * n
+    assert drv.train_steps >= 10
+    assert torch.isfinite(drv.last_loss)
+    assert drv.epsilon < 1.0
+    assert drv.state.shape == (n, drv.state_size)
+
+
+def test_greedy_is_masked_argmax():
+    from gym_narde.dqn import expand_mask
+
+    env, drv = make(epsilon=0.0)
+    x = drv.state
+    m1 = expand_mask(env.legal_mask())
+    q1 = drv.model(x)
+    a = drv.act(x)
+    q1m = q1.masked_fill(~m1, -np.inf)
+    has1 = m1.any(1)
+    assert torch.equal(a[:, 0][has1], q1m.argmax(1)[has1])
+    m2 = expand_mask(env.legal_mask_move2(a[:, 0].to(torch.int16)))
+    q2 = drv.model(x, a[:, 0]).masked_fill(~m2, -np.inf)
+    has2 = m2.any(1)
+    assert torch.equal(a[:, 1][has2], q2.argmax(1)[has2])
+
+
+def test_reference_step_accepts_driver_actions():
+    """Played through the oracle's NardeEnv.step with the same dice, the
+    driver's greedy/explore codes are never ignored: move1 is played whenever
+    list #1 has >= 2 entries, and move2 whenever list #2 is non-empty."""
+    import oracle as O
+
+    env, drv = make(n=2048)
+    env.selfplay(40)
+    drv.state = drv._observe()
+    a = drv.act(drv.state).cpu().numpy().astype(np.int16)
+    st = {k: v.cpu().numpy() for k, v in env.get_state().items()}
+    dice = env.dice().cpu().numpy()
+    ref = O.step(st["board"], st["off"], st["first_turn"], st["player"], dice, a)
+    played1 = ref["count2"] >= 0
+    assert (played1 | (ref["count1"] < 2)).all()

@@ -287,3 +287,54 @@ def test_reset_mask_and_opening_law():
     pl = np_(st["player"])[::2]
     assert abs((pl == 1).mean() - 0.5) < 0.02
     assert (np_(st["first_turn"])[::2] == 1).all()
+
+
+def _codes_of(moves, count):
+    """the reference's requestable codes of a list: encode(f, t), except a
+    normal (f, 0) with f <= 5, which decodes to (f, 'off')"""
+    out = set()
+    for f, t in moves[:count]:
+        f, t = int(f), int(t)
+        if t == 0 and f <= 5:
+            continue
+        out.add(f * 24 + (0 if t == 24 else t))
+    return out
+
+
+def _bits(row):
+    return {c for c in range(576) if (int(row[c >> 6]) >> (c & 63)) & 1}
+
+
+def test_mask576_move2_golden():
+    """move-2 mask for the recorded (state, dice, move1) of every golden step
+    == the requestable codes of the reference's list #2 (empty when the
+    reference made no second list)."""
+    s = golden("steps.npz")
+    n = len(s["dice"])
+    env = vec(n)
+    set_from(env, s)
+    m2 = np_(env.legal_mask_move2(torch.from_numpy(s["action"][:, 0].copy()),
+                                  dice=torch.from_numpy(s["dice"]))).view(np.uint64)
+    for i in range(n):
+        exp = _codes_of(s["list2"][i], s["count2"][i]) if s["count2"][i] >= 0 else set()
+        assert _bits(m2[i]) == exp, i
+
+
+def test_mask576_move2_device_dice_vs_oracle():
+    n, seed = 4096, 21
+    env = vec(n, seed=seed)
+    env.selfplay(53)
+    m1 = np_(env.legal_mask()).view(np.uint64)
+    rng = np.random.RandomState(0)
+    move1 = np.zeros(n, np.int16)
+    for i in range(n):
+        legal = sorted(_bits(m1[i]))
+        move1[i] = legal[rng.randint(len(legal))] if legal and rng.rand() < 0.9 else rng.randint(576)
+    m2 = np_(env.legal_mask_move2(torch.from_numpy(move1))).view(np.uint64)
+    st = {k: np_(v) for k, v in env.get_state().items()}
+    dice = np_(env.dice())
+    ref = O.step(st["board"], st["off"], st["first_turn"], st["player"], dice,
+                 np.stack([move1, np.zeros(n, np.int16)], 1))
+    for i in range(n):
+        exp = _codes_of(ref["list2"][i], ref["count2"][i]) if ref["count2"][i] >= 0 else set()
+        assert _bits(m2[i]) == exp, i
