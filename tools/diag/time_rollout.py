@@ -27,12 +27,13 @@ def timed(fn, reps):
 def main():
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     rules = sys.argv[2] if len(sys.argv) > 2 else "ref2"
+    dice_mode = sys.argv[3] if len(sys.argv) > 3 else "all36"
     P, reps = 100, 30
-    env = VecNardeEnv(n, device="cuda:0", seed=0, rules=rules)
+    env = VecNardeEnv(n, device="cuda:0", seed=0, rules=rules, dice_mode=dice_mode)
     bufs = env.rollout_buffers(P)
     env.selfplay(300)
     out = {"lib": os.path.basename(os.environ.get("NARDE_LIB", "libnarde.so")), "envs": n,
-           "rules": rules,
+           "rules": rules, "dice": dice_mode,
            "rollout_ms": round(timed(lambda: env.rollout(P, bufs), reps), 4),
            "selfplay_ms": round(timed(lambda: env.selfplay(P), reps), 4)}
     out["rollout_steps_per_s"] = round(n * P / (out["rollout_ms"] * 1e-3))
