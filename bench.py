@@ -337,7 +337,7 @@ def main():
                              f"TimeLimit 1000; every ply writes obs/reward/terminated/truncated/"
                              f"legal set/actions for every env"),
                 "rules": args.rules,
-                "kernel": f"k_rollout<{'full' if is_full4 else 'ref2'}>, {P} plies per launch",
+                "kernel": f"{'k_rollout<true, true> (FULL4)' if is_full4 else 'k_rollout_pc<true> (REF2)'}, {P} plies per launch",
                 "envs_per_gpu": per,
                 "global_envs": world * per,
                 "parallelism": f"dp{world} (env-id shards, 1 RCCL all-gather of stats)",
@@ -345,7 +345,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": f"k_rollout<true, {'true' if is_full4 else 'false'}>",
+                "kernel": "k_rollout<true, true>" if is_full4 else "k_rollout_pc<true>",
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -367,7 +367,7 @@ def main():
             "other_rules": {
                 "rules": other_rules,
                 "workload": rules_txt[other_rules],
-                "kernel": f"k_rollout<{'full' if other_rules == 'full4' else 'ref2'}>, {P} plies per launch, all outputs",
+                "kernel": f"{'k_rollout<true, true> (FULL4)' if other_rules == 'full4' else 'k_rollout_pc<true> (REF2)'}, {P} plies per launch, all outputs",
                 "value": round(other_rate, 1),
                 "unit": "env steps/s",
                 "kernel_ms": round(other_ms, 5),

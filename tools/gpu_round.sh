@@ -42,6 +42,10 @@ timeout -k 10 420 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>
         --kernel "k_rollout<true, true>" --bytes-per-ply 118 --out "$OUT/pmc_k_rollout_full.json" \
   && echo "[gpu_round] $(date +%T) bench --rules full4" \
   && timeout -k 10 300 python bench.py --rules full4 --no-cpu-baseline > "$OUT/bench_full4.json" 2> "$OUT/bench_full4.err" \
+  && echo "[gpu_round] $(date +%T) rocprof kernel trace full4" \
+  && (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$OUT/rocprof_full4" -o bench -- python3 "$ROOT/bench.py" --rules full4 --no-cpu-baseline \
+        > "$OUT/rocprof_full4.log" 2>&1) \
   && echo "[gpu_round] $(date +%T) done"
 rc=$?
 echo "[gpu_round] rc=$rc"
