@@ -172,19 +172,232 @@ __global__ void __launch_bounds__(kBlock) k_legal(Planes pl, int n, Rng g,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Wave-cooperative FULL4 turn (device only).
+//
+// Same rule and result as env_turn_full (narde_rules.h, which the host check
+// runs; the GPU parity tests hold this one to the oracle), organised for
+// SIMT.  The expensive part of a turn is per source: "after this first
+// sub-move, can the other die still move" (two dice) and "after this
+// sub-move, are M-k-1 more still playable" (doubles, a depth-first search).
+// Run per lane, a wave loops as long as its busiest lane while the others
+// idle: on a typical ply ~10 of the 64 lanes roll doubles, and the rest wait.
+// Here every lane publishes its (lane, source) checks; a wave prefix sum of
+// the per-lane counts places them in one task list in LDS, and all 64 lanes
+// take tasks 64 at a time (the owner's state is read back from LDS, results
+// are OR-ed into the owner's mask with ds_or).  Every call is made with the
+// whole wave converged: the turn below is straight-line code with per-lane
+// masks instead of rule branches around the calls.
+struct CoopLds {
+  uint4 snap[64][2];          // owner state: {own w0..w2, O}, {S1, P, low, params}
+  uint32_t task[64 * 16];     // (owner lane << 8) | source; <= 15 sources per lane
+  uint32_t res[64];
+};
+
+__device__ __forceinline__ int wave_prefix(int x, int lane, int& total) {
+  int v = x;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(v, o, 64);
+    if (lane >= o) v += y;
+  }
+  total = __shfl(v, 63, 64);
+  return v - x;
+}
+
+// mode 0 (keep): bit p of L stays iff `need` more sub-moves of die a remain
+//   playable after p -- block-free lower bound first, exact search after;
+// mode 1 (pair): bit p stays iff die b still has a move after p with die a.
+__device__ uint32_t coop_check(CoopLds& W, const Side& s, uint32_t low, int a, int b, int hl,
+                               uint32_t L, int need, bool bf, int mode, int lane) {
+  if (__ballot(L != 0u) == 0ull) return 0u;  // wave-uniform: nothing to check
+  const int cnt = __builtin_popcount(L);
+  int total;
+  const int off = wave_prefix(cnt, lane, total);
+  W.res[lane] = 0u;
+  if (cnt) {
+    W.snap[lane][0] = make_uint4(s.own.w[0], s.own.w[1], s.own.w[2], s.O);
+    W.snap[lane][1] = make_uint4(s.S1o, s.P, low,
+                                 (uint32_t)a | ((uint32_t)b << 4) | ((uint32_t)(hl + 1) << 8) |
+                                     ((uint32_t)need << 12) | ((uint32_t)bf << 16) |
+                                     ((uint32_t)mode << 17) | (s.off_own << 20));
+    uint32_t m = L;
+    int k = off;
+    while (m) {
+      const int p = __builtin_ctz(m);
+      m &= m - 1u;
+      W.task[k++] = ((uint32_t)lane << 8) | (uint32_t)p;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();  // a wave's LDS operations retire in issue order
+  for (int base = 0; base < total; base += 64) {
+    const int t = base + lane;
+    if (t < total) {
+      const uint32_t tk = W.task[t];
+      const int ow = (int)(tk >> 8), p = (int)(tk & 0xFFu);
+      const uint4 x = W.snap[ow][0], y = W.snap[ow][1];
+      Side c;
+      c.own.w[0] = x.x; c.own.w[1] = x.y; c.own.w[2] = x.z;
+      c.O = x.w; c.S1o = y.x; c.P = y.y;
+      c.opp.w[0] = c.opp.w[1] = c.opp.w[2] = 0u;
+      c.S1p = 0u; c.off_opp = 0u; c.ft_own = 0u; c.ft_opp = 0u; c.black = 0u; c.elapsed = 0u; c.t = 0u;
+      const uint32_t lw = y.z, prm = y.w;
+      c.off_own = prm >> 20;
+      const int ta = (int)(prm & 15u), tb = (int)((prm >> 4) & 15u);
+      const int thl = (int)((prm >> 8) & 15u) - 1, tneed = (int)((prm >> 12) & 15u);
+      const bool tbf = (prm >> 16) & 1u;
+      bool ok;
+      if ((prm >> 17) & 1u) {
+        uint32_t O2, S2;
+        child_masks(c, p, ta, O2, S2);
+        uint32_t L2 = die_candidates(O2, c.P, tb);
+        if (!tbf) L2 = die_filter(O2, S2, block_info_low(O2, lw), L2, tb);
+        if (p == 23) L2 &= ~HEAD;
+        ok = L2 != 0u;
+      } else {
+        const int hl2 = thl - (p == 23 ? 1 : 0);
+        ok = false;
+        if (tbf) {
+          uint32_t O2, S2;
+          child_masks(c, p, ta, O2, S2);
+          ok = f4_lower_bound(O2, S2, c.P, ta, hl2) >= tneed;
+        }
+        if (!ok) {
+          apply_die(c, p, ta);
+          ok = tneed == 1 ? f4_reach<1>(c, lw, ta, hl2, tbf)
+                          : (tneed == 2 ? f4_reach<2>(c, lw, ta, hl2, tbf) : f4_reach<3>(c, lw, ta, hl2, tbf));
+        }
+      }
+      if (ok) atomicOr(&W.res[ow], 1u << p);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  return W.res[lane];
+}
+
+// env_turn_full with the per-source checks done cooperatively (see above)
+__device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, const uint32_t w[4],
+                               TurnOut& o, CoopLds& W, int lane) {
+  const uint32_t low = block_lowmask(s.P);
+  const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
+  const bool dbl = dh == dl;
+  const bool bf = turn_block_free(s.O, s.P, low, dh, dl);
+  // first sub-move: the lists, the shortcuts, then every lane's checks at once
+  const uint32_t Lh = legal1(s, low, dh, bf);
+  const uint32_t Ll = dbl ? 0u : legal1(s, low, dl, bf);
+  const bool all_h = !dbl && bf && f4_lower_bound(s.O, s.S1o, s.P, dl, 1) >= 2;
+  const bool all_l = !dbl && bf && f4_lower_bound(s.O, s.S1o, s.P, dh, 1) >= 2;
+  const int hl0 = (dbl && s.ft_own && (dh == 3 || dh == 4 || dh == 6)) ? 2 : 1;
+  const bool fast = dbl && bf && f4_lower_bound(s.O, s.S1o, s.P, dh, hl0) >= 4;
+  const bool srch = dbl && !fast && Lh != 0u;
+  const uint32_t ph = coop_check(W, s, low, dh, dl, 1, (!dbl && !all_h) ? Lh : 0u, 0, bf, 1, lane);
+  const uint32_t pl = coop_check(W, s, low, dl, dh, 1, (!dbl && !all_l) ? Ll : 0u, 0, bf, 1, lane);
+  const uint32_t c3 = coop_check(W, s, low, dh, 0, hl0, srch ? Lh : 0u, 3, bf, 0, lane);
+  const uint32_t c2 = coop_check(W, s, low, dh, 0, hl0, (srch && !c3) ? Lh : 0u, 2, bf, 0, lane);
+  const uint32_t c1 = coop_check(W, s, low, dh, 0, hl0, (srch && !c3 && !c2) ? Lh : 0u, 1, bf, 0, lane);
+  uint32_t Ch, Cl;
+  int M;
+  if (!dbl) {
+    Ch = all_h ? Lh : ph;
+    Cl = all_l ? Ll : pl;
+    if (Ch | Cl) {
+      M = 2;
+    } else {
+      M = (Lh | Ll) ? 1 : 0;
+      Ch = Lh;  // only one die playable: the higher one if it can
+      Cl = Lh ? 0u : Ll;
+    }
+  } else {
+    Cl = 0u;
+    if (fast) { Ch = Lh; M = 4; }
+    else if (!Lh) { Ch = 0u; M = 0; }
+    else if (c3) { Ch = c3; M = 4; }
+    else if (c2) { Ch = c2; M = 3; }
+    else if (c1) { Ch = c1; M = 2; }
+    else { Ch = Lh; M = 1; }
+  }
+  o.legal = (uint64_t)Ch | ((uint64_t)Cl << 24) | ((uint64_t)dh << 48) | ((uint64_t)dl << 52) |
+            ((uint64_t)M << 56);
+  uint64_t played = ~0ull;
+  int hl = hl0;
+  bool go = M >= 1;
+  int d = dh;
+  if (go) {
+    const int nh = __builtin_popcount(Ch), n = nh + __builtin_popcount(Cl);
+    int p;
+    if (play) {
+      p = play_byte(pw, 0);
+      d = play_byte(pw, 1);
+      go = p >= 0 && p < 24 && ((d == dh && ((Ch >> p) & 1u)) || (!dbl && d == dl && ((Cl >> p) & 1u)));
+    } else {
+      const int idx = (int)mulhi_u32(w[0], (uint32_t)n);
+      const bool hi = idx < nh;
+      d = hi ? dh : dl;
+      p = select_bit(hi ? Ch : Cl, hi ? idx : idx - nh);
+    }
+    if (go) {
+      apply_die(s, p, d);
+      played = played_set(played, 0, p, d);
+      hl -= p == 23 ? 1 : 0;
+    }
+  }
+  // sub-moves 1..3 (two dice: only k = 1, with the other die)
+  for (int k = 1; k < 4; ++k) {
+    const bool act = go && k < M;
+    const int dk = dbl ? dh : (d == dh ? dl : dh);
+    uint32_t Lk = act ? legal1(s, low, dk, bf) : 0u;
+    if (hl <= 0) Lk &= ~HEAD;
+    const int need = M - k - 1;
+    const bool direct = !dbl || fast || need <= 0;
+    const uint32_t ck = coop_check(W, s, low, dk, 0, hl, (act && !direct) ? Lk : 0u, need, bf, 0, lane);
+    const uint32_t C = direct ? Lk : ck;
+    if (act) {
+      int p;
+      bool ok = true;
+      if (play) {
+        p = play_byte(pw, 2 * k);
+        ok = play_byte(pw, 2 * k + 1) == dk && p >= 0 && p < 24 && ((C >> p) & 1u);
+      } else {
+        const uint32_t wk = k == 1 ? w[1] : (k == 2 ? w[2] : w[3]);
+        p = select_bit(C, (int)mulhi_u32(wk, (uint32_t)__builtin_popcount(C)));
+      }
+      if (ok) {
+        apply_die(s, p, dk);
+        played = played_set(played, k, p, dk);
+        hl -= p == 23 ? 1 : 0;
+      } else {
+        go = false;
+      }
+    }
+  }
+  o.played = played;
+  o.max_dice = M;
+  o.term = s.off_own == 15u;
+  o.reward = o.term ? (s.off_opp > 0u ? 1 : 2) : 0;
+  if (!o.term) side_flip(s);
+}
+
+// this wave's slice of the block's cooperative scratch
+#define COOP_LDS_DECL                                  \
+  __shared__ CoopLds coop_lds[kBlock / 64];           \
+  CoopLds& wave_coop = coop_lds[threadIdx.x >> 6];
+
 // FULL4 first-sub-move set C_0 and max dice M for the given (or the next
 // device) dice: the turn engine run on a copy with a play whose first
 // sub-move is invalid, so nothing is applied.
 __global__ void __launch_bounds__(kBlock) k_legal_full(Planes pl, int n, Rng g,
                                                        const uint8_t* __restrict__ dice2,
                                                        uint64_t* __restrict__ out) {
+  COOP_LDS_DECL
   const int i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  Side s = side_from_record(pl.p0[i], pl.p1[i]);
-  int d0, d1;
+  const bool valid = i < n;  // no early exit: the turn is wave-cooperative
+  Side s = valid ? side_from_record(pl.p0[i], pl.p1[i]) : side_start(0u);
+  int d0 = 1, d1 = 2;
   if (dice2) {
-    d0 = dice2[2 * i];
-    d1 = dice2[2 * i + 1];
+    if (valid) {
+      d0 = dice2[2 * i];
+      d1 = dice2[2 * i + 1];
+    }
   } else {
     uint32_t r[4];
     draw(g, s.t, (uint32_t)i, 0u, r);
@@ -192,8 +405,9 @@ __global__ void __launch_bounds__(kBlock) k_legal_full(Planes pl, int n, Rng g,
   }
   const uint32_t w[4] = {0u, 0u, 0u, 0u};
   TurnOut o;
-  env_turn_full(s, d0, d1, true, ~0ull, w, o);  // play word of -1s: nothing is applied
-  out[i] = o.legal;
+  // play word of -1s: nothing is applied
+  coop_turn_full(s, d0, d1, true, ~0ull, w, o, wave_coop, (int)(threadIdx.x & 63));
+  if (valid) out[i] = o.legal;
 }
 
 // per-ply outputs; a rollout writes ply p of env i at [p * n + i]
@@ -332,18 +546,24 @@ __device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t i,
           autoreset, o, term, trunc);
 }
 
-// one FULL4 ply (a whole turn per step)
-__device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t i, const int8_t* play,
-                                    const uint8_t* dice, int max_steps, bool autoreset, TurnOut& o,
-                                    int& term, int& trunc) {
+// one FULL4 ply (a whole turn per step), the turn
+// played wave-cooperatively: every lane of the wave must call it (lanes past
+// the last env pass valid = false and a dummy state)
+__device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t i, bool valid,
+                                    const int8_t* play, const uint8_t* dice, int max_steps,
+                                    bool autoreset, TurnOut& o, int& term, int& trunc, CoopLds& W) {
   uint32_t r[4];
   draw(g, s.t, i, 0u, r);
-  int d0 = 0, d1 = 0;
-  if (dice) { d0 = dice[2 * i]; d1 = dice[2 * i + 1]; }
+  int d0 = 1, d1 = 2;
+  if (dice && valid) { d0 = dice[2 * i]; d1 = dice[2 * i + 1]; }
   // one 8-B load per env: the play's four (from, die) pairs
-  const uint64_t pw = play ? reinterpret_cast<const uint64_t*>(play)[i] : 0ull;
-  env_ply_full(s, st, r, g.env0 + i, g.k0, g.k1, dice != nullptr, d0, d1, g.dice_mode,
-               play != nullptr, pw, max_steps, autoreset, o, term, trunc);
+  const uint64_t pw = (play && valid) ? reinterpret_cast<const uint64_t*>(play)[i] : ~0ull;
+  const int lane = (int)(threadIdx.x & 63);
+  env_ply_full_with(s, st, r, g.env0 + i, g.k0, g.k1, dice != nullptr, d0, d1, g.dice_mode,
+                    play != nullptr, pw, max_steps, autoreset, o, term, trunc,
+                    [&](Side& s2, int a, int b, bool pl, uint64_t pw2, const uint32_t* w2, TurnOut& o2) {
+                      coop_turn_full(s2, a, b, pl, pw2, w2, o2, W, lane);
+                    });
 }
 
 __device__ __forceinline__ void add_stats(int4* __restrict__ stats, int i, const int4& st) {
@@ -359,16 +579,20 @@ __device__ __forceinline__ void add_stats(int4* __restrict__ stats, int i, const
 template <bool kFull>
 __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
   OBS_LDS_DECL
+  COOP_LDS_DECL
   const int i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= a.n) return;
-  Side s = side_from_record(a.pl.p0[i], a.pl.p1[i]);
+  const bool valid = i < a.n;
+  if (!kFull && !valid) return;  // FULL4 lanes stay: its turn is wave-cooperative
+  Side s = valid ? side_from_record(a.pl.p0[i], a.pl.p1[i]) : side_start(0u);
   int4 st = make_int4(0, 0, 0, 0);
   typename std::conditional<kFull, TurnOut, StepOut>::type o;
   int term, trunc;
   if constexpr (kFull)
-    ply(s, st, a.g, (uint32_t)i, a.play, a.dice, a.max_steps, a.autoreset != 0, o, term, trunc);
+    ply(s, st, a.g, (uint32_t)i, valid, a.play, a.dice, a.max_steps, a.autoreset != 0, o, term, trunc,
+        wave_coop);
   else
     ply(s, st, a.g, (uint32_t)i, a.actions, a.dice, a.max_steps, a.autoreset != 0, o, term, trunc);
+  if (!valid) return;
   uint4 ra, rb;
   side_to_record(s, ra, rb);
   a.pl.p0[i] = ra;
@@ -385,20 +609,24 @@ template <bool kOut, bool kFull>
 __global__ void __launch_bounds__(kBlock) k_rollout(Planes pl, int n, Rng g, int plies, int max_steps,
                                                     Outs out) {
   OBS_LDS_DECL
+  COOP_LDS_DECL
   const int i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
+  const bool valid = i < n;
+  if (!kFull && !valid) return;  // FULL4 lanes stay: its turn is wave-cooperative
   const bool wave_full = i - (int)(threadIdx.x & 63) + 64 <= n;
-  Side s = side_from_record(pl.p0[i], pl.p1[i]);
+  Side s = valid ? side_from_record(pl.p0[i], pl.p1[i]) : side_start(0u);
   int4 st = make_int4(0, 0, 0, 0);
   for (int p = 0; p < plies; ++p) {
     typename std::conditional<kFull, TurnOut, StepOut>::type o;
     int term, trunc;
     if constexpr (kFull)
-      ply(s, st, g, (uint32_t)i, (const int8_t*)nullptr, nullptr, max_steps, true, o, term, trunc);
+      ply(s, st, g, (uint32_t)i, valid, (const int8_t*)nullptr, nullptr, max_steps, true, o, term, trunc,
+          wave_coop);
     else
       ply(s, st, g, (uint32_t)i, (const int16_t*)nullptr, nullptr, max_steps, true, o, term, trunc);
-    if (kOut) store_outs(out, (size_t)p * n + i, s, o, term, trunc, wave_lds, wave_full);
+    if (kOut && valid) store_outs(out, (size_t)p * n + i, s, o, term, trunc, wave_lds, wave_full);
   }
+  if (!valid) return;
   uint4 ra, rb;
   side_to_record(s, ra, rb);
   pl.p0[i] = ra;

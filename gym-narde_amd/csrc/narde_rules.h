@@ -868,10 +868,14 @@ NARDE_FN void env_ply(Side& s, int4& st, const uint32_t r[4], bool have_dice, in
 // One FULL4 ply: env_ply with a whole turn per step.  Pick words w = {r1,
 // r2, q0, q1}, q = Philox4x32-10(ctr = {t, env, 0, 2}) drawn only on doubles
 // (the only turns with more than two sub-moves).
-NARDE_FN void env_ply_full(Side& s, int4& st, const uint32_t r[4], uint32_t env, uint32_t k0,
-                           uint32_t k1, bool have_dice, int d0, int d1, int dice_mode, bool play,
-                           uint64_t pw, int max_steps, bool autoreset, TurnOut& o, int& term,
-                           int& trunc) {
+// Turn = the function that plays the turn (env_turn_full, or the device's
+// wave-cooperative equivalent), called as turn(s, d0, d1, play, pw, w, o)
+// with every lane converged.
+template <class Turn>
+NARDE_FN void env_ply_full_with(Side& s, int4& st, const uint32_t r[4], uint32_t env, uint32_t k0,
+                                uint32_t k1, bool have_dice, int d0, int d1, int dice_mode, bool play,
+                                uint64_t pw, int max_steps, bool autoreset, TurnOut& o, int& term,
+                                int& trunc, Turn&& turn) {
   if (!have_dice) dice_from(r[0], dice_mode, d0, d1);
   uint32_t w[4] = {r[1], r[2], 0u, 0u};
   if (d0 == d1 && !play) {
@@ -881,7 +885,7 @@ NARDE_FN void env_ply_full(Side& s, int4& st, const uint32_t r[4], uint32_t env,
     w[3] = q[1];
   }
   const uint32_t mover_black = s.black;
-  env_turn_full(s, d0, d1, play, pw, w, o);
+  turn(s, d0, d1, play, pw, w, o);
   s.elapsed += 1u;
   term = o.term;
   trunc = max_steps > 0 && s.elapsed >= (uint32_t)max_steps;
@@ -898,6 +902,17 @@ NARDE_FN void env_ply_full(Side& s, int4& st, const uint32_t r[4], uint32_t env,
     }
   }
   s.t += 1u;
+}
+
+NARDE_FN void env_ply_full(Side& s, int4& st, const uint32_t r[4], uint32_t env, uint32_t k0,
+                           uint32_t k1, bool have_dice, int d0, int d1, int dice_mode, bool play,
+                           uint64_t pw, int max_steps, bool autoreset, TurnOut& o, int& term,
+                           int& trunc) {
+  env_ply_full_with(s, st, r, env, k0, k1, have_dice, d0, d1, dice_mode, play, pw, max_steps,
+                    autoreset, o, term, trunc,
+                    [](Side& s2, int a, int b, bool pl, uint64_t pw2, const uint32_t* w2, TurnOut& o2) {
+                      env_turn_full(s2, a, b, pl, pw2, w2, o2);
+                    });
 }
 
 }  // namespace narde
