@@ -260,7 +260,7 @@ __device__ uint32_t coop_check(CoopLds& W, const Side& s, uint32_t low, int a, i
         if (tbf) {
           uint32_t O2, S2;
           child_masks(c, p, ta, O2, S2);
-          ok = f4_lower_bound(O2, S2, c.P, ta, hl2) >= tneed;
+          ok = f4_chain_bound(O2, S2, c.P, ta, hl2) >= tneed;
         }
         if (!ok) {
           apply_die(c, p, ta);
@@ -281,7 +281,11 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   const uint32_t low = block_lowmask(s.P);
   const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
   const bool dbl = dh == dl;
+#if NARDE_DIAG_ABLATE & 4
+  const bool bf = true;  // DIAGNOSTIC timing only: wrong results
+#else
   const bool bf = turn_block_free(s.O, s.P, low, dh, dl);
+#endif
   // first sub-move: the lists, the shortcuts, then every lane's checks at once
   const uint32_t Lh = legal1(s, low, dh, bf);
   const uint32_t Ll = dbl ? 0u : legal1(s, low, dl, bf);
@@ -289,12 +293,25 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   const bool all_l = !dbl && bf && f4_lower_bound(s.O, s.S1o, s.P, dh, 1) >= 2;
   const int hl0 = (dbl && s.ft_own && (dh == 3 || dh == 4 || dh == 6)) ? 2 : 1;
   const bool fast = dbl && bf && f4_lower_bound(s.O, s.S1o, s.P, dh, hl0) >= 4;
-  const bool srch = dbl && !fast && Lh != 0u;
+  // not fast: the chain bound may still prove M = 4 (no search for M) and,
+  // when >= 7, every first sub-move (a sub-move lowers it by <= 4)
+  const int cb0 = (dbl && bf && !fast) ? f4_chain_bound(s.O, s.S1o, s.P, dh, hl0) : 0;
+  const bool m4 = fast || cb0 >= 4;
+  const bool srch = dbl && !fast && Lh != 0u && cb0 < 7;
+#if NARDE_DIAG_ABLATE & 1
+  const uint32_t ph = Lh, pl = Ll;  // DIAGNOSTIC timing only: wrong results
+#else
   const uint32_t ph = coop_check(W, s, low, dh, dl, 1, (!dbl && !all_h) ? Lh : 0u, 0, bf, 1, lane);
   const uint32_t pl = coop_check(W, s, low, dl, dh, 1, (!dbl && !all_l) ? Ll : 0u, 0, bf, 1, lane);
+#endif
+#if NARDE_DIAG_ABLATE & 2
+  const uint32_t c3 = Lh, c2 = Lh, c1 = Lh;  // DIAGNOSTIC timing only: wrong results
+#else
   const uint32_t c3 = coop_check(W, s, low, dh, 0, hl0, srch ? Lh : 0u, 3, bf, 0, lane);
-  const uint32_t c2 = coop_check(W, s, low, dh, 0, hl0, (srch && !c3) ? Lh : 0u, 2, bf, 0, lane);
-  const uint32_t c1 = coop_check(W, s, low, dh, 0, hl0, (srch && !c3 && !c2) ? Lh : 0u, 1, bf, 0, lane);
+  const uint32_t c2 = coop_check(W, s, low, dh, 0, hl0, (srch && !m4 && !c3) ? Lh : 0u, 2, bf, 0, lane);
+  const uint32_t c1 =
+      coop_check(W, s, low, dh, 0, hl0, (srch && !m4 && !c3 && !c2) ? Lh : 0u, 1, bf, 0, lane);
+#endif
   uint32_t Ch, Cl;
   int M;
   if (!dbl) {
@@ -309,7 +326,7 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
     }
   } else {
     Cl = 0u;
-    if (fast) { Ch = Lh; M = 4; }
+    if (fast || (cb0 >= 7 && Lh)) { Ch = Lh; M = 4; }
     else if (!Lh) { Ch = 0u; M = 0; }
     else if (c3) { Ch = c3; M = 4; }
     else if (c2) { Ch = c2; M = 3; }
@@ -344,12 +361,18 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   // sub-moves 1..3 (two dice: only k = 1, with the other die)
   for (int k = 1; k < 4; ++k) {
     const bool act = go && k < M;
+    if (__ballot(act) == 0ull) break;  // wave-uniform: no lane has sub-move k
     const int dk = dbl ? dh : (d == dh ? dl : dh);
     uint32_t Lk = act ? legal1(s, low, dk, bf) : 0u;
     if (hl <= 0) Lk &= ~HEAD;
     const int need = M - k - 1;
-    const bool direct = !dbl || fast || need <= 0;
+    const bool direct = !dbl || fast || need <= 0 ||
+                        (act && bf && f4_chain_bound(s.O, s.S1o, s.P, dk, hl) >= need + 4);
+#if NARDE_DIAG_ABLATE & 2
+    const uint32_t ck = Lk;
+#else
     const uint32_t ck = coop_check(W, s, low, dk, 0, hl, (act && !direct) ? Lk : 0u, need, bf, 0, lane);
+#endif
     const uint32_t C = direct ? Lk : ck;
     if (act) {
       int p;
@@ -443,6 +466,13 @@ struct StepArgs {
 // 0 = one wave per 64 envs (k_rollout; A/B diagnostic builds only)
 #ifndef NARDE_ROLLOUT_PC
 #define NARDE_ROLLOUT_PC 1
+#endif
+
+// DIAGNOSTIC ablations of the cooperative FULL4 turn (timing only; results
+// are wrong): 1 no two-dice checks, 2 no doubles searches, 4 all turns
+// treated as block-free
+#ifndef NARDE_DIAG_ABLATE
+#define NARDE_DIAG_ABLATE 0
 #endif
 
 // wave priority in k_rollout_pc (diagnostic knob): 0 none (age decides),

@@ -600,6 +600,33 @@ NARDE_FN int f4_lower_bound(uint32_t O, uint32_t S1, uint32_t P, int d, int hl) 
   return __builtin_popcount(body) + __builtin_popcount(body & ~S1) + head;
 }
 
+// The same with chains: a checker also walks on from its landing while the
+// next landing is free of the opponent (and bears off at the end when all
+// are home -- only counted if all are home already, which a turn never
+// undoes).  Chains of different checkers do not interfere, so
+//   sum over sources x of min(count, 2) * chain(x)   (head: min(hl, 2))
+// sub-moves are playable (block-free turns).  One sub-move lowers it by at
+// most chain <= 4.
+NARDE_FN int f4_chain_bound(uint32_t O, uint32_t S1, uint32_t P, int d, int hl) {
+  const uint32_t gn = (~P << d) & (MASK24 << d) & MASK24;       // y: y - d on the board, free
+  const uint32_t go = ((O >> 6) == 0u) ? ((1u << d) - 1u) : 0u;  // y: bears off
+  const uint32_t a = gn | go;
+  const uint32_t keep = hl > 0 ? O : (O & ~HEAD);
+  const uint32_t g1 = gn & (gn << d), g2 = g1 & (gn << (2 * d));
+  const uint32_t c1 = keep & a;
+  const uint32_t c2 = keep & gn & (a << d);
+  const uint32_t c3 = keep & g1 & (a << (2 * d));
+  const uint32_t c4 = keep & g2 & (a << (3 * d));
+  const uint32_t multi = ~S1 & ~HEAD;
+  const int hm = (hl >= 2 && !(S1 & HEAD)) ? 2 : 1;
+  int lb = __builtin_popcount(c1 & ~HEAD) + __builtin_popcount(c2 & ~HEAD) +
+           __builtin_popcount(c3 & ~HEAD) + __builtin_popcount(c4 & ~HEAD) +
+           __builtin_popcount(c1 & multi) + __builtin_popcount(c2 & multi) +
+           __builtin_popcount(c3 & multi) + __builtin_popcount(c4 & multi);
+  lb += hm * (int)(((c1 >> 23) & 1u) + ((c2 >> 23) & 1u) + ((c3 >> 23) & 1u) + ((c4 >> 23) & 1u));
+  return lb;
+}
+
 // the sources of L (die d) after which NEED more sub-moves stay playable:
 // block-free turns try the lower bound first, the exact search only where
 // it falls short
