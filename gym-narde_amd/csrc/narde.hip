@@ -945,6 +945,67 @@ __global__ void __launch_bounds__(kBlock) k_mask576_move2(Planes pl, int n, Rng 
   for (int q = 0; q < 9; ++q) mask[(size_t)i * 9 + q] = m[q];
 }
 
+// Masked epsilon-greedy over the 576 action codes for a Q-value row per env
+// (the policy half of train_deepq_pytorch.py:411-600, batched): one wave per
+// row, lane l reads codes l + 64 j (coalesced), the legal ones are compared
+// and a wave reduction keeps the largest value, lowest code on ties
+// (torch.argmax's first maximum).  With probability epsilon the code is
+// uniform over the legal ones instead; 0 where none is legal (the
+// reference's "no move" code, :504-505).  Draws: Philox4x32-10({tag, row, 0,
+// 5}, seed): r0 < epsilon * 2^32 explores, one shared decision for both
+// heads of a step (same tag); the pick is mulhi(r1 or r2 by head, count).
+__global__ void __launch_bounds__(256) k_policy576(const float* __restrict__ q, int64_t ldq,
+                                                   const uint64_t* __restrict__ mask, int n,
+                                                   uint64_t eps_q32, uint32_t k0, uint32_t k1,
+                                                   uint32_t tag, int head, int64_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  if (row >= n) return;  // whole waves: the row is uniform over the wave
+  uint64_t mw[9];
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    mw[j] = mask[(size_t)row * 9 + j];
+    cnt += __builtin_popcountll(mw[j]);
+  }
+  uint32_t r[4];
+  philox4x32_10(tag, (uint32_t)row, 0u, 5u, k0, k1, r);
+  const bool explore = (uint64_t)r[0] < eps_q32;
+  int code = 0;
+  if (cnt > 0 && explore) {
+    int k = (int)mulhi_u32(head ? r[2] : r[1], (uint32_t)cnt);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int c = __builtin_popcountll(mw[j]);
+      if (k >= 0 && k < c) {
+        uint64_t m = mw[j];
+        for (int t = 0; t < k; ++t) m &= m - 1ull;
+        code = 64 * j + __builtin_ctzll(m);
+      }
+      k -= c;
+    }
+  } else if (cnt > 0) {
+    const float* qr = q + (size_t)row * (size_t)ldq;
+    float best = -__builtin_inff();
+    int bi = 0x7FFFFFFF;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      if ((mw[j] >> lane) & 1ull) {
+        const float v = qr[64 * j + lane];
+        if (v > best) { best = v; bi = 64 * j + lane; }  // j ascending: first max kept
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    code = bi;
+  }
+  if (lane == 0) out[row] = code;
+}
+
 __global__ void __launch_bounds__(kBlock) k_block(const int8_t* __restrict__ boards, int n,
                                                   uint8_t* __restrict__ out) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
@@ -1301,6 +1362,20 @@ int narde_legal_mask576_move2(narde_env* e, const int16_t* move1, const uint8_t*
   k_mask576_move2<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), move1, dice,
                                                                   mask);
   return check_launch("k_mask576_move2");
+}
+
+int narde_policy_masked_argmax576(int device, const float* q, int64_t ldq, const uint64_t* mask, int64_t n,
+                                  float epsilon, uint64_t seed, uint32_t tag, int head, int64_t* out,
+                                  void* stream) {
+  if (!q || !mask || !out || n < 0 || n > (int64_t(1) << 31) - 4 || ldq < 576)
+    return fail(NARDE_EINVAL, "bad argument");
+  if (n == 0) return NARDE_OK;
+  const double e = epsilon <= 0.0f ? 0.0 : (epsilon >= 1.0f ? 1.0 : (double)epsilon);
+  const uint64_t eps_q32 = (uint64_t)(e * 4294967296.0);
+  DeviceGuard dg(device);
+  k_policy576<<<(int)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(q, ldq, mask, (int)n, eps_q32, (uint32_t)seed,
+                                                                   (uint32_t)(seed >> 32), tag, head, out);
+  return check_launch("k_policy576");
 }
 
 int narde_violates_block_rule(int device, const int8_t* boards, int64_t n, uint8_t* out, void* stream) {

@@ -32,8 +32,12 @@ move2_head(cat(features, onehot(m1))) = features @ Wf^T + Wm[:, m1] + b with
 W = [Wf | Wm]: mathematically identical to the reference's one-hot concat,
 equal in fp32 up to summation order (tests/test_dqn_cpu.py).
 """
+import ctypes
+
 import torch
 import torch.nn as nn
+
+from . import _lib
 
 MOVES = 576
 
@@ -75,10 +79,29 @@ def expand_mask(mask576):
 
 def masked_argmax(scores, mask):
     """argmax over legal entries; 0 where nothing is legal (the reference's
-    'no move' code, train_deepq_pytorch.py:504-505)."""
+    'no move' code, train_deepq_pytorch.py:504-505).  Torch reference of
+    policy_576's greedy half."""
     neg = torch.finfo(scores.dtype).min
     best = scores.masked_fill(~mask, neg).argmax(1)
     return torch.where(mask.any(1), best, torch.zeros_like(best))
+
+
+def policy_576(q, mask576, epsilon, seed, tag, head, out=None):
+    """Masked epsilon-greedy codes (B,) int64 from Q-values (B,576) f32 and
+    the env's (B,9) bit masks: one HIP kernel (k_policy576), no (B,576)
+    intermediates.  Same tag for both heads of a step = one shared explore
+    decision per env."""
+    q = q.contiguous()
+    if q.dtype != torch.float32 or q.shape[1] != MOVES:
+        raise ValueError("q must be (B, 576) float32")
+    if out is None:
+        out = torch.empty(q.shape[0], dtype=torch.int64, device=q.device)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(q.device).cuda_stream)
+    _lib.check(_lib.load().narde_policy_masked_argmax576(
+        q.device.index, _lib.ptr(q), q.stride(0), _lib.ptr(mask576.contiguous()), q.shape[0],
+        float(epsilon), int(seed) & (2 ** 64 - 1), int(tag) & 0xFFFFFFFF, int(head), _lib.ptr(out),
+        stream), "narde_policy_masked_argmax576")
+    return out
 
 
 class DeviceReplay:
@@ -118,9 +141,14 @@ class DeviceReplay:
 
     def sample(self, batch, generator=None):
         p = self.prio[: self.size] ** self.alpha
-        probs = p / p.sum()
-        idx = torch.multinomial(probs, batch, replacement=True, generator=generator)
-        w = (self.size * probs[idx]) ** (-self.beta)
+        cdf = torch.cumsum(p, 0)
+        total = cdf[-1]
+        # inverse-CDF sampling (torch.multinomial over 1M categories spends
+        # ~0.5 ms renormalising one huge row)
+        u = torch.rand(batch, device=p.device, generator=generator) * total
+        idx = torch.searchsorted(cdf, u, right=True).clamp_(max=self.size - 1)
+        probs_idx = p[idx] / total
+        w = (self.size * probs_idx) ** (-self.beta)
         w = w / w.max()
         self.beta = min(1.0, self.beta + self.beta_increment)
         return idx, w
@@ -156,6 +184,8 @@ class BatchedDQNDriver:
         self.epsilon, self.epsilon_min, self.epsilon_decay = epsilon, epsilon_min, epsilon_decay
         self.target_update, self.updates_per_step = target_update, updates_per_step
         self.shaping = shaping
+        self.seed = seed
+        self.steps = 0
         self.train_steps = 0
         B = env.num_envs
         self.off_seen = torch.zeros((B, 2), dtype=torch.float32, device=self.dev)
@@ -168,25 +198,25 @@ class BatchedDQNDriver:
             return self.env.tesauro198().clone()
         return self.env.observe().to(torch.float32)
 
-    def _off_counts(self):
-        """(B,2) borne-off counts (white, black) and the current player (+1/-1)."""
+    def _off_counts(self, obs):
+        """(B,2) borne-off counts (white, black) and the current player (+1/-1):
+        read off the 198-float obs (off/15 at 97 and 195, player one-hot at
+        196) when that is the observation, else from the env state."""
+        if self.obs_kind == "tesauro198":
+            off = torch.round(obs[:, [97, 195]] * 15.0)
+            return off, torch.where(obs[:, 196] > 0.5, 1.0, -1.0)
         st = self.env.get_state()
         return st["off"].to(torch.float32), st["player"].to(torch.float32)
 
     @torch.no_grad()
     def act(self, x):
-        """Masked epsilon-greedy (move1, move2) codes for the next step."""
-        B = x.shape[0]
-        m1 = expand_mask(self.env.legal_mask())
+        """Masked epsilon-greedy (move1, move2) codes for the next step: the
+        env's exact legal masks and the fused policy kernel."""
+        tag = self.steps
         f = self.model.features(x)
-        q1 = self.model.move1_head(f)
-        explore = torch.rand(B, device=self.dev, generator=self.gen) < self.epsilon
-        rnd1 = torch.rand((B, MOVES), device=self.dev, generator=self.gen)
-        a1 = masked_argmax(torch.where(explore.unsqueeze(1), rnd1, q1), m1)
-        m2 = expand_mask(self.env.legal_mask_move2(a1.to(torch.int16)))
-        q2 = self.model.move2_from_features(f, a1)
-        rnd2 = torch.rand((B, MOVES), device=self.dev, generator=self.gen)
-        a2 = masked_argmax(torch.where(explore.unsqueeze(1), rnd2, q2), m2)
+        a1 = policy_576(self.model.move1_head(f), self.env.legal_mask(), self.epsilon, self.seed, tag, 0)
+        m2 = self.env.legal_mask_move2(a1.to(torch.int16))
+        a2 = policy_576(self.model.move2_from_features(f, a1), m2, self.epsilon, self.seed, tag, 1)
         return torch.stack([a1, a2], 1)
 
     def step(self):
@@ -195,18 +225,19 @@ class BatchedDQNDriver:
         _, reward, term, trunc, _ = self.env.step(actions.to(torch.int16))
         r = reward.to(torch.float32)
         done = (term | trunc).to(torch.float32)
+        nxt = self._observe()
+        self.steps += 1
         if self.shaping:
             # train_deepq_pytorch.py:885-908: +1 per checker newly borne off
             # and +0.1 x total off, for env.unwrapped.current_player read AFTER
             # the step (the reference reads the post-flip player)
-            off, player = self._off_counts()
+            off, player = self._off_counts(nxt)
             col = (player < 0).long()
             now = off.gather(1, col.unsqueeze(1)).squeeze(1)
             before = self.off_seen.gather(1, col.unsqueeze(1)).squeeze(1)
             r = r + (now - before).clamp(min=0) + 0.1 * now
             self.off_seen.scatter_(1, col.unsqueeze(1), now.unsqueeze(1))
             self.off_seen.mul_((1.0 - done).unsqueeze(1))  # new episode: trackers restart at 0
-        nxt = self._observe()
         self.replay.add(x, actions, r, nxt, done)
         self.state = nxt
         loss = None

@@ -188,6 +188,19 @@ int narde_legal_mask576(narde_env *env, uint64_t *mask, void *stream);
 int narde_legal_mask576_move2(narde_env *env, const int16_t *move1, const uint8_t *dice,
                               uint64_t *mask, void *stream);
 
+/* Masked epsilon-greedy over the 576 codes (the policy of
+ * train_deepq_pytorch.py:411-600, batched; stateless): q f32[n][ldq]
+ * (ldq >= 576) Q-values, mask u64[n][9] legal codes (the two mask entry
+ * points above).  out i64[n] = the legal code with the largest Q (lowest
+ * code on ties, as torch.argmax), or with probability epsilon a legal code
+ * uniformly at random, or 0 when none is legal.  Draws are Philox4x32-10
+ * ({tag, row, 0, 5}, seed); the explore decision depends only on (seed, tag,
+ * row), so both heads of one step called with the same tag explore together
+ * (head 0 / 1 select independent picks). */
+int narde_policy_masked_argmax576(int device, const float *q, int64_t ldq, const uint64_t *mask,
+                                  int64_t n, float epsilon, uint64_t seed, uint32_t tag, int head,
+                                  int64_t *out, void *stream);
+
 /* Stateless: Narde._violates_block_rule on n perspective boards i8[n][24]. */
 int narde_violates_block_rule(int device, const int8_t *boards, int64_t n, uint8_t *out,
                               void *stream);

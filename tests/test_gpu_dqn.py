@@ -82,3 +82,32 @@ def test_reference_step_accepts_driver_actions():
     ref = O.step(st["board"], st["off"], st["first_turn"], st["player"], dice, a)
     played1 = ref["count2"] >= 0
     assert (played1 | (ref["count1"] < 2)).all()
+
+
+def test_policy_kernel_matches_torch_and_explores_legally():
+    from gym_narde.dqn import expand_mask, masked_argmax, policy_576
+    from gym_narde.vector import VecNardeEnv
+
+    env = VecNardeEnv(8192, device="cuda:0", seed=3)
+    env.selfplay(29)
+    words = env.legal_mask()
+    m = expand_mask(words)
+    q = torch.randn((8192, 576), device="cuda:0")
+    q[:, 100] = q[:, 7]  # ties: the lowest legal code wins, as torch.argmax
+    greedy = policy_576(q, words, 0.0, seed=1, tag=0, head=0)
+    assert torch.equal(greedy, masked_argmax(q, m))
+    ex = policy_576(q, words, 1.0, seed=1, tag=5, head=0)
+    rows = torch.arange(8192, device="cuda:0")
+    has = m.any(1)
+    assert bool(m[rows, ex][has].all()) and bool((ex[~has] == 0).all())
+    # uniform over the legal codes: per-row counts of the picked rank
+    ranks = (m.long().cumsum(1)[rows, ex] - 1)[has].float()
+    cnt = m.sum(1)[has].float()
+    u = (ranks + 0.5) / cnt
+    assert abs(float(u.mean()) - 0.5) < 0.02
+    # one shared explore decision per (seed, tag, row) for both heads
+    e1 = policy_576(q, words, 0.5, seed=9, tag=11, head=0) != greedy
+    e2 = policy_576(q, words, 0.5, seed=9, tag=11, head=1) != greedy
+    both = has & (m.sum(1) > 3)
+    agree = (e1 == e2)[both].float().mean()
+    assert float(agree) > 0.6
