@@ -140,6 +140,29 @@ class VecNardeEnv:
         self.handle.call("narde_observe", None, _lib.ptr(out), self._s())
         return out
 
+    def observe_host(self, kind="int24", out=None):
+        """Observations for CPU-side agents:
+        the observe kernel writes the device buffer and a non-blocking copy
+        lands it in PINNED host memory on the same stream.  Returns (host
+        tensor, event); read the host tensor after event.synchronize().
+        kind: "int24" (the reference's int32[24] obs) or "tesauro198"."""
+        t = self.torch
+        if kind == "int24":
+            dev, shape, dt = self.observe(), (self.num_envs, 24), t.int32
+        elif kind == "tesauro198":
+            dev, shape, dt = self.tesauro198(), (self.num_envs, 198), t.float32
+        else:
+            raise ValueError("kind must be 'int24' or 'tesauro198'")
+        if out is None:
+            out = t.empty(shape, dtype=dt, pin_memory=True)
+        elif tuple(out.shape) != shape or out.dtype != dt or not out.is_pinned():
+            raise ValueError(f"out must be a pinned {dt} tensor of shape {shape}")
+        out.copy_(dev, non_blocking=True)
+        ev = t.cuda.Event()
+        ev.record(t.cuda.current_stream(self.device))
+        self._keep_host = dev  # the source stays alive until the copy is done
+        return out, ev
+
     def dice(self):
         """Dice of the next device-RNG step, (B,2) uint8 in roll order."""
         d = self.torch.empty((self.num_envs, 2), dtype=self.torch.uint8, device=self.device)

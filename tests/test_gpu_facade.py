@@ -116,3 +116,20 @@ def test_make_timelimit_truncates_at_1000():
         if term:
             break
     assert trunc and k == 999
+
+
+def test_observe_host_pinned():
+    """f-4: observations land in pinned host memory, equal to the device ones."""
+    from gym_narde.vector import VecNardeEnv
+
+    env = VecNardeEnv(4096, device="cuda:0", seed=8)
+    env.selfplay(17)
+    host, ev = env.observe_host("int24")
+    ev.synchronize()
+    assert host.is_pinned() and torch.equal(host, env.observe().cpu())
+    h2, ev2 = env.observe_host("tesauro198")
+    ev2.synchronize()
+    assert h2.is_pinned() and torch.equal(h2, env.tesauro198().cpu())
+    h3, ev3 = env.observe_host("int24", out=host)  # reuse the pinned buffer
+    ev3.synchronize()
+    assert h3.data_ptr() == host.data_ptr()
