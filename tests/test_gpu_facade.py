@@ -133,3 +133,19 @@ def test_observe_host_pinned():
     h3, ev3 = env.observe_host("int24", out=host)  # reuse the pinned buffer
     ev3.synchronize()
     assert h3.data_ptr() == host.data_ptr()
+
+
+def test_example_play_random_agent_runs():
+    """configs[0] plumbing: the examples/play_random_agent.py counterpart
+    plays whole games through gym_narde.make (both agent modes)."""
+    import importlib.util
+    import os
+
+    path = os.path.join(os.path.dirname(__file__), "..", "examples", "play_random_agent.py")
+    spec = importlib.util.spec_from_file_location("play_random_agent", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    wins, lengths = mod.make_plays(games=3, seed=0, legal=True)
+    assert len(lengths) == 3 and sum(wins.values()) + sum(1 for x in lengths if x >= 1000) >= 3
+    wins, lengths = mod.make_plays(games=1, seed=1, legal=False)
+    assert len(lengths) == 1
