@@ -443,8 +443,11 @@ struct StepOut {
 // NardeEnv.step (narde_env.py:27-103) with dice (d0, d1) in roll order.
 // policy: draw code1 from list1 with r1 and code2 from the env's own second
 // list with r2 (the build's random-legal policy); otherwise use code1/code2.
+// flip_always: flip even after the game ended -- for callers that reset a
+// terminated env in the same ply anyway (auto-reset), where it saves the
+// divergent branch around the flip
 NARDE_FN void env_step(Side& s, int d0, int d1, int code1, int code2, bool policy, uint32_t r1,
-                       uint32_t r2, StepOut& o) {
+                       uint32_t r2, StepOut& o, bool flip_always = false) {
   legal2(s, d0, d1, o.l1);
   o.L2 = 0u; o.d2 = 0; o.count2 = -1;
   const int n1 = o.l1.count;
@@ -499,7 +502,7 @@ NARDE_FN void env_step(Side& s, int d0, int d1, int code1, int code2, bool polic
   // _check_game_ended (narde_env.py:134-141): only the mover is checked
   o.term = s.off_own == 15u;
   o.reward = o.term ? (s.off_opp > 0u ? 1 : 2) : 0;
-  if (!o.term) side_flip(s);
+  if (flip_always || !o.term) side_flip(s);
 }
 
 // ============================================================ FULL4 turns
@@ -873,7 +876,7 @@ NARDE_FN void env_ply(Side& s, int4& st, const uint32_t r[4], bool have_dice, in
                       StepOut& o, int& term, int& trunc) {
   if (!have_dice) dice_from(r[0], dice_mode, d0, d1);
   const uint32_t mover_black = s.black;
-  env_step(s, d0, d1, c1, c2, policy, r[1], r[2], o);
+  env_step(s, d0, d1, c1, c2, policy, r[1], r[2], o, autoreset);
   s.elapsed += 1u;
   term = o.term;
   trunc = max_steps > 0 && s.elapsed >= (uint32_t)max_steps;
