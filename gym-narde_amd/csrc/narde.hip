@@ -722,11 +722,17 @@ __device__ __forceinline__ void pc_emit(const PcLds& L, int slot, int np, int p0
         const int el = j / 6, qq = j - 6 * el;
         if (g0 + el >= n) continue;
         const int wi = qq >> 1, sh = (qq & 1) * 16;
-        const uint4 a = L.res[slot][k][0][e0 + el];
-        const uint4 b = L.res[slot][k][1][e0 + el];
-        const uint32_t own = wi == 0 ? a.x : (wi == 1 ? a.y : a.z);
-        const uint32_t opp = wi == 0 ? a.w : (wi == 1 ? b.x : b.y);
+        // read only the two words this quad needs: own word wi is dword wi
+        // of group 0, opponent word wi is dword 3 of group 0 or wi - 1 of
+        // group 1 (2 x ds_read_b32 instead of 2 x ds_read_b128)
+        const uint32_t* g0w = reinterpret_cast<const uint32_t*>(&L.res[slot][k][0][e0 + el]);
+        const uint32_t* g1w = reinterpret_cast<const uint32_t*>(&L.res[slot][k][1][e0 + el]);
+        const uint32_t own = g0w[wi];
+        const uint32_t opp = wi == 0 ? g0w[3] : g1w[wi - 1];
         int4 v;
+#if NARDE_DIAG_ABLATE & 8
+        st_out(dst + j, make_int4(own, opp, 0, 0)); continue;
+#endif
         v.x = (int)((own >> sh) & 15u) - (int)((opp >> sh) & 15u);
         v.y = (int)((own >> (sh + 4)) & 15u) - (int)((opp >> (sh + 4)) & 15u);
         v.z = (int)((own >> (sh + 8)) & 15u) - (int)((opp >> (sh + 8)) & 15u);
@@ -778,7 +784,11 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
     const int np = min(kPcR, plies - p0);
     for (int k = 0; k < np; ++k) {
       uint32_t r[4];
+#if NARDE_DIAG_ABLATE & 16
+      r[0] = (t0 + p0 + k) * 0x9E3779B9u ^ (uint32_t)i; r[1] = r[0] * 0x85EBCA6Bu; r[2] = r[1] ^ 0xC2B2AE35u; r[3] = r[0] + 7u;
+#else
       draw(g, t0 + (uint32_t)(p0 + k), (uint32_t)i, 0u, r);
+#endif
       L.draw[b & 1][k][le] = make_uint4(r[0], r[1], r[2], r[3]);
     }
   };
