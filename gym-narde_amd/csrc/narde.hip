@@ -681,8 +681,12 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Planes pl, int n, Rng g, int
 // Plies go in blocks of kPcR with one workgroup barrier per block; LDS holds
 // two slots of each ring (draws and results), 32 + 96 KiB.
 // Equivalent, bit for bit, to `plies` narde_step(NULL, NULL, autoreset=1).
+#ifndef NARDE_PC_SETS
+#define NARDE_PC_SETS 1
+#endif
 constexpr int kPcEnvs = 256;                  // envs per workgroup
-constexpr int kPcThreads = 2 * kPcEnvs;       // producers + consumers
+constexpr int kPcSets = NARDE_PC_SETS;        // consumer waves per producer wave
+constexpr int kPcThreads = (1 + kPcSets) * kPcEnvs;  // producers + consumers
 constexpr int kPcR = 4;                       // plies per barrier block
 
 struct PcLds {
@@ -706,11 +710,11 @@ __device__ __forceinline__ void pc_put(PcLds& L, int slot, int k, int le, const 
 
 // consumer: outputs of plies p0 .. p0+np-1 for the 64 envs of consumer wave cw
 __device__ __forceinline__ void pc_emit(const PcLds& L, int slot, int np, int p0, int n, int wg_env0,
-                                        int cw, int lane, const Outs& out) {
+                                        int cw, int lane, const Outs& out, int k0, int kstep) {
   const int e0 = cw * 64;          // first env of this wave, workgroup-local
   const int g0 = wg_env0 + e0;     // ... global (handle) index
   const bool mine = g0 + lane < n;
-  for (int k = 0; k < np; ++k) {
+  for (int k = k0; k < np; k += kstep) {
     const size_t row0 = (size_t)(p0 + k) * n + g0;
     if (out.obs) {
       // the wave's 64 obs rows are 384 contiguous int4 quads: lane takes
@@ -765,6 +769,9 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
   if (producer) __builtin_amdgcn_s_setprio(1);
 #endif
   const int le = (wave & 3) * 64 + lane;            // workgroup-local env
+  // consumer set: with kPcSets > 1 the consumer waves of one env group split
+  // the plies of each block (set c takes plies k = c, c + kPcSets, ...)
+  const int cset = producer ? 0 : (wave - 4) >> 2;
   const int wg_env0 = blockIdx.x * kPcEnvs;
   const int i = wg_env0 + le;
   const bool valid = i < n;
@@ -782,7 +789,7 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
   auto draw_block = [&](int b) {
     const int p0 = b * kPcR;
     const int np = min(kPcR, plies - p0);
-    for (int k = 0; k < np; ++k) {
+    for (int k = cset; k < np; k += kPcSets) {
       uint32_t r[4];
 #if NARDE_DIAG_ABLATE & 16
       r[0] = (t0 + p0 + k) * 0x9E3779B9u ^ (uint32_t)i; r[1] = r[0] * 0x85EBCA6Bu; r[2] = r[1] ^ 0xC2B2AE35u; r[3] = r[0] + 7u;
@@ -810,13 +817,14 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
       }
     } else {
       if (b + 1 < nb) draw_block(b + 1);
-      if (kOut && b > 0) pc_emit(L, (b - 1) & 1, kPcR, p0 - kPcR, n, wg_env0, wave & 3, lane, out);
+      if (kOut && b > 0)
+        pc_emit(L, (b - 1) & 1, kPcR, p0 - kPcR, n, wg_env0, wave & 3, lane, out, cset, kPcSets);
     }
     __syncthreads();
   }
   if (kOut && !producer && nb > 0) {
     const int p0 = (nb - 1) * kPcR;
-    pc_emit(L, (nb - 1) & 1, plies - p0, p0, n, wg_env0, wave & 3, lane, out);
+    pc_emit(L, (nb - 1) & 1, plies - p0, p0, n, wg_env0, wave & 3, lane, out, cset, kPcSets);
   }
   if (producer && valid) {
     uint4 ra, rb;
