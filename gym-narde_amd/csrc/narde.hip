@@ -190,8 +190,8 @@ __global__ void __launch_bounds__(kBlock) k_legal(Planes pl, int n, Rng g,
 // masks instead of rule branches around the calls.
 struct CoopLds {
   uint4 snap[64][2];          // owner state: {own w0..w2, O}, {S1, P, low, params}
-  uint32_t task[64 * 16];     // (owner lane << 8) | source; <= 15 sources per lane
-  uint32_t res[64];
+  uint32_t task[64 * 32];     // (lane << 8) | (which << 7) | source; 2 masks x <= 15 sources
+  uint32_t res[64][3];
 };
 
 __device__ __forceinline__ int wave_prefix(int x, int lane, int& total) {
@@ -205,28 +205,35 @@ __device__ __forceinline__ int wave_prefix(int x, int lane, int& total) {
   return v - x;
 }
 
-// mode 0 (keep): bit p of L stays iff `need` more sub-moves of die a remain
-//   playable after p -- block-free lower bound first, exact search after;
-// mode 1 (pair): bit p stays iff die b still has a move after p with die a.
-__device__ uint32_t coop_check(CoopLds& W, const Side& s, uint32_t low, int a, int b, int hl,
-                               uint32_t L, int need, bool bf, int mode, int lane) {
-  if (__ballot(L != 0u) == 0ull) return 0u;  // wave-uniform: nothing to check
-  const int cnt = __builtin_popcount(L);
+// One cooperative pass over every lane's per-source checks.  Per lane:
+//   mode 1 (pair, two dice a = d_hi, b = d_lo): m0 = first moves with a,
+//     kept (res 0) iff b still has a move after them; m1 = first moves with
+//     b, kept (res 1) iff a still does.
+//   mode 0 (depth, doubles a): m0 = sources; res j gets the sources after
+//     which at least j + 1 more sub-moves are playable (searched up to
+//     `need`; block-free lanes try the chain bound first).
+__device__ void coop_run(CoopLds& W, const Side& s, uint32_t low, int a, int b, int hl, uint32_t m0,
+                         uint32_t m1, int need, bool bf, int mode, int lane, uint32_t out[3]) {
+  out[0] = out[1] = out[2] = 0u;
+  if (__ballot((m0 | m1) != 0u) == 0ull) return;  // wave-uniform: nothing to check
+  const int c0 = __builtin_popcount(m0), cnt = c0 + __builtin_popcount(m1);
   int total;
   const int off = wave_prefix(cnt, lane, total);
-  W.res[lane] = 0u;
+  W.res[lane][0] = W.res[lane][1] = W.res[lane][2] = 0u;
   if (cnt) {
     W.snap[lane][0] = make_uint4(s.own.w[0], s.own.w[1], s.own.w[2], s.O);
     W.snap[lane][1] = make_uint4(s.S1o, s.P, low,
                                  (uint32_t)a | ((uint32_t)b << 4) | ((uint32_t)(hl + 1) << 8) |
                                      ((uint32_t)need << 12) | ((uint32_t)bf << 16) |
                                      ((uint32_t)mode << 17) | (s.off_own << 20));
-    uint32_t m = L;
     int k = off;
-    while (m) {
-      const int p = __builtin_ctz(m);
-      m &= m - 1u;
-      W.task[k++] = ((uint32_t)lane << 8) | (uint32_t)p;
+    for (int which = 0; which < 2; ++which) {
+      uint32_t m = which ? m1 : m0;
+      while (m) {
+        const int p = __builtin_ctz(m);
+        m &= m - 1u;
+        W.task[k++] = ((uint32_t)lane << 8) | ((uint32_t)which << 7) | (uint32_t)p;
+      }
     }
   }
   __builtin_amdgcn_wave_barrier();  // a wave's LDS operations retire in issue order
@@ -234,7 +241,7 @@ __device__ uint32_t coop_check(CoopLds& W, const Side& s, uint32_t low, int a, i
     const int t = base + lane;
     if (t < total) {
       const uint32_t tk = W.task[t];
-      const int ow = (int)(tk >> 8), p = (int)(tk & 0xFFu);
+      const int ow = (int)(tk >> 8), which = (int)((tk >> 7) & 1u), p = (int)(tk & 0x7Fu);
       const uint4 x = W.snap[ow][0], y = W.snap[ow][1];
       Side c;
       c.own.w[0] = x.x; c.own.w[1] = x.y; c.own.w[2] = x.z;
@@ -243,36 +250,39 @@ __device__ uint32_t coop_check(CoopLds& W, const Side& s, uint32_t low, int a, i
       c.S1p = 0u; c.off_opp = 0u; c.ft_own = 0u; c.ft_opp = 0u; c.black = 0u; c.elapsed = 0u; c.t = 0u;
       const uint32_t lw = y.z, prm = y.w;
       c.off_own = prm >> 20;
-      const int ta = (int)(prm & 15u), tb = (int)((prm >> 4) & 15u);
+      const int pa = (int)(prm & 15u), pb = (int)((prm >> 4) & 15u);
       const int thl = (int)((prm >> 8) & 15u) - 1, tneed = (int)((prm >> 12) & 15u);
       const bool tbf = (prm >> 16) & 1u;
-      bool ok;
       if ((prm >> 17) & 1u) {
+        const int ta = which ? pb : pa, tb = which ? pa : pb;
         uint32_t O2, S2;
         child_masks(c, p, ta, O2, S2);
         uint32_t L2 = die_candidates(O2, c.P, tb);
         if (!tbf) L2 = die_filter(O2, S2, block_info_low(O2, lw), L2, tb);
         if (p == 23) L2 &= ~HEAD;
-        ok = L2 != 0u;
+        if (L2) atomicOr(&W.res[ow][which], 1u << p);
       } else {
         const int hl2 = thl - (p == 23 ? 1 : 0);
-        ok = false;
+        int dep = 0;
         if (tbf) {
           uint32_t O2, S2;
-          child_masks(c, p, ta, O2, S2);
-          ok = f4_chain_bound(O2, S2, c.P, ta, hl2) >= tneed;
+          child_masks(c, p, pa, O2, S2);
+          const int lb = f4_chain_bound(O2, S2, c.P, pa, hl2);
+          dep = lb >= tneed ? tneed : 0;
         }
-        if (!ok) {
-          apply_die(c, p, ta);
-          ok = tneed == 1 ? f4_reach<1>(c, lw, ta, hl2, tbf)
-                          : (tneed == 2 ? f4_reach<2>(c, lw, ta, hl2, tbf) : f4_reach<3>(c, lw, ta, hl2, tbf));
+        if (dep < tneed) {
+          apply_die(c, p, pa);
+          dep = tneed == 1 ? f4_depth<1>(c, lw, pa, hl2, tbf)
+                           : (tneed == 2 ? f4_depth<2>(c, lw, pa, hl2, tbf) : f4_depth<3>(c, lw, pa, hl2, tbf));
         }
+        for (int j = 0; j < dep; ++j) atomicOr(&W.res[ow][j], 1u << p);
       }
-      if (ok) atomicOr(&W.res[ow], 1u << p);
     }
   }
   __builtin_amdgcn_wave_barrier();
-  return W.res[lane];
+  out[0] = W.res[lane][0];
+  out[1] = W.res[lane][1];
+  out[2] = W.res[lane][2];
 }
 
 // env_turn_full with the per-source checks done cooperatively (see above)
@@ -293,30 +303,28 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   const bool all_l = !dbl && bf && f4_lower_bound(s.O, s.S1o, s.P, dh, 1) >= 2;
   const int hl0 = (dbl && s.ft_own && (dh == 3 || dh == 4 || dh == 6)) ? 2 : 1;
   const bool fast = dbl && bf && f4_lower_bound(s.O, s.S1o, s.P, dh, hl0) >= 4;
-  // not fast: the chain bound may still prove M = 4 (no search for M) and,
-  // when >= 7, every first sub-move (a sub-move lowers it by <= 4)
+  // not fast: a chain bound >= 7 still keeps every first sub-move (one
+  // sub-move lowers it by <= 4) with M = 4
   const int cb0 = (dbl && bf && !fast) ? f4_chain_bound(s.O, s.S1o, s.P, dh, hl0) : 0;
-  const bool m4 = fast || cb0 >= 4;
   const bool srch = dbl && !fast && Lh != 0u && cb0 < 7;
-#if NARDE_DIAG_ABLATE & 1
-  const uint32_t ph = Lh, pl = Ll;  // DIAGNOSTIC timing only: wrong results
+  // one cooperative pass for every lane's first-sub-move checks
+  uint32_t r0[3];
+  {
+    const bool pair = !dbl;
+    const uint32_t m0 = pair ? (all_h ? 0u : Lh) : (srch ? Lh : 0u);
+    const uint32_t m1 = pair ? (all_l ? 0u : Ll) : 0u;
+#if NARDE_DIAG_ABLATE & 3
+    r0[0] = Lh; r0[1] = Ll; r0[2] = Lh;  // DIAGNOSTIC timing only: wrong results
+    (void)m0; (void)m1; (void)pair;
 #else
-  const uint32_t ph = coop_check(W, s, low, dh, dl, 1, (!dbl && !all_h) ? Lh : 0u, 0, bf, 1, lane);
-  const uint32_t pl = coop_check(W, s, low, dl, dh, 1, (!dbl && !all_l) ? Ll : 0u, 0, bf, 1, lane);
+    coop_run(W, s, low, dh, dl, pair ? 1 : hl0, m0, m1, 3, bf, pair ? 1 : 0, lane, r0);
 #endif
-#if NARDE_DIAG_ABLATE & 2
-  const uint32_t c3 = Lh, c2 = Lh, c1 = Lh;  // DIAGNOSTIC timing only: wrong results
-#else
-  const uint32_t c3 = coop_check(W, s, low, dh, 0, hl0, srch ? Lh : 0u, 3, bf, 0, lane);
-  const uint32_t c2 = coop_check(W, s, low, dh, 0, hl0, (srch && !m4 && !c3) ? Lh : 0u, 2, bf, 0, lane);
-  const uint32_t c1 =
-      coop_check(W, s, low, dh, 0, hl0, (srch && !m4 && !c3 && !c2) ? Lh : 0u, 1, bf, 0, lane);
-#endif
+  }
   uint32_t Ch, Cl;
   int M;
   if (!dbl) {
-    Ch = all_h ? Lh : ph;
-    Cl = all_l ? Ll : pl;
+    Ch = all_h ? Lh : r0[0];
+    Cl = all_l ? Ll : r0[1];
     if (Ch | Cl) {
       M = 2;
     } else {
@@ -328,9 +336,9 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
     Cl = 0u;
     if (fast || (cb0 >= 7 && Lh)) { Ch = Lh; M = 4; }
     else if (!Lh) { Ch = 0u; M = 0; }
-    else if (c3) { Ch = c3; M = 4; }
-    else if (c2) { Ch = c2; M = 3; }
-    else if (c1) { Ch = c1; M = 2; }
+    else if (r0[2]) { Ch = r0[2]; M = 4; }  // some source leaves 3 more
+    else if (r0[1]) { Ch = r0[1]; M = 3; }
+    else if (r0[0]) { Ch = r0[0]; M = 2; }
     else { Ch = Lh; M = 1; }
   }
   o.legal = (uint64_t)Ch | ((uint64_t)Cl << 24) | ((uint64_t)dh << 48) | ((uint64_t)dl << 52) |
@@ -368,12 +376,13 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
     const int need = M - k - 1;
     const bool direct = !dbl || fast || need <= 0 ||
                         (act && bf && f4_chain_bound(s.O, s.S1o, s.P, dk, hl) >= need + 4);
+    uint32_t rk[3];
 #if NARDE_DIAG_ABLATE & 2
-    const uint32_t ck = Lk;
+    rk[0] = rk[1] = rk[2] = Lk;
 #else
-    const uint32_t ck = coop_check(W, s, low, dk, 0, hl, (act && !direct) ? Lk : 0u, need, bf, 0, lane);
+    coop_run(W, s, low, dk, 0, hl, (act && !direct) ? Lk : 0u, 0u, need > 0 ? need : 1, bf, 0, lane, rk);
 #endif
-    const uint32_t C = direct ? Lk : ck;
+    const uint32_t C = direct ? Lk : (need >= 2 ? rk[1] : rk[0]);
     if (act) {
       int p;
       bool ok = true;

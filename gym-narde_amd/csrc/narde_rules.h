@@ -590,6 +590,29 @@ NARDE_FN bool f4_reach(const Side& s, uint32_t low, int d, int hl, bool bf) {
   }
 }
 
+// the most sub-moves of die d (up to N) playable from s: depth-first with
+// early exit at N (hl head moves still allowed)
+template <int N>
+NARDE_FN int f4_depth(const Side& s, uint32_t low, int d, int hl, bool bf) {
+  uint32_t L = legal1(s, low, d, bf);
+  if (hl <= 0) L &= ~HEAD;
+  if (!L) return 0;
+  if constexpr (N == 1) {
+    return 1;
+  } else {
+    int best = 1;
+    while (L && best < N) {
+      const int p = __builtin_ctz(L);
+      L &= L - 1u;
+      Side c = s;
+      apply_die(c, p, d);
+      const int v = 1 + f4_depth<N - 1>(c, low, d, hl - (p == 23 ? 1 : 0), bf);
+      best = v > best ? v : best;
+    }
+    return best;
+  }
+}
+
 // Block-free lower bound on the sub-moves of die d playable from a node with
 // own masks (O, S1): every checker of a listed source can make the same move
 // (its landing stays free of the opponent, bear-off stays allowed), sources
