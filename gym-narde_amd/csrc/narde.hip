@@ -194,15 +194,20 @@ struct CoopLds {
   uint32_t res[64][3];
 };
 
+// exclusive prefix sum of x (0 <= x < 64) over the wave, and the total, from
+// one ballot per bit of x: lane l's prefix adds 2^b for every lower lane with
+// bit b set (v_mbcnt counts them) -- no LDS round trips, unlike shuffles
 __device__ __forceinline__ int wave_prefix(int x, int lane, int& total) {
-  int v = x;
+  (void)lane;
+  int excl = 0;
+  total = 0;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(v, o, 64);
-    if (lane >= o) v += y;
+  for (int b = 0; b < 6; ++b) {
+    const uint64_t m = __ballot((x >> b) & 1);
+    excl += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
+    total += __builtin_popcountll(m) << b;
   }
-  total = __shfl(v, 63, 64);
-  return v - x;
+  return excl;
 }
 
 // One cooperative pass over every lane's per-source checks.  Per lane:
