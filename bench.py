@@ -290,12 +290,25 @@ def main():
         drv.update()
         ev[2].record()
         torch.cuda.synchronize()
+        # the same step captured once as a CUDA graph and replayed
+        drv.capture_graph(warmup=2)
+        for _ in range(3):
+            drv.step()
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        for _ in range(args.dqn_steps):
+            drv.step()
+        torch.cuda.synchronize()
+        g_el = time.perf_counter() - g0
         dqn = {
             "config": "configs[3]: batch=65536, legal-action masks + 198-d obs -> DecomposedDQN "
                       "(train_deepq_pytorch.py:184-277) on PyTorch-ROCm, fp32",
-            "value": round(world * per * args.dqn_steps / q_el, 1),
+            "value": round(world * per * args.dqn_steps / g_el, 1),
             "unit": "env steps/s",
-            "ms_per_step": round(q_el / args.dqn_steps * 1e3, 4),
+            "ms_per_step": round(g_el / args.dqn_steps * 1e3, 4),
+            "mode": "hipGraph replay of the whole step (BatchedDQNDriver.capture_graph)",
+            "eager_value": round(world * per * args.dqn_steps / q_el, 1),
+            "eager_ms_per_step": round(q_el / args.dqn_steps * 1e3, 4),
             "act_plus_env_ms": round(ev[0].elapsed_time(ev[1]), 4),
             "update_ms": round(ev[1].elapsed_time(ev[2]), 4),
             "train_batch": args.dqn_train_batch,

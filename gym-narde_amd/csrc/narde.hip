@@ -986,13 +986,22 @@ __global__ void __launch_bounds__(kBlock) k_mask576_move2(Planes pl, int n, Rng 
 // reference's "no move" code, :504-505).  Draws: Philox4x32-10({tag, row, 0,
 // 5}, seed): r0 < epsilon * 2^32 explores, one shared decision for both
 // heads of a step (same tag); the pick is mulhi(r1 or r2 by head, count).
+__host__ __device__ inline uint64_t eps_to_q32(float epsilon) {
+  const double e = epsilon <= 0.0f ? 0.0 : (epsilon >= 1.0f ? 1.0 : (double)epsilon);
+  return (uint64_t)(e * 4294967296.0);
+}
+
 __global__ void __launch_bounds__(256) k_policy576(const float* __restrict__ q, int64_t ldq,
                                                    const uint64_t* __restrict__ mask, int n,
                                                    uint64_t eps_q32, uint32_t k0, uint32_t k1,
-                                                   uint32_t tag, int head, int64_t* __restrict__ out) {
+                                                   uint32_t tag, int head, int64_t* __restrict__ out,
+                                                   const float* __restrict__ eps_p,
+                                                   const int64_t* __restrict__ tag_p) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
   if (row >= n) return;  // whole waves: the row is uniform over the wave
+  if (eps_p) eps_q32 = eps_to_q32(*eps_p);  // device-resident epsilon / tag (graph replays)
+  if (tag_p) tag = (uint32_t)*tag_p;
   uint64_t mw[9];
   int cnt = 0;
 #pragma unroll
@@ -1402,11 +1411,23 @@ int narde_policy_masked_argmax576(int device, const float* q, int64_t ldq, const
   if (!q || !mask || !out || n < 0 || n > (int64_t(1) << 31) - 4 || ldq < 576)
     return fail(NARDE_EINVAL, "bad argument");
   if (n == 0) return NARDE_OK;
-  const double e = epsilon <= 0.0f ? 0.0 : (epsilon >= 1.0f ? 1.0 : (double)epsilon);
-  const uint64_t eps_q32 = (uint64_t)(e * 4294967296.0);
   DeviceGuard dg(device);
-  k_policy576<<<(int)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(q, ldq, mask, (int)n, eps_q32, (uint32_t)seed,
-                                                                   (uint32_t)(seed >> 32), tag, head, out);
+  k_policy576<<<(int)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(q, ldq, mask, (int)n, eps_to_q32(epsilon),
+                                                                   (uint32_t)seed, (uint32_t)(seed >> 32), tag,
+                                                                   head, out, nullptr, nullptr);
+  return check_launch("k_policy576");
+}
+
+int narde_policy_masked_argmax576_dev(int device, const float* q, int64_t ldq, const uint64_t* mask, int64_t n,
+                                      const float* epsilon, uint64_t seed, const int64_t* tag, int head,
+                                      int64_t* out, void* stream) {
+  if (!q || !mask || !out || !epsilon || !tag || n < 0 || n > (int64_t(1) << 31) - 4 || ldq < 576)
+    return fail(NARDE_EINVAL, "bad argument");
+  if (n == 0) return NARDE_OK;
+  DeviceGuard dg(device);
+  k_policy576<<<(int)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(q, ldq, mask, (int)n, 0ull, (uint32_t)seed,
+                                                                   (uint32_t)(seed >> 32), 0u, head, out, epsilon,
+                                                                   tag);
   return check_launch("k_policy576");
 }
 

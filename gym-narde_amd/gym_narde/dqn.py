@@ -90,16 +90,25 @@ def policy_576(q, mask576, epsilon, seed, tag, head, out=None):
     """Masked epsilon-greedy codes (B,) int64 from Q-values (B,576) f32 and
     the env's (B,9) bit masks: one HIP kernel (k_policy576), no (B,576)
     intermediates.  Same tag for both heads of a step = one shared explore
-    decision per env."""
+    decision per env.  epsilon / tag may be Python numbers or device scalars
+    (f32 / int64 0-d tensors, read by the kernel at run time: graph-safe)."""
     q = q.contiguous()
     if q.dtype != torch.float32 or q.shape[1] != MOVES:
         raise ValueError("q must be (B, 576) float32")
     if out is None:
         out = torch.empty(q.shape[0], dtype=torch.int64, device=q.device)
     stream = ctypes.c_void_p(torch.cuda.current_stream(q.device).cuda_stream)
-    _lib.check(_lib.load().narde_policy_masked_argmax576(
-        q.device.index, _lib.ptr(q), q.stride(0), _lib.ptr(mask576.contiguous()), q.shape[0],
-        float(epsilon), int(seed) & (2 ** 64 - 1), int(tag) & 0xFFFFFFFF, int(head), _lib.ptr(out),
+    lib = _lib.load()
+    args = (q.device.index, _lib.ptr(q), q.stride(0), _lib.ptr(mask576.contiguous()), q.shape[0])
+    if torch.is_tensor(epsilon) or torch.is_tensor(tag):
+        eps = torch.as_tensor(epsilon, dtype=torch.float32, device=q.device)
+        tg = torch.as_tensor(tag, dtype=torch.int64, device=q.device)
+        _lib.check(lib.narde_policy_masked_argmax576_dev(
+            *args, _lib.ptr(eps), int(seed) & (2 ** 64 - 1), _lib.ptr(tg), int(head), _lib.ptr(out),
+            stream), "narde_policy_masked_argmax576_dev")
+        return out
+    _lib.check(lib.narde_policy_masked_argmax576(
+        *args, float(epsilon), int(seed) & (2 ** 64 - 1), int(tag) & 0xFFFFFFFF, int(head), _lib.ptr(out),
         stream), "narde_policy_masked_argmax576")
     return out
 
@@ -108,12 +117,17 @@ class DeviceReplay:
     """PrioritizedReplayBuffer (train_deepq_pytorch.py:279-342) on device
     tensors: new transitions get the running max priority, sampling is
     proportional to priority**alpha, importance weights (N p)^-beta / max,
-    beta anneals by beta_increment per sample, priorities = |td| + epsilon."""
+    beta anneals by beta_increment per sample, priorities = |td| + epsilon.
+
+    The write cursor, beta and the max priority live in device scalars and
+    are updated in place, so add/sample/update can be captured in a graph
+    (`pos` / `size` are host mirrors; sample() needs `size` fixed, i.e. a
+    full ring, to be replayed)."""
 
     def __init__(self, capacity, state_size, device, alpha=0.6, beta=0.4, beta_increment=0.001,
                  epsilon=0.01):
         self.capacity, self.device = int(capacity), device
-        self.alpha, self.beta, self.beta_increment, self.epsilon = alpha, beta, beta_increment, epsilon
+        self.alpha, self.beta_increment, self.epsilon = alpha, beta_increment, epsilon
         z = dict(device=device)
         self.obs = torch.zeros((self.capacity, state_size), dtype=torch.float32, **z)
         self.next_obs = torch.zeros((self.capacity, state_size), dtype=torch.float32, **z)
@@ -122,20 +136,31 @@ class DeviceReplay:
         self.done = torch.zeros(self.capacity, dtype=torch.float32, **z)
         self.prio = torch.ones(self.capacity, dtype=torch.float32, **z)
         self.max_prio = torch.ones((), dtype=torch.float32, **z)
+        self.beta_t = torch.full((), beta, dtype=torch.float64, **z)
+        self.pos_t = torch.zeros((), dtype=torch.int64, **z)
         self.pos = 0
         self.size = 0
+
+    @property
+    def beta(self):
+        return float(self.beta_t)
 
     def add(self, obs, action, reward, next_obs, done):
         n = obs.shape[0]
         if n > self.capacity:
             raise ValueError("batch larger than the replay capacity")
-        idx = (torch.arange(n, device=self.device) + self.pos) % self.capacity
+        idx = (torch.arange(n, device=self.device) + self.pos_t) % self.capacity
         self.obs.index_copy_(0, idx, obs)
         self.next_obs.index_copy_(0, idx, next_obs)
         self.action.index_copy_(0, idx, action)
         self.reward.index_copy_(0, idx, reward)
         self.done.index_copy_(0, idx, done)
         self.prio.index_copy_(0, idx, self.max_prio.expand(n))
+        self.pos_t.add_(n).remainder_(self.capacity)
+        self.advance(n)
+
+    def advance(self, n):
+        """Host mirrors of one add() of n rows (also called per graph replay)."""
         self.pos = (self.pos + n) % self.capacity
         self.size = min(self.size + n, self.capacity)
 
@@ -148,20 +173,29 @@ class DeviceReplay:
         u = torch.rand(batch, device=p.device, generator=generator) * total
         idx = torch.searchsorted(cdf, u, right=True).clamp_(max=self.size - 1)
         probs_idx = p[idx] / total
-        w = (self.size * probs_idx) ** (-self.beta)
+        w = (self.size * probs_idx) ** (-self.beta_t)
         w = w / w.max()
-        self.beta = min(1.0, self.beta + self.beta_increment)
+        self.beta_t.add_(self.beta_increment).clamp_(max=1.0)
         return idx, w
 
     def update(self, idx, td):
         pr = td + self.epsilon
         self.prio.index_copy_(0, idx, pr)
-        self.max_prio = torch.maximum(self.max_prio, pr.max())
+        torch.maximum(self.max_prio, pr.max(), out=self.max_prio)
 
 
 class BatchedDQNDriver:
     """B envs of DQN self-play on one GPU; one call of step() = one env step
-    for every env + `updates_per_step` prioritized DQN updates."""
+    for every env + `updates_per_step` prioritized DQN updates.
+
+    All driver state (epsilon, the step tag, the replay cursor, beta, the
+    max priority, the current observation) lives in device tensors updated
+    in place, so a whole step -- masks, both policy heads, env step,
+    shaping, replay write, minibatch sample, loss, backward, clip, Adam --
+    can be captured once in a torch.cuda.CUDAGraph and replayed
+    (capture_graph()); the replay then costs one launch instead of ~150.
+    The target-network sync stays on the host (every target_update
+    updates, an in-place copy the graph reads)."""
 
     def __init__(self, env, obs="tesauro198", train_batch=4096, capacity=1 << 20,
                  learning_rate=1e-4, gamma=0.99, epsilon=1.0, epsilon_min=0.01,
@@ -178,32 +212,47 @@ class BatchedDQNDriver:
         self.model = DecomposedDQN(self.state_size).to(self.dev)
         self.target = DecomposedDQN(self.state_size).to(self.dev)
         self.target.load_state_dict(self.model.state_dict())
-        self.opt = torch.optim.Adam(self.model.parameters(), lr=learning_rate)
+        # capturable: the step count and bias corrections stay on the device
+        self.opt = torch.optim.Adam(self.model.parameters(), lr=learning_rate, capturable=True)
         self.replay = DeviceReplay(capacity, self.state_size, self.dev)
         self.train_batch, self.gamma = int(train_batch), gamma
-        self.epsilon, self.epsilon_min, self.epsilon_decay = epsilon, epsilon_min, epsilon_decay
+        z = dict(device=self.dev)
+        self.eps_t = torch.full((), epsilon, dtype=torch.float32, **z)
+        self.epsilon_min, self.epsilon_decay = epsilon_min, epsilon_decay
         self.target_update, self.updates_per_step = target_update, updates_per_step
         self.shaping = shaping
         self.seed = seed
+        self.tag_t = torch.zeros((), dtype=torch.int64, **z)
         self.steps = 0
         self.train_steps = 0
         B = env.num_envs
-        self.off_seen = torch.zeros((B, 2), dtype=torch.float32, device=self.dev)
+        self.off_seen = torch.zeros((B, 2), dtype=torch.float32, **z)
         self.state = self._observe()
+        self._next = torch.empty_like(self.state)
+        self.loss_t = torch.zeros((), dtype=torch.float32, **z)
         self.last_loss = None
+        self.graph = None
+        self._capturing = False
+
+    @property
+    def epsilon(self):
+        return float(self.eps_t)
 
     # ---------------------------------------------------------------- env side
-    def _observe(self):
+    def _observe(self, out=None):
         if self.obs_kind == "tesauro198":
-            return self.env.tesauro198().clone()
-        return self.env.observe().to(torch.float32)
+            if out is None:
+                return self.env.tesauro198().clone()
+            return self.env.tesauro198(out=out)
+        x = self.env.observe().to(torch.float32)
+        return x if out is None else out.copy_(x)
 
     def _off_counts(self, obs):
         """(B,2) borne-off counts (white, black) and the current player (+1/-1):
         read off the 198-float obs (off/15 at 97 and 195, player one-hot at
         196) when that is the observation, else from the env state."""
         if self.obs_kind == "tesauro198":
-            off = torch.round(obs[:, [97, 195]] * 15.0)
+            off = torch.round(obs[:, 97:196:98] * 15.0)
             return off, torch.where(obs[:, 196] > 0.5, 1.0, -1.0)
         st = self.env.get_state()
         return st["off"].to(torch.float32), st["player"].to(torch.float32)
@@ -211,22 +260,33 @@ class BatchedDQNDriver:
     @torch.no_grad()
     def act(self, x):
         """Masked epsilon-greedy (move1, move2) codes for the next step: the
-        env's exact legal masks and the fused policy kernel."""
-        tag = self.steps
+        env's exact legal masks and the fused policy kernel (epsilon and the
+        step tag read from device memory)."""
         f = self.model.features(x)
-        a1 = policy_576(self.model.move1_head(f), self.env.legal_mask(), self.epsilon, self.seed, tag, 0)
+        a1 = policy_576(self.model.move1_head(f), self.env.legal_mask(), self.eps_t, self.seed,
+                        self.tag_t, 0)
         m2 = self.env.legal_mask_move2(a1.to(torch.int16))
-        a2 = policy_576(self.model.move2_from_features(f, a1), m2, self.epsilon, self.seed, tag, 1)
+        a2 = policy_576(self.model.move2_from_features(f, a1), m2, self.eps_t, self.seed, self.tag_t, 1)
         return torch.stack([a1, a2], 1)
 
     def step(self):
+        """One env step for every env + the updates; returns the last loss
+        (a device scalar) or None while the replay holds < train_batch."""
+        if self.graph is not None:
+            return self._replay_graph()
+        loss = self._step_body()
+        self._host_after_step(loss is not None)
+        return self.last_loss if loss is not None else None
+
+    def _step_body(self):
+        """Everything one step runs on the device, host-sync free (the body
+        capture_graph() records).  Host-side counters: _host_after_step."""
         x = self.state
         actions = self.act(x)
         _, reward, term, trunc, _ = self.env.step(actions.to(torch.int16))
         r = reward.to(torch.float32)
         done = (term | trunc).to(torch.float32)
-        nxt = self._observe()
-        self.steps += 1
+        nxt = self._observe(out=self._next)
         if self.shaping:
             # train_deepq_pytorch.py:885-908: +1 per checker newly borne off
             # and +0.1 x total off, for env.unwrapped.current_player read AFTER
@@ -239,15 +299,66 @@ class BatchedDQNDriver:
             self.off_seen.scatter_(1, col.unsqueeze(1), now.unsqueeze(1))
             self.off_seen.mul_((1.0 - done).unsqueeze(1))  # new episode: trackers restart at 0
         self.replay.add(x, actions, r, nxt, done)
-        self.state = nxt
+        self.state.copy_(nxt)
+        self.tag_t.add_(1)
         loss = None
         for _ in range(self.updates_per_step):
-            loss = self.update()
+            loss = self._update_body()
         return loss
+
+    def _host_after_step(self, trained):
+        self.steps += 1
+        if trained:
+            self.last_loss = self.loss_t.clone()
+
+    def capture_graph(self, warmup=3):
+        """Record one step into a CUDA graph; later step() calls replay it.
+        Needs a full replay ring after the warmup steps (sample() sizes are
+        fixed in the graph) and one update per step (the host-side target
+        sync runs between replays).  The warmup steps are real steps, run
+        eagerly on a side stream as torch's capture rules ask."""
+        if self.updates_per_step != 1:
+            raise ValueError("graph capture needs updates_per_step == 1")
+        cap = self.replay.capacity
+        need = max(0, -(-(cap - self.replay.size - warmup * self.env.num_envs) // self.env.num_envs))
+        side = torch.cuda.Stream(self.dev)
+        side.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(side):
+            for _ in range(need + warmup):
+                self.step()
+        torch.cuda.current_stream(self.dev).wait_stream(side)
+        if self.replay.size != cap or self.replay.size < self.train_batch:
+            raise RuntimeError("replay ring not full before capture")
+        g = torch.cuda.CUDAGraph()
+        g.register_generator_state(self.gen)
+        # the captured body must not advance the host mirrors: replays do
+        pos, size = self.replay.pos, self.replay.size
+        self._capturing = True
+        try:
+            with torch.cuda.graph(g):
+                self._step_body()
+        finally:
+            self._capturing = False
+        self.replay.pos, self.replay.size = pos, size
+        self.graph = g
+        return self._replay_graph()  # capture does not execute: run it once
+
+    def _replay_graph(self):
+        self.graph.replay()
+        self.replay.advance(self.env.num_envs)
+        self._after_update()
+        self._host_after_step(True)
+        return self.last_loss
 
     # ------------------------------------------------------------ learner side
     def update(self):
         """DQNAgent.replay (train_deepq_pytorch.py:602-750), decomposed branch."""
+        if self._update_body() is None:
+            return None
+        self.last_loss = self.loss_t.clone()
+        return self.last_loss
+
+    def _update_body(self):
         if self.replay.size < self.train_batch:
             return None
         idx, w = self.replay.sample(self.train_batch, generator=self.gen)
@@ -269,10 +380,16 @@ class BatchedDQNDriver:
         torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=10.0)
         self.opt.step()
         self.replay.update(idx, td)
+        # epsilon decay per update (:745-746): if eps > eps_min: eps *= decay
+        self.eps_t.copy_(torch.where(self.eps_t > self.epsilon_min, self.eps_t * self.epsilon_decay,
+                                     self.eps_t))
+        self.loss_t.copy_(loss.detach())
+        if self._capturing:
+            return self.loss_t  # the host-side bookkeeping below runs per replay
+        self._after_update()
+        return self.loss_t
+
+    def _after_update(self):
         self.train_steps += 1
         if self.train_steps % self.target_update == 0:
             self.target.load_state_dict(self.model.state_dict())
-        if self.epsilon > self.epsilon_min:
-            self.epsilon *= self.epsilon_decay
-        self.last_loss = loss.detach()
-        return self.last_loss

@@ -201,6 +201,13 @@ int narde_policy_masked_argmax576(int device, const float *q, int64_t ldq, const
                                   int64_t n, float epsilon, uint64_t seed, uint32_t tag, int head,
                                   int64_t *out, void *stream);
 
+/* The same with epsilon (f32) and tag (int64, low 32 bits used) read from
+ * DEVICE memory at run time, so a captured hipGraph replays with the values
+ * current at each replay (the DQN driver's decaying epsilon and step tag). */
+int narde_policy_masked_argmax576_dev(int device, const float *q, int64_t ldq, const uint64_t *mask,
+                                      int64_t n, const float *epsilon, uint64_t seed,
+                                      const int64_t *tag, int head, int64_t *out, void *stream);
+
 /* Stateless: Narde._violates_block_rule on n perspective boards i8[n][24]. */
 int narde_violates_block_rule(int device, const int8_t *boards, int64_t n, uint8_t *out,
                               void *stream);

@@ -111,3 +111,44 @@ def test_policy_kernel_matches_torch_and_explores_legally():
     both = has & (m.sum(1) > 3)
     agree = (e1 == e2)[both].float().mean()
     assert float(agree) > 0.6
+
+
+def test_graph_replay_matches_driver_semantics():
+    """capture_graph(): every replay reads the CURRENT params, observation,
+    epsilon and tag (greedy move 1 == masked argmax of the live network), the
+    host mirrors and device scalars advance one step per replay, and the
+    target sync keeps running between replays."""
+    from gym_narde.dqn import expand_mask, masked_argmax
+
+    n = 4096
+    env, drv = make(n=n)
+    drv.capture_graph(warmup=2)
+    cap = drv.replay.capacity
+    assert drv.replay.size == cap
+    steps0, train0 = drv.steps, drv.train_steps
+    drv.eps_t.fill_(0.0)
+    for k in range(12):
+        with torch.no_grad():
+            m1 = expand_mask(env.legal_mask())
+            want = masked_argmax(drv.model(drv.state), m1)
+        pos = drv.replay.pos
+        tag = int(drv.tag_t)
+        loss = drv.step()
+        assert int(drv.tag_t) == tag + 1
+        assert drv.replay.pos == (pos + n) % cap == int(drv.replay.pos_t)
+        got = drv.replay.action[pos:pos + n, 0]
+        has = m1.any(1)
+        assert torch.equal(got[has], want[has])
+        assert bool((got[~has] == 0).all())
+        assert torch.isfinite(loss)
+    assert drv.steps == steps0 + 12 and drv.train_steps == train0 + 12
+    drv.eps_t.fill_(0.5)
+    drv.step()
+    assert drv.epsilon == pytest.approx(0.5 * 0.995, rel=1e-6)
+    # the target net was synced at a multiple of 10 updates inside the replays
+    drv.step()
+    while drv.train_steps % drv.target_update:
+        drv.step()
+    torch.cuda.synchronize()
+    for p, q in zip(drv.model.parameters(), drv.target.parameters()):
+        assert torch.equal(p, q)

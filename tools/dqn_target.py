@@ -1,0 +1,27 @@
+"""Profiling target for the config-4 DQN driver (rocprofv3 --kernel-trace):
+B envs, graph-captured step, N replays.  argv: [B] [steps] [eager]"""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gym-narde_amd"))
+import torch  # noqa: E402
+
+from gym_narde.dqn import BatchedDQNDriver  # noqa: E402
+from gym_narde.vector import VecNardeEnv  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+eager = len(sys.argv) > 3 and sys.argv[3] == "eager"
+env = VecNardeEnv(B, device="cuda:0", seed=1)
+drv = BatchedDQNDriver(env, train_batch=4096, capacity=max(1 << 20, 4 * B))
+if not eager:
+    drv.capture_graph(warmup=2)
+for _ in range(3):
+    drv.step()
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+for _ in range(N):
+    drv.step()
+torch.cuda.synchronize()
+print(f"{'eager' if eager else 'graph'} B={B}: {(time.perf_counter() - t0) / N * 1e3:.4f} ms/step")
