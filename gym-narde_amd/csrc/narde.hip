@@ -996,7 +996,9 @@ __global__ void __launch_bounds__(256) k_policy576(const float* __restrict__ q, 
                                                    uint64_t eps_q32, uint32_t k0, uint32_t k1,
                                                    uint32_t tag, int head, int64_t* __restrict__ out,
                                                    const float* __restrict__ eps_p,
-                                                   const int64_t* __restrict__ tag_p) {
+                                                   const int64_t* __restrict__ tag_p,
+                                                   const float* __restrict__ add_tab, int64_t ld_add,
+                                                   const int64_t* __restrict__ add_row) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
   if (row >= n) return;  // whole waves: the row is uniform over the wave
@@ -1027,12 +1029,15 @@ __global__ void __launch_bounds__(256) k_policy576(const float* __restrict__ q, 
     }
   } else if (cnt > 0) {
     const float* qr = q + (size_t)row * (size_t)ldq;
+    // optional addend row (the move-2 head's one-hot column, DecomposedDQN):
+    // v = q[row][c] + add_tab[add_row[row]][c], the same single fp32 add
+    const float* ar = add_tab ? add_tab + (size_t)add_row[row] * (size_t)ld_add : nullptr;
     float best = -__builtin_inff();
     int bi = 0x7FFFFFFF;
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
       if ((mw[j] >> lane) & 1ull) {
-        const float v = qr[64 * j + lane];
+        const float v = ar ? qr[64 * j + lane] + ar[64 * j + lane] : qr[64 * j + lane];
         if (v > best) { best = v; bi = 64 * j + lane; }  // j ascending: first max kept
       }
     }
@@ -1414,20 +1419,23 @@ int narde_policy_masked_argmax576(int device, const float* q, int64_t ldq, const
   DeviceGuard dg(device);
   k_policy576<<<(int)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(q, ldq, mask, (int)n, eps_to_q32(epsilon),
                                                                    (uint32_t)seed, (uint32_t)(seed >> 32), tag,
-                                                                   head, out, nullptr, nullptr);
+                                                                   head, out, nullptr, nullptr, nullptr, 0,
+                                                                   nullptr);
   return check_launch("k_policy576");
 }
 
 int narde_policy_masked_argmax576_dev(int device, const float* q, int64_t ldq, const uint64_t* mask, int64_t n,
                                       const float* epsilon, uint64_t seed, const int64_t* tag, int head,
+                                      const float* add_tab, int64_t ld_add, const int64_t* add_row,
                                       int64_t* out, void* stream) {
   if (!q || !mask || !out || !epsilon || !tag || n < 0 || n > (int64_t(1) << 31) - 4 || ldq < 576)
     return fail(NARDE_EINVAL, "bad argument");
+  if (add_tab && (!add_row || ld_add < 576)) return fail(NARDE_EINVAL, "bad addend table");
   if (n == 0) return NARDE_OK;
   DeviceGuard dg(device);
   k_policy576<<<(int)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(q, ldq, mask, (int)n, 0ull, (uint32_t)seed,
                                                                    (uint32_t)(seed >> 32), 0u, head, out, epsilon,
-                                                                   tag);
+                                                                   tag, add_tab, ld_add, add_row);
   return check_launch("k_policy576");
 }
 

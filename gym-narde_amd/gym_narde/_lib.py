@@ -51,7 +51,7 @@ SIGNATURES = {
     "narde_policy_masked_argmax576": (_i32, [_i32, _vp, _i64, _vp, _i64, ctypes.c_float, _u64, _u32,
                                              _i32, _vp, _vp]),
     "narde_policy_masked_argmax576_dev": (_i32, [_i32, _vp, _i64, _vp, _i64, _vp, _u64, _vp, _i32, _vp,
-                                                 _vp]),
+                                                 _i64, _vp, _vp, _vp]),
     "narde_violates_block_rule": (_i32, [_i32, _vp, _i64, _vp, _vp]),
     "narde_host_legal_moves": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "narde_host_step": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -86,12 +86,14 @@ def masked_argmax(scores, mask):
     return torch.where(mask.any(1), best, torch.zeros_like(best))
 
 
-def policy_576(q, mask576, epsilon, seed, tag, head, out=None):
+def policy_576(q, mask576, epsilon, seed, tag, head, out=None, add=None):
     """Masked epsilon-greedy codes (B,) int64 from Q-values (B,576) f32 and
     the env's (B,9) bit masks: one HIP kernel (k_policy576), no (B,576)
     intermediates.  Same tag for both heads of a step = one shared explore
     decision per env.  epsilon / tag may be Python numbers or device scalars
-    (f32 / int64 0-d tensors, read by the kernel at run time: graph-safe)."""
+    (f32 / int64 0-d tensors, read by the kernel at run time: graph-safe).
+    add = (table (R,576) f32, rows (B,) int64): greedy values become
+    q[i] + table[rows[i]] (one fp32 add, fused)."""
     q = q.contiguous()
     if q.dtype != torch.float32 or q.shape[1] != MOVES:
         raise ValueError("q must be (B, 576) float32")
@@ -100,12 +102,21 @@ def policy_576(q, mask576, epsilon, seed, tag, head, out=None):
     stream = ctypes.c_void_p(torch.cuda.current_stream(q.device).cuda_stream)
     lib = _lib.load()
     args = (q.device.index, _lib.ptr(q), q.stride(0), _lib.ptr(mask576.contiguous()), q.shape[0])
-    if torch.is_tensor(epsilon) or torch.is_tensor(tag):
+    if torch.is_tensor(epsilon) or torch.is_tensor(tag) or add is not None:
         eps = torch.as_tensor(epsilon, dtype=torch.float32, device=q.device)
         tg = torch.as_tensor(tag, dtype=torch.int64, device=q.device)
+        tab, rows, ld = None, None, 0
+        if add is not None:
+            tab, rows = add
+            if tab.dtype != torch.float32 or tab.dim() != 2 or tab.shape[1] != MOVES or tab.stride(1) != 1:
+                raise ValueError("add table must be (R, 576) float32 with unit column stride")
+            rows = rows.to(torch.int64).contiguous()
+            if rows.shape != (q.shape[0],):
+                raise ValueError("add rows must be (B,)")
+            ld = tab.stride(0)
         _lib.check(lib.narde_policy_masked_argmax576_dev(
-            *args, _lib.ptr(eps), int(seed) & (2 ** 64 - 1), _lib.ptr(tg), int(head), _lib.ptr(out),
-            stream), "narde_policy_masked_argmax576_dev")
+            *args, _lib.ptr(eps), int(seed) & (2 ** 64 - 1), _lib.ptr(tg), int(head), _lib.ptr(tab), ld,
+            _lib.ptr(rows), _lib.ptr(out), stream), "narde_policy_masked_argmax576_dev")
         return out
     _lib.check(lib.narde_policy_masked_argmax576(
         *args, float(epsilon), int(seed) & (2 ** 64 - 1), int(tag) & 0xFFFFFFFF, int(head), _lib.ptr(out),
@@ -213,7 +224,7 @@ class BatchedDQNDriver:
         self.target = DecomposedDQN(self.state_size).to(self.dev)
         self.target.load_state_dict(self.model.state_dict())
         # capturable: the step count and bias corrections stay on the device
-        self.opt = torch.optim.Adam(self.model.parameters(), lr=learning_rate, capturable=True)
+        self.opt = torch.optim.Adam(self.model.parameters(), lr=learning_rate, capturable=True, fused=True)
         self.replay = DeviceReplay(capacity, self.state_size, self.dev)
         self.train_batch, self.gamma = int(train_batch), gamma
         z = dict(device=self.dev)
@@ -266,7 +277,12 @@ class BatchedDQNDriver:
         a1 = policy_576(self.model.move1_head(f), self.env.legal_mask(), self.eps_t, self.seed,
                         self.tag_t, 0)
         m2 = self.env.legal_mask_move2(a1.to(torch.int16))
-        a2 = policy_576(self.model.move2_from_features(f, a1), m2, self.eps_t, self.seed, self.tag_t, 1)
+        # move-2 Q = (f @ Wf^T + b) + Wm[:, move1]: the column add is fused
+        # into the policy kernel (rows of Wm^T, a 1.3 MB transpose per step)
+        w = self.model.move2_head.weight
+        base = torch.nn.functional.linear(f, w[:, :256], self.model.move2_head.bias)
+        wm_rows = w[:, 256:].t().contiguous()
+        a2 = policy_576(base, m2, self.eps_t, self.seed, self.tag_t, 1, add=(wm_rows, a1))
         return torch.stack([a1, a2], 1)
 
     def step(self):

@@ -203,10 +203,16 @@ int narde_policy_masked_argmax576(int device, const float *q, int64_t ldq, const
 
 /* The same with epsilon (f32) and tag (int64, low 32 bits used) read from
  * DEVICE memory at run time, so a captured hipGraph replays with the values
- * current at each replay (the DQN driver's decaying epsilon and step tag). */
+ * current at each replay (the DQN driver's decaying epsilon and step tag).
+ * Optional addend: with add_tab != NULL the greedy value of code c is
+ * q[i][c] + add_tab[add_row[i] * ld_add + c] -- the move-2 head's one-hot
+ * column (W[:, 256 + move1], pre-transposed into rows) fused into the
+ * argmax instead of materialising a second (n, 576) matrix. */
 int narde_policy_masked_argmax576_dev(int device, const float *q, int64_t ldq, const uint64_t *mask,
                                       int64_t n, const float *epsilon, uint64_t seed,
-                                      const int64_t *tag, int head, int64_t *out, void *stream);
+                                      const int64_t *tag, int head, const float *add_tab,
+                                      int64_t ld_add, const int64_t *add_row, int64_t *out,
+                                      void *stream);
 
 /* Stateless: Narde._violates_block_rule on n perspective boards i8[n][24]. */
 int narde_violates_block_rule(int device, const int8_t *boards, int64_t n, uint8_t *out,

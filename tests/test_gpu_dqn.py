@@ -152,3 +152,26 @@ def test_graph_replay_matches_driver_semantics():
     torch.cuda.synchronize()
     for p, q in zip(drv.model.parameters(), drv.target.parameters()):
         assert torch.equal(p, q)
+
+
+def test_policy_kernel_device_scalars_and_fused_addend():
+    """The _dev entry point: epsilon / tag from device memory give the same
+    codes as the scalar entry point, and the fused addend row equals the
+    argmax of q + table[rows] (the move-2 head's one-hot column)."""
+    from gym_narde.dqn import expand_mask, masked_argmax, policy_576
+    from gym_narde.vector import VecNardeEnv
+
+    env = VecNardeEnv(4096, device="cuda:0", seed=5)
+    env.selfplay(13)
+    words = env.legal_mask()
+    m = expand_mask(words)
+    q = torch.randn((4096, 576), device="cuda:0")
+    for eps in (0.0, 0.3, 1.0):
+        want = policy_576(q, words, eps, seed=7, tag=21, head=1)
+        got = policy_576(q, words, torch.tensor(eps, device="cuda:0"), seed=7,
+                         tag=torch.tensor(21, device="cuda:0"), head=1)
+        assert torch.equal(got, want)
+    tab = torch.randn((576, 576), device="cuda:0")
+    rows = torch.randint(0, 576, (4096,), device="cuda:0")
+    got = policy_576(q, words, 0.0, seed=7, tag=0, head=1, add=(tab, rows))
+    assert torch.equal(got, masked_argmax(q + tab[rows], m))
