@@ -907,6 +907,95 @@ __global__ void __launch_bounds__(kBlock) k_observe(Planes pl, int n, int32_t* _
   }
 }
 
+// One DQN transition for every env, fused (config 4, gym_narde/dqn.py
+// BatchedDQNDriver): the 198-float observation of the post-step record
+// (k_observe's encoding), the reference trainer's reward shaping
+// (train_deepq_pytorch.py:885-908), the prioritized-replay write of
+// (s, a, r', s', done) at ring slot (pos + i) % capacity with the running max
+// priority, and s <- s'.  One thread per observation float (coalesced rows;
+// the 32 B record is an L1 hit for the row's 198 threads); column 0 also
+// writes the env's scalars.  HBM per env: 792 B read (s) + 3 x 792 B written.
+struct TransArgs {
+  Planes pl;
+  int n;
+  int shaping;
+  float* state;                 // (n,198) in: s, out: s'
+  const int64_t* actions;       // (n,2)
+  const int32_t* reward;        // (n,)
+  const uint8_t* term;          // (n,)
+  const uint8_t* trunc;         // (n,)
+  float* off_seen;              // (n,2) borne-off trackers, white/black
+  float* r_obs;                 // replay (capacity,198)
+  float* r_next;                // replay (capacity,198)
+  int64_t* r_action;            // replay (capacity,2)
+  float* r_reward;              // replay (capacity,)
+  float* r_done;                // replay (capacity,)
+  float* r_prio;                // replay (capacity,)
+  const float* max_prio;        // device scalar
+  const int64_t* pos;           // device scalar: ring write cursor
+  int64_t capacity;
+};
+
+__device__ __forceinline__ float tes_value(uint4 a, uint4 b, int col) {
+  if (col >= 196) {
+    const bool black = (b.z >> 10) & 1u;
+    return (col == 196) != black ? 1.0f : 0.0f;
+  }
+  const int side = col >= 98 ? 1 : 0;
+  const int cc = col - 98 * side;
+  if (cc == 96) return 0.0f;  // bar
+  if (cc == 97) return (float)(side ? ((b.z >> 4) & 15u) : (b.z & 15u)) / 15.0f;
+  const Nib c = side ? Nib{{a.z, a.w, b.y}} : Nib{{a.x, a.y, b.x}};
+  const uint32_t v = nib_get(c, cc >> 2);
+  switch (cc & 3) {
+    case 0: return v >= 1u ? 1.0f : 0.0f;
+    case 1: return v >= 2u ? 1.0f : 0.0f;
+    case 2: return v >= 3u ? 1.0f : 0.0f;
+    default: return v >= 3u ? (float)(v - 3u) / 2.0f : 0.0f;
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_dqn_transition(TransArgs t) {
+  const uint32_t e = blockIdx.x * kBlock + threadIdx.x;  // n * 198 < 2^31 (checked on the host)
+  if (e >= (uint32_t)t.n * 198u) return;
+  const int i = (int)(e / 198u);
+  const int col = (int)(e - (uint32_t)i * 198u);
+  const uint4 a = t.pl.p0[i], b = t.pl.p1[i];
+  int64_t slot = *t.pos + i;  // pos < capacity and i < n <= capacity: one wrap at most
+  if (slot >= t.capacity) slot -= t.capacity;
+  const float nv = tes_value(a, b, col);
+  const float ov = t.state[e];
+  t.r_obs[slot * 198 + col] = ov;
+  t.r_next[slot * 198 + col] = nv;
+  t.state[e] = nv;
+  if (col != 0) return;
+  const float done = (t.term[i] | t.trunc[i]) ? 1.0f : 0.0f;
+  float r = (float)t.reward[i];
+  if (t.shaping) {
+    // +1 per checker newly borne off and +0.1 x total off, for the player
+    // to move AFTER the step (the reference reads the post-flip player);
+    // the trackers restart at 0 with a new episode.  Same fp32 ops as the
+    // torch restatement (BatchedDQNDriver._transition_torch).
+    const int black = (int)((b.z >> 10) & 1u);
+    const float now = (float)(black ? ((b.z >> 4) & 15u) : (b.z & 15u));
+    const float before = t.off_seen[2 * i + black];
+    {
+#pragma clang fp contract(off)  // torch rounds the product and the sum separately: no FMA
+      r = (r + fmaxf(now - before, 0.0f)) + 0.1f * now;
+    }
+    const float keep = 1.0f - done;
+    const float o0 = black ? t.off_seen[2 * i] : now;
+    const float o1 = black ? now : t.off_seen[2 * i + 1];
+    t.off_seen[2 * i] = o0 * keep;
+    t.off_seen[2 * i + 1] = o1 * keep;
+  }
+  t.r_action[2 * slot] = t.actions[2 * i];
+  t.r_action[2 * slot + 1] = t.actions[2 * i + 1];
+  t.r_reward[slot] = r;
+  t.r_done[slot] = done;
+  t.r_prio[slot] = *t.max_prio;
+}
+
 __global__ void __launch_bounds__(kBlock) k_mask576(Planes pl, int n, Rng g,
                                                     uint64_t* __restrict__ mask) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
@@ -1392,6 +1481,24 @@ int narde_observe(narde_env* e, int32_t* obs, float* tes, void* stream) {
   DeviceGuard dg(e->device);
   k_observe<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, obs, tes);
   return check_launch("k_observe");
+}
+
+int narde_dqn_transition(narde_env* e, float* state, const int64_t* actions, const int32_t* reward,
+                         const uint8_t* terminated, const uint8_t* truncated, float* off_seen, int shaping,
+                         float* r_obs, float* r_next, int64_t* r_action, float* r_reward, float* r_done,
+                         float* r_prio, const float* max_prio, const int64_t* pos, int64_t capacity,
+                         void* stream) {
+  if (!e || !state || !actions || !reward || !terminated || !truncated || !r_obs || !r_next || !r_action ||
+      !r_reward || !r_done || !r_prio || !max_prio || !pos || (shaping && !off_seen))
+    return fail(NARDE_EINVAL, "NULL argument");
+  if (capacity < e->n) return fail(NARDE_EINVAL, "replay capacity below the env count");
+  if (e->n * 198 >= (int64_t(1) << 31)) return fail(NARDE_EINVAL, "too many envs for one transition launch");
+  DeviceGuard dg(e->device);
+  TransArgs t{e->pl, (int)e->n, shaping, state, actions, reward, terminated, truncated, off_seen,
+              r_obs, r_next, r_action, r_reward, r_done, r_prio, max_prio, pos, capacity};
+  const int64_t total = e->n * 198;
+  k_dqn_transition<<<(unsigned)((total + kBlock - 1) / kBlock), kBlock, 0, (hipStream_t)stream>>>(t);
+  return check_launch("k_dqn_transition");
 }
 
 int narde_legal_mask576(narde_env* e, uint64_t* mask, void* stream) {

@@ -52,6 +52,8 @@ SIGNATURES = {
                                              _i32, _vp, _vp]),
     "narde_policy_masked_argmax576_dev": (_i32, [_i32, _vp, _i64, _vp, _i64, _vp, _u64, _vp, _i32, _vp,
                                                  _i64, _vp, _vp, _vp]),
+    "narde_dqn_transition": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
+                                    _vp, _vp, _i64, _vp]),
     "narde_violates_block_rule": (_i32, [_i32, _vp, _i64, _vp, _vp]),
     "narde_host_legal_moves": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "narde_host_step": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

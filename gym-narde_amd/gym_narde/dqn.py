@@ -211,7 +211,7 @@ class BatchedDQNDriver:
     def __init__(self, env, obs="tesauro198", train_batch=4096, capacity=1 << 20,
                  learning_rate=1e-4, gamma=0.99, epsilon=1.0, epsilon_min=0.01,
                  epsilon_decay=0.995, target_update=10, updates_per_step=1, shaping=True,
-                 seed=0):
+                 seed=0, fused=True):
         if env.full:
             raise ValueError("the DQN driver plays the reference's (move1, move2) actions: rules='ref2'")
         self.env, self.dev = env, env.device
@@ -232,6 +232,9 @@ class BatchedDQNDriver:
         self.epsilon_min, self.epsilon_decay = epsilon_min, epsilon_decay
         self.target_update, self.updates_per_step = target_update, updates_per_step
         self.shaping = shaping
+        # k_dqn_transition: observation + shaping + replay write in one kernel
+        # (the 198-float observation only; the torch restatement otherwise)
+        self.fused = bool(fused) and obs == "tesauro198"
         self.seed = seed
         self.tag_t = torch.zeros((), dtype=torch.int64, **z)
         self.steps = 0
@@ -300,6 +303,19 @@ class BatchedDQNDriver:
         x = self.state
         actions = self.act(x)
         _, reward, term, trunc, _ = self.env.step(actions.to(torch.int16))
+        if self.fused:
+            self._transition_fused(actions, reward, term, trunc)
+        else:
+            self._transition_torch(x, actions, reward, term, trunc)
+        self.tag_t.add_(1)
+        loss = None
+        for _ in range(self.updates_per_step):
+            loss = self._update_body()
+        return loss
+
+    def _transition_torch(self, x, actions, reward, term, trunc):
+        """Shaping + replay write + s <- s' in torch ops (the restatement
+        k_dqn_transition is tested against; the int24 observation path)."""
         r = reward.to(torch.float32)
         done = (term | trunc).to(torch.float32)
         nxt = self._observe(out=self._next)
@@ -316,11 +332,19 @@ class BatchedDQNDriver:
             self.off_seen.mul_((1.0 - done).unsqueeze(1))  # new episode: trackers restart at 0
         self.replay.add(x, actions, r, nxt, done)
         self.state.copy_(nxt)
-        self.tag_t.add_(1)
-        loss = None
-        for _ in range(self.updates_per_step):
-            loss = self._update_body()
-        return loss
+
+    def _transition_fused(self, actions, reward, term, trunc):
+        rp, n = self.replay, self.env.num_envs
+        if not (self.state.is_contiguous() and actions.is_contiguous() and actions.dtype == torch.int64):
+            raise ValueError("state / actions layout")
+        self.env.handle.call(
+            "narde_dqn_transition", _lib.ptr(self.state), _lib.ptr(actions), _lib.ptr(reward),
+            _lib.ptr(term), _lib.ptr(trunc), _lib.ptr(self.off_seen), int(self.shaping),
+            _lib.ptr(rp.obs), _lib.ptr(rp.next_obs), _lib.ptr(rp.action), _lib.ptr(rp.reward),
+            _lib.ptr(rp.done), _lib.ptr(rp.prio), _lib.ptr(rp.max_prio), _lib.ptr(rp.pos_t),
+            rp.capacity, ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream))
+        rp.pos_t.add_(n).remainder_(rp.capacity)
+        rp.advance(n)
 
     def _host_after_step(self, trained):
         self.steps += 1

@@ -214,6 +214,26 @@ int narde_policy_masked_argmax576_dev(int device, const float *q, int64_t ldq, c
                                       int64_t ld_add, const int64_t *add_row, int64_t *out,
                                       void *stream);
 
+/* One DQN transition for all B envs, fused (the batched trainer of
+ * gym_narde/dqn.py, config 4; reward shaping as train_deepq_pytorch.py:
+ * 885-908).  After a narde_step: s' = the Tesauro-198 observation of each
+ * env's record; r' = reward (+ shaping if `shaping`: +1 per checker newly
+ * borne off and +0.1 x total off for the player to move, off_seen f32[B][2]
+ * trackers updated and zeroed on done); done = terminated | truncated; the
+ * replay ring rows (pos + i) % capacity get (state[i], actions[i], r', s',
+ * done) and priority *max_prio; state[i] <- s'.  state f32[B][198] in/out,
+ * actions i64[B][2], reward i32[B], terminated/truncated u8[B]; replay
+ * arrays r_obs/r_next f32[capacity][198], r_action i64[capacity][2],
+ * r_reward/r_done/r_prio f32[capacity]; max_prio f32 and pos i64 are device
+ * scalars, 0 <= *pos < capacity (the caller advances pos).  capacity >= B,
+ * B * 198 < 2^31. */
+int narde_dqn_transition(narde_env *env, float *state, const int64_t *actions,
+                         const int32_t *reward, const uint8_t *terminated,
+                         const uint8_t *truncated, float *off_seen, int shaping, float *r_obs,
+                         float *r_next, int64_t *r_action, float *r_reward, float *r_done,
+                         float *r_prio, const float *max_prio, const int64_t *pos,
+                         int64_t capacity, void *stream);
+
 /* Stateless: Narde._violates_block_rule on n perspective boards i8[n][24]. */
 int narde_violates_block_rule(int device, const int8_t *boards, int64_t n, uint8_t *out,
                               void *stream);

@@ -175,3 +175,46 @@ def test_policy_kernel_device_scalars_and_fused_addend():
     rows = torch.randint(0, 576, (4096,), device="cuda:0")
     got = policy_576(q, words, 0.0, seed=7, tag=0, head=1, add=(tab, rows))
     assert torch.equal(got, masked_argmax(q + tab[rows], m))
+
+
+@pytest.mark.parametrize("shaping", [True, False])
+def test_fused_transition_matches_torch_restatement(shaping):
+    """k_dqn_transition (observation + reward shaping + replay write + s <- s')
+    is bit-exact against the driver's torch restatement on the same step,
+    including a replay-ring wrap and games that end in the step."""
+    from gym_narde.dqn import BatchedDQNDriver
+    from gym_narde.vector import VecNardeEnv
+
+    n = 4096
+    env = VecNardeEnv(n, device="cuda:0", seed=23)
+    env.selfplay(260)
+    drv = BatchedDQNDriver(env, capacity=3 * n, train_batch=1024, shaping=shaping)
+    drv.state = drv._observe()
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    off0 = torch.randint(0, 16, (n, 2), device="cuda:0", generator=g).float()
+    state0 = drv.state.clone()
+    rp = drv.replay
+    rp.pos_t.fill_(3 * n - 100)
+    rp.max_prio.fill_(2.5)
+    a = drv.act(drv.state)
+    _, reward, term, trunc, _ = env.step(a.to(torch.int16))
+    reward, term, trunc = reward.clone(), term.clone(), trunc.clone()
+    assert int((term | trunc).sum()) > 0
+
+    def run(fn):
+        drv.state.copy_(state0)
+        drv.off_seen.copy_(off0)
+        for t in (rp.obs, rp.next_obs, rp.action, rp.reward, rp.done, rp.prio):
+            t.zero_()
+        rp.pos_t.fill_(3 * n - 100)
+        fn()
+        return [t.clone() for t in (drv.state, drv.off_seen, rp.obs, rp.next_obs, rp.action, rp.reward,
+                                    rp.done, rp.prio, rp.pos_t)]
+
+    fused = run(lambda: drv._transition_fused(a, reward, term, trunc))
+    ref = run(lambda: drv._transition_torch(drv.state, a, reward, term, trunc))
+    names = ["state", "off_seen", "obs", "next_obs", "action", "reward", "done", "prio", "pos"]
+    for nm, x, y in zip(names, fused, ref):
+        assert torch.equal(x, y), nm
+    # the wrap really happened: rows at both ends of the ring were written
+    assert float(ref[7][0]) == 2.5 and float(ref[7][3 * n - 1]) == 2.5
