@@ -229,6 +229,36 @@ def test_full_batch_subset_and_invariants():
     assert stats[:, 0].sum() > B  # several episodes per env on average
 
 
+def test_bench_launch_window_and_invariants():
+    """The exact launch bench.py times (k_rollout_pc<true>: B = 65,536, 100
+    plies, every output), twice: a 2,048-env window of every output equals
+    the oracle on those global ids; over the whole batch the outputs obey
+    the rules' invariants (at most 15 checkers a side, reward only on a
+    finished game, no truncation within 200 plies of a fresh start)."""
+    B, P, seed, lo, m = 65536, 100, 99, 50000, 2048
+    env = vec(B, seed=seed)
+    bufs = env.rollout_buffers(P)
+    ref = O.SelfPlay(m, seed=seed, env0=lo)
+    ref.reset(0)
+    sl = slice(lo, lo + m)
+    for _ in range(2):
+        env.rollout(P, bufs)
+        rec = ref.run(P)
+        assert np.array_equal(np_(bufs["obs"][:, sl]), rec["obs"].astype(np.int32))
+        assert np.array_equal(np_(bufs["reward"][:, sl]), rec["reward"].astype(np.int32))
+        assert np.array_equal(np_(bufs["terminated"][:, sl]), rec["terminated"])
+        assert np.array_equal(np_(bufs["truncated"][:, sl]), rec["truncated"])
+        assert np.array_equal(np_(bufs["actions"][:, sl]), rec["action"])
+        obs = bufs["obs"]
+        assert int(obs.abs().max()) <= 15
+        assert bool((obs.clamp(min=0).sum(-1) <= 15).all()) and bool(((-obs).clamp(min=0).sum(-1) <= 15).all())
+        rew, term, trunc = bufs["reward"], bufs["terminated"].bool(), bufs["truncated"].bool()
+        assert bool(((rew == 0) | ((rew == 1) & term)).all())
+        assert not bool(trunc.any())
+    assert np.array_equal(np_(env.stats())[sl], ref.stats)
+    assert env.ply == 2 * P
+
+
 def test_sharded_handles_equal_single():
     B, seed, plies = 8192, 31337, 200
     full = vec(B, seed=seed)

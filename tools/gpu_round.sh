@@ -46,6 +46,10 @@ timeout -k 10 420 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>
   && (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
         -d "$OUT/rocprof_full4" -o bench -- python3 "$ROOT/bench.py" --rules full4 --no-cpu-baseline \
         > "$OUT/rocprof_full4.log" 2>&1) \
+  && echo "[gpu_round] $(date +%T) rocprof kernel trace dqn (config 4, graph replay)" \
+  && (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$OUT/rocprof_dqn" -o dqn -- python3 "$ROOT/tools/dqn_target.py" 65536 20 \
+        > "$OUT/rocprof_dqn.log" 2>&1) \
   && echo "[gpu_round] $(date +%T) done"
 rc=$?
 echo "[gpu_round] rc=$rc"
