@@ -234,7 +234,7 @@ def test_bench_launch_window_and_invariants():
     plies, every output), twice: a 2,048-env window of every output equals
     the oracle on those global ids; over the whole batch the outputs obey
     the rules' invariants (at most 15 checkers a side, reward only on a
-    finished game, no truncation within 200 plies of a fresh start)."""
+    finished game (1 or 2), no truncation within 200 plies of a fresh start)."""
     B, P, seed, lo, m = 65536, 100, 99, 50000, 2048
     env = vec(B, seed=seed)
     bufs = env.rollout_buffers(P)
@@ -253,7 +253,9 @@ def test_bench_launch_window_and_invariants():
         assert int(obs.abs().max()) <= 15
         assert bool((obs.clamp(min=0).sum(-1) <= 15).all()) and bool(((-obs).clamp(min=0).sum(-1) <= 15).all())
         rew, term, trunc = bufs["reward"], bufs["terminated"].bool(), bufs["truncated"].bool()
-        assert bool(((rew == 0) | ((rew == 1) & term)).all())
+        # narde_env.py:134-141: 1 for a win, 2 for a mars (loser bore off nothing)
+        assert bool(((rew == 0) | (((rew == 1) | (rew == 2)) & term)).all())
+        assert bool((rew[term] > 0).all())
         assert not bool(trunc.any())
     assert np.array_equal(np_(env.stats())[sl], ref.stats)
     assert env.ply == 2 * P
