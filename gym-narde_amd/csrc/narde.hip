@@ -65,6 +65,14 @@ __device__ __forceinline__ void draw(const Rng& g, uint32_t t, uint32_t i, uint3
   philox4x32_10(t, g.env0 + i, 0u, stream, g.k0, g.k1, r);
 }
 
+// the four words of ply t of env i (narde_rules.h ply_words: one Philox
+// block per two plies; a kernel that runs consecutive plies keeps the block)
+__device__ __forceinline__ void ply_draw(const Rng& g, uint32_t t, uint32_t i, uint32_t r[4]) {
+  uint32_t R[4];
+  ply_block(t, g.env0 + i, g.k0, g.k1, R);
+  ply_words_of(R, t, g.dice_mode, r);
+}
+
 // ------------------------------------------------------------------ kernels
 // init_t >= 0: also set the RNG counter (create); < 0: keep each env's counter
 __global__ void __launch_bounds__(kBlock) k_reset(Planes pl, int n, Rng g, uint32_t epoch,
@@ -120,7 +128,7 @@ __global__ void __launch_bounds__(kBlock) k_peek_dice(Planes pl, int n, Rng g, u
   const int i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   uint32_t r[4];
-  draw(g, pl.p1[i].w, (uint32_t)i, 0u, r);
+  ply_draw(g, pl.p1[i].w, (uint32_t)i, r);
   int d0, d1;
   dice_from(r[0], g.dice_mode, d0, d1);
   dice[2 * i] = (uint8_t)d0;
@@ -145,7 +153,7 @@ __global__ void __launch_bounds__(kBlock) k_legal(Planes pl, int n, Rng g,
     legal_roll(s, dice4 + 4 * i, l);
   } else {
     uint32_t r[4];
-    draw(g, s.t, (uint32_t)i, 0u, r);
+    ply_draw(g, s.t, (uint32_t)i, r);
     int d0, d1;
     dice_from(r[0], g.dice_mode, d0, d1);
     legal2(s, d0, d1, l);
@@ -437,7 +445,7 @@ __global__ void __launch_bounds__(kBlock) k_legal_full(Planes pl, int n, Rng g,
     }
   } else {
     uint32_t r[4];
-    draw(g, s.t, (uint32_t)i, 0u, r);
+    ply_draw(g, s.t, (uint32_t)i, r);
     dice_from(r[0], g.dice_mode, d0, d1);
   }
   const uint32_t w[4] = {0u, 0u, 0u, 0u};
@@ -576,13 +584,22 @@ __device__ __forceinline__ void store_outs(const Outs& out, size_t ix, const Sid
   __shared__ int4 obs_lds[kBlock * 6];                 \
   int4* const wave_lds = obs_lds + (threadIdx.x & ~63) * 6;
 
+// the words of ply t with the Philox block kept in R across consecutive
+// plies: a new block on the first ply of a launch and on every even t
+__device__ __forceinline__ void ply_draw_cached(const Rng& g, uint32_t t, uint32_t i, uint32_t R[4], bool first,
+                                                uint32_t r[4]) {
+  if (first || (t & 1u) == 0u) ply_block(t, g.env0 + i, g.k0, g.k1, R);
+  ply_words_of(R, t, g.dice_mode, r);
+}
+
 // one ply for env i: draw with the env's own counter, then the shared
 // host/device ply (narde_rules.h)
 __device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t i,
                                     const int16_t* actions, const uint8_t* dice, int max_steps,
-                                    bool autoreset, StepOut& o, int& term, int& trunc) {
+                                    bool autoreset, StepOut& o, int& term, int& trunc, uint32_t R[4],
+                                    bool first) {
   uint32_t r[4];
-  draw(g, s.t, i, 0u, r);
+  ply_draw_cached(g, s.t, i, R, first, r);
   int d0 = 0, d1 = 0, c1 = 0, c2 = 0;
   if (dice) { d0 = dice[2 * i]; d1 = dice[2 * i + 1]; }
   if (actions) { c1 = actions[2 * i]; c2 = actions[2 * i + 1]; }
@@ -595,9 +612,10 @@ __device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t i,
 // the last env pass valid = false and a dummy state)
 __device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t i, bool valid,
                                     const int8_t* play, const uint8_t* dice, int max_steps,
-                                    bool autoreset, TurnOut& o, int& term, int& trunc, CoopLds& W) {
+                                    bool autoreset, TurnOut& o, int& term, int& trunc, CoopLds& W,
+                                    uint32_t R[4], bool first) {
   uint32_t r[4];
-  draw(g, s.t, i, 0u, r);
+  ply_draw_cached(g, s.t, i, R, first, r);
   int d0 = 1, d1 = 2;
   if (dice && valid) { d0 = dice[2 * i]; d1 = dice[2 * i + 1]; }
   // one 8-B load per env: the play's four (from, die) pairs
@@ -631,11 +649,12 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
   int4 st = make_int4(0, 0, 0, 0);
   typename std::conditional<kFull, TurnOut, StepOut>::type o;
   int term, trunc;
+  uint32_t R[4];
   if constexpr (kFull)
     ply(s, st, a.g, (uint32_t)i, valid, a.play, a.dice, a.max_steps, a.autoreset != 0, o, term, trunc,
-        wave_coop);
+        wave_coop, R, true);
   else
-    ply(s, st, a.g, (uint32_t)i, a.actions, a.dice, a.max_steps, a.autoreset != 0, o, term, trunc);
+    ply(s, st, a.g, (uint32_t)i, a.actions, a.dice, a.max_steps, a.autoreset != 0, o, term, trunc, R, true);
   if (!valid) return;
   uint4 ra, rb;
   side_to_record(s, ra, rb);
@@ -660,14 +679,16 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Planes pl, int n, Rng g, int
   const bool wave_full = i - (int)(threadIdx.x & 63) + 64 <= n;
   Side s = valid ? side_from_record(pl.p0[i], pl.p1[i]) : side_start(0u);
   int4 st = make_int4(0, 0, 0, 0);
+  uint32_t R[4];  // the Philox block of the current ply pair
   for (int p = 0; p < plies; ++p) {
     typename std::conditional<kFull, TurnOut, StepOut>::type o;
     int term, trunc;
     if constexpr (kFull)
       ply(s, st, g, (uint32_t)i, valid, (const int8_t*)nullptr, nullptr, max_steps, true, o, term, trunc,
-          wave_coop);
+          wave_coop, R, p == 0);
     else
-      ply(s, st, g, (uint32_t)i, (const int16_t*)nullptr, nullptr, max_steps, true, o, term, trunc);
+      ply(s, st, g, (uint32_t)i, (const int16_t*)nullptr, nullptr, max_steps, true, o, term, trunc, R,
+          p == 0);
     if (kOut && valid) store_outs(out, (size_t)p * n + i, s, o, term, trunc, wave_lds, wave_full);
   }
   if (!valid) return;
@@ -693,7 +714,7 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Planes pl, int n, Rng g, int
 //     from the ply results the producers left in LDS and stored so that
 //     every wave-wide store is one contiguous 1 KiB.
 // Plies go in blocks of kPcR with one workgroup barrier per block; LDS holds
-// two slots of each ring (draws and results), 32 + 96 KiB.
+// two slots of each ring (draws and results), 16 + 96 KiB.
 // Equivalent, bit for bit, to `plies` narde_step(NULL, NULL, autoreset=1).
 #ifndef NARDE_PC_SETS
 #define NARDE_PC_SETS 1
@@ -704,7 +725,7 @@ constexpr int kPcThreads = (1 + kPcSets) * kPcEnvs;  // producers + consumers
 constexpr int kPcR = 4;                       // plies per barrier block
 
 struct PcLds {
-  uint4 draw[2][kPcR][kPcEnvs];               // Philox r0..r3 per env and ply
+  uint2 draw[2][kPcR][kPcEnvs];               // the ply's (wa, wb) per env and ply
   uint4 res[2][kPcR][3][kPcEnvs];             // ply results (kOut only)
 };
 
@@ -799,18 +820,22 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
   } else if (valid) {
     t0 = pl.p1[i].w;
   }
-  // consumer: draws of block b into slot b & 1 (Philox ctr {t, env, 0, 0})
+  // consumer: draws of block b into slot b & 1: one Philox block (ctr
+  // {t >> 1, env, 0, 0}) per ply pair, its halves to plies 2j and 2j + 1
+  // (narde_rules.h ply_words)
   auto draw_block = [&](int b) {
     const int p0 = b * kPcR;
     const int np = min(kPcR, plies - p0);
+    uint32_t R[4];
     for (int k = cset; k < np; k += kPcSets) {
-      uint32_t r[4];
+      const uint32_t t = t0 + (uint32_t)(p0 + k);
 #if NARDE_DIAG_ABLATE & 16
-      r[0] = (t0 + p0 + k) * 0x9E3779B9u ^ (uint32_t)i; r[1] = r[0] * 0x85EBCA6Bu; r[2] = r[1] ^ 0xC2B2AE35u; r[3] = r[0] + 7u;
+      R[0] = t * 0x9E3779B9u ^ (uint32_t)i; R[1] = R[0] * 0x85EBCA6Bu; R[2] = R[1] ^ 0xC2B2AE35u; R[3] = R[0] + 7u;
 #else
-      draw(g, t0 + (uint32_t)(p0 + k), (uint32_t)i, 0u, r);
+      if (k == cset || (t & 1u) == 0u || kPcSets > 1) ply_block(t, g.env0 + (uint32_t)i, g.k0, g.k1, R);
 #endif
-      L.draw[b & 1][k][le] = make_uint4(r[0], r[1], r[2], r[3]);
+      const bool odd = (t & 1u) != 0u;
+      L.draw[b & 1][k][le] = odd ? make_uint2(R[2], R[3]) : make_uint2(R[0], R[1]);
     }
   };
   if (!producer) draw_block(0);
@@ -821,8 +846,9 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
     if (producer) {
       if (valid) {
         for (int k = 0; k < np; ++k) {
-          const uint4 rv = L.draw[b & 1][k][le];
-          const uint32_t r[4] = {rv.x, rv.y, rv.z, rv.w};
+          const uint2 rv = L.draw[b & 1][k][le];
+          uint32_t r[4];
+          ply_words(rv.x, rv.y, g.dice_mode, r);
           StepOut o;
           int term, trunc;
           env_ply(s, st, r, false, 0, 0, g.dice_mode, true, 0, 0, max_steps, true, o, term, trunc);
@@ -1002,7 +1028,7 @@ __global__ void __launch_bounds__(kBlock) k_mask576(Planes pl, int n, Rng g,
   if (i >= n) return;
   const Side s = side_from_record(pl.p0[i], pl.p1[i]);
   uint32_t r[4];
-  draw(g, s.t, (uint32_t)i, 0u, r);
+  ply_draw(g, s.t, (uint32_t)i, r);
   int d0, d1;
   dice_from(r[0], g.dice_mode, d0, d1);
   Legal l;
@@ -1041,7 +1067,7 @@ __global__ void __launch_bounds__(kBlock) k_mask576_move2(Planes pl, int n, Rng 
     d1 = dice[2 * i + 1];
   } else {
     uint32_t r[4];
-    draw(g, s.t, (uint32_t)i, 0u, r);
+    ply_draw(g, s.t, (uint32_t)i, r);
     dice_from(r[0], g.dice_mode, d0, d1);
   }
   Legal l;

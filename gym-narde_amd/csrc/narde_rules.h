@@ -888,10 +888,36 @@ NARDE_FN Side side_reset(uint32_t r) {
   return side_start(w > b ? 0u : 1u);
 }
 
+// The ply stream.  One Philox4x32-10 block serves two
+// consecutive plies of an env: R = Philox(ctr = {t >> 1, env, 0, 0}); ply t
+// takes (wa, wb) = (R0, R1) if t is even, (R2, R3) if odd, and derives the
+// four words it consumes:
+//   r0 = wa                 dice (mulhi(r0, 36), or 30 non-double pairs)
+//   r1 = wa * m mod 2^32    policy pick 1: the low part the dice draw leaves
+//                           (m = 36, or 30), uniform and independent of it
+//   r2 = wb                 policy pick 2
+//   r3 = wb * 0x9E3779B9    opening roll of the next episode (odd multiplier)
+NARDE_FN void ply_words(uint32_t wa, uint32_t wb, int dice_mode, uint32_t r[4]) {
+  r[0] = wa;
+  r[1] = wa * (dice_mode == 1 ? 30u : 36u);
+  r[2] = wb;
+  r[3] = wb * 0x9E3779B9u;
+}
+
+// the Philox block of ply t (shared by plies 2j and 2j + 1)
+NARDE_FN void ply_block(uint32_t t, uint32_t env, uint32_t k0, uint32_t k1, uint32_t R[4]) {
+  philox4x32_10(t >> 1, env, 0u, 0u, k0, k1, R);
+}
+
+NARDE_FN void ply_words_of(const uint32_t R[4], uint32_t t, int dice_mode, uint32_t r[4]) {
+  const bool odd = (t & 1u) != 0u;
+  ply_words(odd ? R[2] : R[0], odd ? R[3] : R[1], dice_mode, r);
+}
+
 // One ply for one env: NardeEnv.step + gymnasium TimeLimit
 // (max_episode_steps, gym_narde/__init__.py:3-7) + optional auto-reset,
 // then t += 1.
-// r = Philox4x32-10(ctr = {s.t, env, 0, 0}): r0 dice (unless given), r1/r2
+// r = the ply's words (ply_words above): r0 dice (unless given), r1/r2
 // policy picks, r3 opening roll of the next episode.  st = {episodes,
 // white points, black points} increments.
 NARDE_FN void env_ply(Side& s, int4& st, const uint32_t r[4], bool have_dice, int d0, int d1,

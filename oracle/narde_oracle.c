@@ -544,11 +544,31 @@ static void or_reset_state(or_state *s, uint32_t r) {
 
 /*
  * Self-play driver restatement.  For env e (global id) and lockstep ply t:
- *   Philox4x32-10(ctr = {t, e, 0, 0}, key = {seed_lo, seed_hi}) -> r0..r3
- *   r0 dice, r1 move1 pick, r2 move2 pick, r3 opening roll of the episode
- *   that starts if this ply ends the current one.
+ *   R = Philox4x32-10(ctr = {t >> 1, e, 0, 0}, key = {seed_lo, seed_hi})
+ *   (one block per ply pair), (wa, wb) = (R0, R1) for even t, (R2, R3) for
+ *   odd t, and the ply's words
+ *   r0 = wa dice, r1 = wa * m mod 2^32 move1 pick (m = 36, or 30 for the
+ *   non-double dice law), r2 = wb move2 pick, r3 = wb * 0x9E3779B9 opening
+ *   roll of the episode that starts if this ply ends the current one.
  * Reset of env e with reset-epoch q: ctr = {q, e, 0, 1}, r0 = opening roll.
  */
+static void or_ply_words(const uint32_t R[4], uint32_t t, int dice_mode, uint32_t r[4]) {
+    uint32_t wa = (t & 1u) ? R[2] : R[0];
+    uint32_t wb = (t & 1u) ? R[3] : R[1];
+    r[0] = wa;
+    r[1] = wa * (dice_mode == 1 ? 30u : 36u);
+    r[2] = wb;
+    r[3] = wb * 0x9E3779B9u;
+}
+
+static void or_ply_draw(uint32_t t, int64_t e, const uint32_t key[2], int first, int dice_mode,
+                        uint32_t R[4], uint32_t r[4]) {
+    if (first || (t & 1u) == 0u) {
+        uint32_t ctr[4] = {t >> 1, (uint32_t)e, 0, 0};
+        or_philox4x32_10(ctr, key, R);
+    }
+    or_ply_words(R, t, dice_mode, r);
+}
 void or_reset_batch(int64_t n, int64_t env0, uint64_t seed, uint32_t epoch,
                     int8_t *board, uint8_t *off, uint8_t *ft, int8_t *player, uint16_t *elapsed) {
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
@@ -580,9 +600,10 @@ void or_selfplay(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int plies,
         or_state s;
         load_state(&s, board + i * 24, off + i * 2, ft + i * 2, player[i]);
         s.elapsed = elapsed[i];
+        uint32_t R[4];
         for (int p = 0; p < plies; ++p) {
-            uint32_t ctr[4] = {t0 + (uint32_t)p, (uint32_t)(env0 + i), 0, 0}, r[4];
-            or_philox4x32_10(ctr, key, r);
+            uint32_t r[4];
+            or_ply_draw(t0 + (uint32_t)p, env0 + i, key, p == 0, dice_mode, R, r);
             int32_t d[2];
             or_dice_from(r[0], dice_mode, d);
             or_step_out o;
@@ -635,9 +656,10 @@ void or_selfplay_full(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int p
         or_state s;
         load_state(&s, board + i * 24, off + i * 2, ft + i * 2, player[i]);
         s.elapsed = elapsed[i];
+        uint32_t R[4];
         for (int p = 0; p < plies; ++p) {
-            uint32_t ctr[4] = {t0 + (uint32_t)p, (uint32_t)(env0 + i), 0, 0}, r[4];
-            or_philox4x32_10(ctr, key, r);
+            uint32_t r[4];
+            or_ply_draw(t0 + (uint32_t)p, env0 + i, key, p == 0, dice_mode, R, r);
             int32_t d[2];
             or_dice_from(r[0], dice_mode, d);
             uint32_t w[4] = {r[1], r[2], 0, 0};

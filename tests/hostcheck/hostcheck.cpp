@@ -16,6 +16,13 @@ static void draw(uint64_t seed, uint32_t t, uint32_t env, uint32_t stream, uint3
   philox4x32_10(t, env, 0u, stream, (uint32_t)seed, (uint32_t)(seed >> 32), r);
 }
 
+// the words of ply t (narde_rules.h ply_words), a fresh Philox block per ply
+static void ply_draw(uint64_t seed, uint32_t t, uint32_t env, int dice_mode, uint32_t r[4]) {
+  uint32_t R[4];
+  ply_block(t, env, (uint32_t)seed, (uint32_t)(seed >> 32), R);
+  ply_words_of(R, t, dice_mode, r);
+}
+
 static Side load(const int8_t* board, const uint8_t* off, const uint8_t* ft, int player,
                  uint32_t elapsed) {
   uint4 a, b;
@@ -97,7 +104,7 @@ void hc_selfplay(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int plies,
     int4 st = make_int4(0, 0, 0, 0);
     for (int p = 0; p < plies; ++p) {
       uint32_t r[4];
-      draw(seed, t0 + (uint32_t)p, (uint32_t)(env0 + i), 0u, r);
+      ply_draw(seed, t0 + (uint32_t)p, (uint32_t)(env0 + i), dice_mode, r);
       int d0, d1;
       dice_from(r[0], dice_mode, d0, d1);
       StepOut o;
@@ -164,7 +171,7 @@ void hc_selfplay_full(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int p
     int4 st = make_int4(0, 0, 0, 0);
     for (int p = 0; p < plies; ++p) {
       uint32_t r[4];
-      draw(seed, s.t, (uint32_t)(env0 + i), 0u, r);
+      ply_draw(seed, s.t, (uint32_t)(env0 + i), dice_mode, r);
       TurnOut o;
       int tm, tr;
       env_ply_full(s, st, r, (uint32_t)(env0 + i), (uint32_t)seed, (uint32_t)(seed >> 32), false, 0,
