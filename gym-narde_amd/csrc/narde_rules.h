@@ -317,10 +317,11 @@ NARDE_FN void legal_sorted(const Side& s, const int* dd, int n, Legal& l) {
   l.count = count;
 }
 
-// the two-dice list of NardeEnv.step (roll in any order)
-NARDE_FN void legal2(const Side& s, int d0, int d1, Legal& l) {
+// the two-dice list of NardeEnv.step (roll in any order); low =
+// block_lowmask(s.P)
+NARDE_FN void legal2_low(const Side& s, int d0, int d1, uint32_t low, Legal& l) {
   const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
-  const Blocks bl = block_info(s.O, s.P);
+  const Blocks bl = block_info_low(s.O, low);
   l.n = 2;
   l.d[0] = dh; l.d[1] = dl; l.d[2] = 0; l.d[3] = 0;
   l.L[2] = 0u; l.L[3] = 0u;
@@ -333,6 +334,7 @@ NARDE_FN void legal2(const Side& s, int d0, int d1, Legal& l) {
   l.L[1] = Ll;
   l.count = __builtin_popcount(Lh) + __builtin_popcount(Ll);
 }
+NARDE_FN void legal2(const Side& s, int d0, int d1, Legal& l) { legal2_low(s, d0, d1, block_lowmask(s.P), l); }
 
 // get_valid_moves for an explicit roll of up to 4 dice (0 = unused slot)
 NARDE_FN void legal_roll(const Side& s, const uint8_t* d4, Legal& l) {
@@ -448,7 +450,10 @@ struct StepOut {
 // divergent branch around the flip
 NARDE_FN void env_step(Side& s, int d0, int d1, int code1, int code2, bool policy, uint32_t r1,
                        uint32_t r2, StepOut& o, bool flip_always = false) {
-  legal2(s, d0, d1, o.l1);
+  // the mover's moves never change the opponent's points: one low mask
+  // serves both lists
+  const uint32_t low = block_lowmask(s.P);
+  legal2_low(s, d0, d1, low, o.l1);
   o.L2 = 0u; o.d2 = 0; o.count2 = -1;
   const int n1 = o.l1.count;
   int f1 = -1, t1 = -1;
@@ -477,7 +482,7 @@ NARDE_FN void env_step(Side& s, int d0, int d1, int code1, int code2, bool polic
     const int dist = t1 == OFF ? f1 + 1 : (f1 > t1 ? f1 - t1 : t1 - f1);
     const int rem = (d0 == dist) ? d1 : ((d1 == dist) ? d0 : d1);
     // second get_valid_moves([rem]) (:88): one die, first_turn already cleared
-    const Blocks bl = block_info(s.O, s.P);
+    const Blocks bl = block_info_low(s.O, low);
     const uint32_t L2 = die_filter(s.O, s.S1o, bl, die_candidates(s.O, s.P, rem), rem);
     o.L2 = L2;
     o.d2 = rem;
@@ -870,13 +875,15 @@ NARDE_FN void philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, 
 NARDE_FN void dice_from(uint32_t r, int dice_mode, int& d0, int& d1) {
   if (dice_mode == 1) {
     const uint32_t k = mulhi_u32(r, 30u);
-    const int a = (int)(k / 5u) + 1, j = (int)(k % 5u);
+    const uint32_t q = (k * 205u) >> 10;  // k / 5 for k < 30
+    const int a = (int)q + 1, j = (int)(k - 5u * q);
     d0 = a;
     d1 = j < a - 1 ? j + 1 : j + 2;
   } else {
     const uint32_t k = mulhi_u32(r, 36u);
-    d0 = (int)(k / 6u) + 1;
-    d1 = (int)(k % 6u) + 1;
+    const uint32_t q = (k * 43u) >> 8;  // k / 6 for k < 36, a full-rate 24-bit multiply
+    d0 = (int)q + 1;
+    d1 = (int)(k - 6u * q) + 1;
   }
 }
 
