@@ -206,3 +206,75 @@ def test_oracle_tesauro_bounds():
     assert np.array_equal(cnt.astype(np.int64), np.where(d["post_board"] > 0, d["post_board"], 0))
     random.seed(0)
 
+
+
+def _prime_boards(n, seed):
+    """Random legal positions biased toward 4-5-point own runs with single
+    checkers around them: where the block rule's window completion (and its
+    single-checker source exception) decides legality.  White moves from
+    perspective point 23 down; +counts white, -counts black."""
+    rng = np.random.default_rng(seed)
+    boards = np.zeros((n, 24), np.int8)
+    for i in range(n):
+        b = boards[i]
+        own = 15
+        start = int(rng.integers(0, 20))
+        length = int(rng.integers(4, 6))
+        for p in range(start, min(24, start + length)):
+            c = int(rng.integers(1, 3))
+            b[p] = c
+            own -= c
+        while own > 0:
+            p = int(rng.integers(0, 24))
+            if b[p] >= 0:
+                b[p] += 1
+                own -= 1
+        opp = 15
+        free = np.nonzero(b == 0)[0]
+        k = int(rng.integers(1, 5))
+        pts = rng.choice(free, size=min(k, len(free)), replace=False)
+        for j, p in enumerate(pts):
+            c = opp if j == len(pts) - 1 else int(rng.integers(1, opp - (len(pts) - 1 - j) + 1))
+            b[p] = -c
+            opp -= c
+            if opp == 0:
+                break
+    return boards
+
+
+def test_hostcheck_legal_random_prime_boards(hostcheck):
+    """The bitmask engine's lists (incl. the branch-free block filter) equal
+    the oracle's on 20,000 random run-heavy positions and every roll of one
+    and two dice."""
+    n = 20000
+    boards = _prime_boards(n, 7)
+    assert (np.where(boards > 0, boards, 0).sum(1) == 15).all()
+    assert (np.where(boards < 0, -boards, 0).sum(1) == 15).all()
+    rng = np.random.default_rng(8)
+    roll4 = np.zeros((n, 4), np.uint8)
+    nd = rng.integers(1, 3, n)
+    roll4[:, 0] = rng.integers(1, 7, n)
+    roll4[:, 1] = np.where(nd == 2, rng.integers(1, 7, n), 0)
+    ft = np.zeros((n, 2), np.uint8)
+    player = np.ones(n, np.int8)
+    off = np.zeros((n, 2), np.uint8)
+    ref_moves, ref_cnt = O.legal_moves(boards, ft, player, roll4, nd.astype(np.uint8))
+    moves = np.empty((n, 64, 2), np.int8)
+    cnt = np.empty(n, np.int16)
+    hostcheck.hc_legal_batch(ctypes.c_int64(n), P(boards), P(off), P(ft), P(player), P(roll4), P(moves),
+                             P(cnt))
+    assert np.array_equal(cnt, ref_cnt)
+    assert np.array_equal(moves, ref_moves)
+    # the sample reaches the block rule: on one-die rolls, count the
+    # positions where a plain candidate (own source, landing not on the
+    # opponent, no bear-off) is missing from the list
+    one = np.nonzero(nd == 1)[0]
+    d = roll4[one, 0].astype(np.int64)
+    b = boards[one].astype(np.int64)
+    pts = np.arange(24)
+    to = pts[None, :] - d[:, None]
+    land = np.take_along_axis(b, np.clip(to, 0, 23), 1)
+    cand = ((b > 0) & (to >= 0) & (land >= 0)).sum(1)
+    normal = ((ref_moves[one, :, 1] != 24) & (np.arange(64)[None, :] < ref_cnt[one, None])).sum(1)
+    assert (normal <= cand).all()
+    assert int((normal < cand).sum()) > 200
