@@ -1,0 +1,333 @@
+// dqn_learner.hip -- the learner half of the batched DQN driver (config 4,
+// gym_narde/dqn.py BatchedDQNDriver) as a handful of fused HIP kernels.
+//
+// The reference trainer's replay() (train_deepq_pytorch.py:602-750) runs on a
+// 64-sample minibatch as ~100 tiny tensor ops; at B = 65,536 envs the driver
+// trains on 4,096 samples per step and those ops are launch-bound (each
+// kernel boundary costs ~4.5 us on MI355X even inside a CUDA graph).  These
+// kernels fold the chains that are not GEMMs:
+//   k_per_sample       prioritized sampling (PrioritizedReplayBuffer.sample,
+//                      :279-342): inverse-CDF search, importance weights,
+//                      beta annealing -- one block;
+//   k_gather_batch     the minibatch rows of the replay ring;
+//   k_rowmax_addend    the target move-2 head's max over codes with the
+//                      one-hot column added on the fly;
+//   k_dqn_loss         targets, TD errors, the decomposed loss (:653-720) and
+//                      its gradient w.r.t. the two Q-values -- one block;
+//   k_prio_update      new priorities |td| + eps, the running max priority and
+//                      the per-update epsilon decay (:745-746) -- one block.
+// Every scalar the driver updates per step (sampling counter, beta, max
+// priority, epsilon) lives in device memory, so a captured graph replays
+// with current values.  fp32 throughout, the same operation order as the
+// torch restatement (BatchedDQNDriver._update_torch); tests/test_gpu_dqn.py
+// checks each kernel against it.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/narde.h"
+#include "narde_rules.h"
+
+namespace narde_abi {
+int set_error(int code, const char* what);  // narde.hip: narde_last_error()'s buffer
+}
+
+namespace {
+
+constexpr int kLearnThreads = 1024;
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != d) (void)hipSetDevice(d);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int check_launch(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return narde_abi::set_error(NARDE_EHIP, hipGetErrorString(e));
+  (void)what;
+  return NARDE_OK;
+}
+
+int bad(const char* what) { return narde_abi::set_error(NARDE_EINVAL, what); }
+
+// block-wide max / sum over kLearnThreads threads (wave shuffles, then the
+// 16 wave results through LDS); every thread gets the result
+__device__ __forceinline__ float block_max(float v, float* lds) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) lds[wave] = v;
+  __syncthreads();
+  v = lane < kLearnThreads / 64 ? lds[lane] : -__builtin_inff();
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  __syncthreads();
+  return v;
+}
+
+// a fixed-order tree sum (deterministic from run to run)
+__device__ __forceinline__ float block_sum(float v, float* lds) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) lds[wave] = v;
+  __syncthreads();
+  v = lane < kLearnThreads / 64 ? lds[lane] : 0.0f;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  return v;
+}
+
+// ---------------------------------------------------------------- sampling
+// batch draws u_j = Philox4x32-10({*counter, j, 0, 7}, seed) r0 / 2^32 (24
+// significant bits, as torch.rand), v_j = u_j * total; idx_j = the first k
+// with cdf[k] > v_j (torch.searchsorted(right=True)), clamped to n - 1;
+// w_j = (n * p[idx] / total)^-beta normalised by the batch max.  Then beta
+// <- min(1, beta + beta_inc) and *counter += 1.
+// One sample per thread over ceil(batch / 256) blocks (a single block would
+// pull every search through one CU's L1); the batch max meets in
+// scratch[0] (atomicMax on the float's bits: the weights are positive) and
+// the last block to finish (ticket scratch[1]) normalises, steps beta and
+// the counter, and clears the scratch for the next call.
+constexpr int kSampleThreads = 256;
+
+__global__ void __launch_bounds__(kSampleThreads) k_per_sample(const float* __restrict__ p,
+                                                               const float* __restrict__ cdf, int64_t n,
+                                                               int batch, uint32_t k0, uint32_t k1,
+                                                               int64_t* __restrict__ counter,
+                                                               double* __restrict__ beta, double beta_inc,
+                                                               int64_t* __restrict__ idx_out,
+                                                               float* __restrict__ w_out,
+                                                               float* __restrict__ u_out,
+                                                               uint32_t* __restrict__ scratch) {
+  __shared__ float red[kSampleThreads / 64];
+  __shared__ bool last;
+  const int j = blockIdx.x * kSampleThreads + threadIdx.x;
+  float x = 0.0f;
+  if (j < batch) {
+    const float total = cdf[n - 1];
+    uint32_t r[4];
+    narde::philox4x32_10((uint32_t)*counter, (uint32_t)j, 0u, 7u, k0, k1, r);
+    const float u = (float)(r[0] >> 8) * (1.0f / 16777216.0f);
+    if (u_out) u_out[j] = u;
+    const float v = u * total;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (cdf[mid] > v) hi = mid;
+      else lo = mid + 1;
+    }
+    const int64_t k = lo < n - 1 ? lo : n - 1;
+    x = powf((float)n * (p[k] / total), -(float)*beta);
+    idx_out[j] = k;
+    w_out[j] = x;
+  }
+  __threadfence();  // this thread's idx/w writes before the block's ticket (release)
+  // block max, then the grid max in scratch[0]
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = red[0];
+    for (int w = 1; w < kSampleThreads / 64; ++w) m = fmaxf(m, red[w]);
+    atomicMax(&scratch[0], __float_as_uint(m));
+    __threadfence();
+    last = atomicAdd(&scratch[1], 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();  // acquire: every block's w writes are visible
+  const float wmax = __uint_as_float(atomicAdd(&scratch[0], 0u));
+  for (int i = threadIdx.x; i < batch; i += kSampleThreads) w_out[i] = w_out[i] / wmax;
+  if (threadIdx.x == 0) {
+    const double b = *beta + beta_inc;
+    *beta = b < 1.0 ? b : 1.0;
+    *counter += 1;
+    scratch[0] = 0u;
+    scratch[1] = 0u;
+  }
+}
+
+// ------------------------------------------------------------- minibatch rows
+__global__ void __launch_bounds__(256) k_gather_batch(const int64_t* __restrict__ idx, int batch, int ss,
+                                                      const float* __restrict__ obs,
+                                                      const float* __restrict__ next_obs,
+                                                      const int64_t* __restrict__ action,
+                                                      const float* __restrict__ reward,
+                                                      const float* __restrict__ done, float* __restrict__ s,
+                                                      float* __restrict__ ns, int64_t* __restrict__ a,
+                                                      float* __restrict__ r, float* __restrict__ d) {
+  const uint32_t e = blockIdx.x * 256u + threadIdx.x;
+  if (e >= (uint32_t)batch * (uint32_t)ss) return;
+  const int j = (int)(e / (uint32_t)ss);
+  const int col = (int)(e - (uint32_t)j * (uint32_t)ss);
+  const int64_t k = idx[j];
+  s[e] = obs[k * ss + col];
+  ns[e] = next_obs[k * ss + col];
+  if (col == 0) {
+    a[2 * j] = action[2 * k];
+    a[2 * j + 1] = action[2 * k + 1];
+    r[j] = reward[k];
+    d[j] = done[k];
+  }
+}
+
+// ------------------------------------------------- target move-2 head max
+// out[i] = max_c base[i][c] + tab[rows[i]][c] over the 576 codes: one wave
+// per row (the same single fp32 add as the torch path, then max)
+__global__ void __launch_bounds__(256) k_rowmax_addend(const float* __restrict__ base, int64_t ld,
+                                                       const float* __restrict__ tab, int64_t ld_tab,
+                                                       const int64_t* __restrict__ rows, int n,
+                                                       float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  if (i >= n) return;
+  const float* br = base + (size_t)i * (size_t)ld;
+  const float* tr = tab + (size_t)rows[i] * (size_t)ld_tab;
+  float m = -__builtin_inff();
+#pragma unroll
+  for (int j = 0; j < 9; ++j) m = fmaxf(m, br[64 * j + lane] + tr[64 * j + lane]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if (lane == 0) out[i] = m;
+}
+
+// --------------------------------------------------------------- the loss
+// t1 = r + (1 - d) * gamma * m1, t2 likewise (m = the target heads' maxima);
+// td = clamp(|t1 - q1| + |t2 - q2|, 0, 100); loss = mean(w (q1 - t1)^2) +
+// mean(w (q2 - t2)^2); g = dloss/dq = (1/B) * w * (2 (q - t)) in torch's
+// autograd order.  Each fp32 operation rounds on its own, as torch's
+// elementwise kernels do (no contraction).
+__global__ void __launch_bounds__(kLearnThreads) k_dqn_loss(const float* __restrict__ q1,
+                                                            const float* __restrict__ q2,
+                                                            const float* __restrict__ m1,
+                                                            const float* __restrict__ m2,
+                                                            const float* __restrict__ r,
+                                                            const float* __restrict__ d,
+                                                            const float* __restrict__ w, int batch,
+                                                            float gamma, float* __restrict__ td,
+                                                            float* __restrict__ loss,
+                                                            float* __restrict__ loss_copy,
+                                                            float* __restrict__ g1, float* __restrict__ g2) {
+#pragma clang fp contract(off)
+  __shared__ float red[kLearnThreads / 64];
+  const float inv_b = 1.0f / (float)batch;
+  float s1 = 0.0f, s2 = 0.0f;
+  for (int j = threadIdx.x; j < batch; j += kLearnThreads) {
+    const float nd = (1.0f - d[j]) * gamma;
+    const float t1 = r[j] + nd * m1[j];
+    const float t2 = r[j] + nd * m2[j];
+    const float e1 = q1[j] - t1, e2 = q2[j] - t2;
+    const float a = fabsf(t1 - q1[j]) + fabsf(t2 - q2[j]);
+    td[j] = fminf(fmaxf(a, 0.0f), 100.0f);
+    s1 += w[j] * (e1 * e1);
+    s2 += w[j] * (e2 * e2);
+    const float gw = inv_b * w[j];
+    g1[j] = gw * (2.0f * e1);
+    g2[j] = gw * (2.0f * e2);
+  }
+  s1 = block_sum(s1, red);
+  s2 = block_sum(s2, red);
+  if (threadIdx.x == 0) {
+    const float l = s1 / (float)batch + s2 / (float)batch;
+    *loss = l;
+    if (loss_copy) *loss_copy = l;
+  }
+}
+
+// ------------------------------------------------------ priorities, epsilon
+// prio[idx_j] = td_j + eps; max_prio = max(max_prio, max_j prio); then
+// epsilon <- epsilon * decay if epsilon > eps_min (one decay per update)
+__global__ void __launch_bounds__(kLearnThreads) k_prio_update(const int64_t* __restrict__ idx,
+                                                               const float* __restrict__ td, int batch,
+                                                               float eps, float* __restrict__ prio,
+                                                               float* __restrict__ max_prio,
+                                                               float* __restrict__ epsilon, float eps_min,
+                                                               float eps_decay) {
+  __shared__ float red[kLearnThreads / 64];
+  float m = -__builtin_inff();
+  for (int j = threadIdx.x; j < batch; j += kLearnThreads) {
+    const float pr = td[j] + eps;
+    prio[idx[j]] = pr;
+    m = fmaxf(m, pr);
+  }
+  m = block_max(m, red);
+  if (threadIdx.x == 0) {
+    *max_prio = fmaxf(*max_prio, m);
+    if (epsilon) {
+      const float e = *epsilon;
+      *epsilon = e > eps_min ? e * eps_decay : e;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int narde_per_sample(int device, const float* p, const float* cdf, int64_t n, int64_t batch, uint64_t seed,
+                     int64_t* counter, double* beta, double beta_inc, int64_t* idx, float* w, float* u,
+                     uint32_t* scratch, void* stream) {
+  if (!p || !cdf || !counter || !beta || !idx || !w || !scratch) return bad("NULL argument");
+  if (n <= 0 || batch <= 0 || batch > (int64_t(1) << 24)) return bad("need n > 0 and 0 < batch <= 2^24");
+  DeviceGuard dg(device);
+  const unsigned blocks = (unsigned)((batch + kSampleThreads - 1) / kSampleThreads);
+  k_per_sample<<<blocks, kSampleThreads, 0, (hipStream_t)stream>>>(p, cdf, n, (int)batch, (uint32_t)seed,
+                                                                   (uint32_t)(seed >> 32), counter, beta, beta_inc,
+                                                                   idx, w, u, scratch);
+  return check_launch("k_per_sample");
+}
+
+int narde_gather_batch(int device, const int64_t* idx, int64_t batch, int state_size, const float* obs,
+                       const float* next_obs, const int64_t* action, const float* reward, const float* done,
+                       float* s, float* ns, int64_t* a, float* r, float* d, void* stream) {
+  if (!idx || !obs || !next_obs || !action || !reward || !done || !s || !ns || !a || !r || !d)
+    return bad("NULL argument");
+  if (batch <= 0 || state_size <= 0 || batch * state_size >= (int64_t(1) << 31)) return bad("bad sizes");
+  DeviceGuard dg(device);
+  const int64_t total = batch * state_size;
+  k_gather_batch<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(
+      idx, (int)batch, state_size, obs, next_obs, action, reward, done, s, ns, a, r, d);
+  return check_launch("k_gather_batch");
+}
+
+int narde_rowmax_addend(int device, const float* base, int64_t ld, const float* tab, int64_t ld_tab,
+                        const int64_t* rows, int64_t n, float* out, void* stream) {
+  if (!base || !tab || !rows || !out) return bad("NULL argument");
+  if (n < 0 || n > (int64_t(1) << 31) - 4 || ld < 576 || ld_tab < 576) return bad("bad sizes");
+  if (n == 0) return NARDE_OK;
+  DeviceGuard dg(device);
+  k_rowmax_addend<<<(unsigned)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(base, ld, tab, ld_tab, rows, (int)n,
+                                                                            out);
+  return check_launch("k_rowmax_addend");
+}
+
+int narde_dqn_loss(int device, const float* q1, const float* q2, const float* m1, const float* m2, const float* r,
+                   const float* d, const float* w, int64_t batch, float gamma, float* td, float* loss,
+                   float* loss_copy, float* g1, float* g2, void* stream) {
+  if (!q1 || !q2 || !m1 || !m2 || !r || !d || !w || !td || !loss || !g1 || !g2) return bad("NULL argument");
+  if (batch <= 0 || batch > (int64_t(1) << 24)) return bad("bad batch");
+  DeviceGuard dg(device);
+  k_dqn_loss<<<1, kLearnThreads, 0, (hipStream_t)stream>>>(q1, q2, m1, m2, r, d, w, (int)batch, gamma, td, loss,
+                                                           loss_copy, g1, g2);
+  return check_launch("k_dqn_loss");
+}
+
+int narde_prio_update(int device, const int64_t* idx, const float* td, int64_t batch, float eps, float* prio,
+                      float* max_prio, float* epsilon, float eps_min, float eps_decay, void* stream) {
+  if (!idx || !td || !prio || !max_prio) return bad("NULL argument");
+  if (batch <= 0 || batch > (int64_t(1) << 24)) return bad("bad batch");
+  DeviceGuard dg(device);
+  k_prio_update<<<1, kLearnThreads, 0, (hipStream_t)stream>>>(idx, td, (int)batch, eps, prio, max_prio, epsilon,
+                                                              eps_min, eps_decay);
+  return check_launch("k_prio_update");
+}
+
+}  // extern "C"

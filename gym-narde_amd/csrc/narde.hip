@@ -962,39 +962,30 @@ struct TransArgs {
   int64_t capacity;
 };
 
+// value of column col of the 198-float observation of a record (k_observe's
+// layout), branch-free: the 64 lanes of a wave hold 64 consecutive columns,
+// so per-column branches would run every case on every wave
 __device__ __forceinline__ float tes_value(uint4 a, uint4 b, int col) {
-  if (col >= 196) {
-    const bool black = (b.z >> 10) & 1u;
-    return (col == 196) != black ? 1.0f : 0.0f;
-  }
+  const bool black = (b.z >> 10) & 1u;
+  const float player = (col == 196) != black ? 1.0f : 0.0f;
   const int side = col >= 98 ? 1 : 0;
   const int cc = col - 98 * side;
-  if (cc == 96) return 0.0f;  // bar
-  if (cc == 97) return (float)(side ? ((b.z >> 4) & 15u) : (b.z & 15u)) / 15.0f;
-  const Nib c = side ? Nib{{a.z, a.w, b.y}} : Nib{{a.x, a.y, b.x}};
-  const uint32_t v = nib_get(c, cc >> 2);
-  switch (cc & 3) {
-    case 0: return v >= 1u ? 1.0f : 0.0f;
-    case 1: return v >= 2u ? 1.0f : 0.0f;
-    case 2: return v >= 3u ? 1.0f : 0.0f;
-    default: return v >= 3u ? (float)(v - 3u) / 2.0f : 0.0f;
-  }
+  const float offv = (float)(side ? ((b.z >> 4) & 15u) : (b.z & 15u)) / 15.0f;
+  const int pt = cc < 96 ? (cc >> 2) : 0;
+  const uint32_t w0 = side ? a.z : a.x, w1 = side ? a.w : a.y, w2 = side ? b.y : b.x;
+  const int k = pt >> 3;
+  const uint32_t word = k == 0 ? w0 : (k == 1 ? w1 : w2);
+  const uint32_t v = (word >> (4 * (pt & 7))) & 15u;
+  const int j = cc & 3;
+  const float thr = v >= (uint32_t)(j + 1) ? 1.0f : 0.0f;  // j = 0, 1, 2: v >= 1, 2, 3
+  const float over = v >= 3u ? (float)(v - 3u) / 2.0f : 0.0f;
+  const float board = j == 3 ? over : thr;
+  const float pv = cc == 96 ? 0.0f : (cc == 97 ? offv : board);
+  return col >= 196 ? player : pv;
 }
 
-__global__ void __launch_bounds__(kBlock) k_dqn_transition(TransArgs t) {
-  const uint32_t e = blockIdx.x * kBlock + threadIdx.x;  // n * 198 < 2^31 (checked on the host)
-  if (e >= (uint32_t)t.n * 198u) return;
-  const int i = (int)(e / 198u);
-  const int col = (int)(e - (uint32_t)i * 198u);
-  const uint4 a = t.pl.p0[i], b = t.pl.p1[i];
-  int64_t slot = *t.pos + i;  // pos < capacity and i < n <= capacity: one wrap at most
-  if (slot >= t.capacity) slot -= t.capacity;
-  const float nv = tes_value(a, b, col);
-  const float ov = t.state[e];
-  t.r_obs[slot * 198 + col] = ov;
-  t.r_next[slot * 198 + col] = nv;
-  t.state[e] = nv;
-  if (col != 0) return;
+// the env scalars of one transition (the thread holding column 0 of row i)
+__device__ __forceinline__ void trans_scalars(const TransArgs& t, int i, int64_t slot, uint4 b) {
   const float done = (t.term[i] | t.trunc[i]) ? 1.0f : 0.0f;
   float r = (float)t.reward[i];
   if (t.shaping) {
@@ -1020,6 +1011,69 @@ __global__ void __launch_bounds__(kBlock) k_dqn_transition(TransArgs t) {
   t.r_reward[slot] = r;
   t.r_done[slot] = done;
   t.r_prio[slot] = *t.max_prio;
+}
+
+// Each thread owns 4 consecutive floats of the flat (n, 198) arrays, so the
+// state load and the three row stores are 16 B per lane (1 KiB per wave
+// instruction; the two replay rows are written once and read only when
+// sampled: non-temporal).  That needs the ring rows pos .. pos + n - 1
+// contiguous and 16-B aligned (pos * 198 % 4 == 0, no wrap -- the steady
+// state when the capacity is a multiple of n); otherwise each float goes
+// on its own.
+__global__ void __launch_bounds__(kBlock) k_dqn_transition(TransArgs t) {
+  const uint32_t total = (uint32_t)t.n * 198u;  // n * 198 < 2^31 (checked on the host)
+  const uint32_t e0 = 4u * (blockIdx.x * kBlock + threadIdx.x);
+  if (e0 >= total) return;
+  const int64_t pos = *t.pos;  // pos < capacity and i < n <= capacity: one wrap at most
+  const bool vec = (pos * 198) % 4 == 0 && pos + t.n <= t.capacity && e0 + 4u <= total;
+  const int i0 = (int)(e0 / 198u);
+  const int c0 = (int)(e0 - (uint32_t)i0 * 198u);
+  const uint4 a0 = t.pl.p0[i0], b0 = t.pl.p1[i0];
+  // the 4 floats span rows i0 and (if c0 > 194) i0 + 1
+  const bool split = c0 > 194 && i0 + 1 < t.n;
+  uint4 a1 = a0, b1 = b0;
+  if (split) { a1 = t.pl.p0[i0 + 1]; b1 = t.pl.p1[i0 + 1]; }
+  float nv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = c0 + q;
+    nv[q] = c < 198 ? tes_value(a0, b0, c) : tes_value(a1, b1, c - 198);
+  }
+  if (vec) {
+    float4* st4 = reinterpret_cast<float4*>(t.state + e0);
+    const float4 ov = *st4;
+    const size_t d = (size_t)pos * 198 + e0;
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f o = {ov.x, ov.y, ov.z, ov.w};
+    const v4f nn = {nv[0], nv[1], nv[2], nv[3]};
+    __builtin_nontemporal_store(o, reinterpret_cast<v4f*>(t.r_obs + d));
+    __builtin_nontemporal_store(nn, reinterpret_cast<v4f*>(t.r_next + d));
+    *st4 = make_float4(nv[0], nv[1], nv[2], nv[3]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t e = e0 + (uint32_t)q;
+      if (e >= total) break;
+      const int i = (int)(e / 198u);
+      const int col = (int)(e - (uint32_t)i * 198u);
+      int64_t slot = pos + i;
+      if (slot >= t.capacity) slot -= t.capacity;
+      t.r_obs[slot * 198 + col] = t.state[e];
+      t.r_next[slot * 198 + col] = nv[q];
+      t.state[e] = nv[q];
+    }
+  }
+  // column 0 of a row lies in at most one thread's 4 floats
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t e = e0 + (uint32_t)q;
+    if (e >= total) break;
+    const int i = (int)(e / 198u);
+    if (e - (uint32_t)i * 198u != 0u) continue;
+    int64_t slot = pos + i;
+    if (slot >= t.capacity) slot -= t.capacity;
+    trans_scalars(t, i, slot, i == i0 ? b0 : b1);
+  }
 }
 
 __global__ void __launch_bounds__(kBlock) k_mask576(Planes pl, int n, Rng g,
@@ -1248,6 +1302,11 @@ bool valid_position(const int8_t* board, const uint8_t* off, const uint8_t* ft, 
 }
 
 }  // namespace
+
+namespace narde_abi {
+// the other translation units' (dqn_learner.hip) way into narde_last_error()
+int set_error(int code, const char* what) { return fail(code, "%s", what); }
+}  // namespace narde_abi
 
 extern "C" {
 
@@ -1522,8 +1581,8 @@ int narde_dqn_transition(narde_env* e, float* state, const int64_t* actions, con
   DeviceGuard dg(e->device);
   TransArgs t{e->pl, (int)e->n, shaping, state, actions, reward, terminated, truncated, off_seen,
               r_obs, r_next, r_action, r_reward, r_done, r_prio, max_prio, pos, capacity};
-  const int64_t total = e->n * 198;
-  k_dqn_transition<<<(unsigned)((total + kBlock - 1) / kBlock), kBlock, 0, (hipStream_t)stream>>>(t);
+  const int64_t quads = (e->n * 198 + 3) / 4;
+  k_dqn_transition<<<(unsigned)((quads + kBlock - 1) / kBlock), kBlock, 0, (hipStream_t)stream>>>(t);
   return check_launch("k_dqn_transition");
 }
 

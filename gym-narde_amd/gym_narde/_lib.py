@@ -54,6 +54,15 @@ SIGNATURES = {
                                                  _i64, _vp, _vp, _vp]),
     "narde_dqn_transition": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
                                     _vp, _vp, _i64, _vp]),
+    "narde_per_sample": (_i32, [_i32, _vp, _vp, _i64, _i64, _u64, _vp, _vp, ctypes.c_double, _vp, _vp, _vp,
+                                _vp, _vp]),
+    "narde_gather_batch": (_i32, [_i32, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  _vp]),
+    "narde_rowmax_addend": (_i32, [_i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp]),
+    "narde_dqn_loss": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, ctypes.c_float, _vp, _vp, _vp,
+                              _vp, _vp, _vp]),
+    "narde_prio_update": (_i32, [_i32, _vp, _vp, _i64, ctypes.c_float, _vp, _vp, _vp, ctypes.c_float,
+                                 ctypes.c_float, _vp]),
     "narde_violates_block_rule": (_i32, [_i32, _vp, _i64, _vp, _vp]),
     "narde_host_legal_moves": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "narde_host_step": (_i32, [_vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

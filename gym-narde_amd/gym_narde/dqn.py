@@ -124,6 +124,54 @@ def policy_576(q, mask576, epsilon, seed, tag, head, out=None, add=None):
     return out
 
 
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _f32(x):
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        raise ValueError("expected a contiguous float32 tensor")
+    return _lib.ptr(x)
+
+
+def rowmax_addend(base, tab, rows, out=None):
+    """max_c base[i][c] + tab[rows[i]][c] over the 576 codes (k_rowmax_addend):
+    the target move-2 head's max without the (B,576) sum."""
+    n = base.shape[0]
+    if base.stride(1) != 1 or tab.stride(1) != 1 or base.shape[1] != MOVES or tab.shape[1] != MOVES:
+        raise ValueError("base / tab must be (., 576) float32 with unit column stride")
+    rows = rows.to(torch.int64).contiguous()
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=base.device)
+    _lib.check(_lib.load().narde_rowmax_addend(
+        base.device.index, _lib.ptr(base), base.stride(0), _lib.ptr(tab), tab.stride(0), _lib.ptr(rows), n,
+        _lib.ptr(out), _stream(base.device)), "narde_rowmax_addend")
+    return out
+
+
+class DQNLoss(torch.autograd.Function):
+    """The decomposed loss of train_deepq_pytorch.py:653-720 as one kernel
+    (k_dqn_loss): forward returns the loss and writes the TD errors into
+    `td`; the saved dloss/dq1, dloss/dq2 make the backward one multiply."""
+
+    @staticmethod
+    def forward(ctx, q1, q2, m1, m2, r, d, w, gamma, td, loss_copy):
+        B = q1.shape[0]
+        loss = torch.empty((), dtype=torch.float32, device=q1.device)
+        g1, g2 = torch.empty_like(q1), torch.empty_like(q2)
+        _lib.check(_lib.load().narde_dqn_loss(
+            q1.device.index, _f32(q1), _f32(q2), _f32(m1), _f32(m2), _f32(r), _f32(d), _f32(w), B,
+            float(gamma), _f32(td), _lib.ptr(loss), None if loss_copy is None else _f32(loss_copy),
+            _lib.ptr(g1), _lib.ptr(g2), _stream(q1.device)), "narde_dqn_loss")
+        ctx.save_for_backward(g1, g2)
+        return loss
+
+    @staticmethod
+    def backward(ctx, go):
+        g1, g2 = ctx.saved_tensors
+        return go * g1, go * g2, None, None, None, None, None, None, None, None
+
+
 class DeviceReplay:
     """PrioritizedReplayBuffer (train_deepq_pytorch.py:279-342) on device
     tensors: new transitions get the running max priority, sampling is
@@ -149,6 +197,8 @@ class DeviceReplay:
         self.max_prio = torch.ones((), dtype=torch.float32, **z)
         self.beta_t = torch.full((), beta, dtype=torch.float64, **z)
         self.pos_t = torch.zeros((), dtype=torch.int64, **z)
+        self.sample_ctr = torch.zeros((), dtype=torch.int64, **z)  # k_per_sample's Philox counter
+        self._sample_scratch = torch.zeros(2, dtype=torch.int32, **z)  # its grid max + ticket
         self.pos = 0
         self.size = 0
 
@@ -194,6 +244,45 @@ class DeviceReplay:
         self.prio.index_copy_(0, idx, pr)
         torch.maximum(self.max_prio, pr.max(), out=self.max_prio)
 
+    # ---- fused (HIP) learner path: the same rules, one kernel each
+    def sample_fused(self, batch, seed, u_out=None):
+        """sample() as k_per_sample: priority^alpha and its prefix sum in
+        torch (rocPRIM scan), then the search, weights and beta step in one
+        kernel with its own device Philox counter (`sample_ctr`)."""
+        p = self.prio[: self.size] ** self.alpha
+        cdf = torch.cumsum(p, 0)
+        idx = torch.empty(batch, dtype=torch.int64, device=p.device)
+        w = torch.empty(batch, dtype=torch.float32, device=p.device)
+        _lib.check(_lib.load().narde_per_sample(
+            p.device.index, _lib.ptr(p), _lib.ptr(cdf), self.size, batch, int(seed) & (2 ** 64 - 1),
+            _lib.ptr(self.sample_ctr), _lib.ptr(self.beta_t), float(self.beta_increment), _lib.ptr(idx),
+            _lib.ptr(w), None if u_out is None else _f32(u_out), _lib.ptr(self._sample_scratch),
+            _stream(p.device)), "narde_per_sample")
+        return idx, w
+
+    def gather(self, idx):
+        """(s, ns, a, r, d) rows of idx (k_gather_batch)."""
+        B, ss = idx.shape[0], self.obs.shape[1]
+        z = dict(device=self.obs.device)
+        s = torch.empty((B, ss), dtype=torch.float32, **z)
+        ns = torch.empty((B, ss), dtype=torch.float32, **z)
+        a = torch.empty((B, 2), dtype=torch.int64, **z)
+        r = torch.empty(B, dtype=torch.float32, **z)
+        d = torch.empty(B, dtype=torch.float32, **z)
+        _lib.check(_lib.load().narde_gather_batch(
+            self.obs.device.index, _lib.ptr(idx), B, ss, _lib.ptr(self.obs), _lib.ptr(self.next_obs),
+            _lib.ptr(self.action), _lib.ptr(self.reward), _lib.ptr(self.done), _lib.ptr(s), _lib.ptr(ns),
+            _lib.ptr(a), _lib.ptr(r), _lib.ptr(d), _stream(self.obs.device)), "narde_gather_batch")
+        return s, ns, a, r, d
+
+    def update_fused(self, idx, td, epsilon=None, eps_min=0.0, eps_decay=1.0):
+        """update() as k_prio_update (+ the driver's epsilon decay when an
+        epsilon device scalar is given)."""
+        _lib.check(_lib.load().narde_prio_update(
+            idx.device.index, _lib.ptr(idx), _f32(td), idx.shape[0], float(self.epsilon), _lib.ptr(self.prio),
+            _lib.ptr(self.max_prio), None if epsilon is None else _lib.ptr(epsilon), float(eps_min),
+            float(eps_decay), _stream(idx.device)), "narde_prio_update")
+
 
 class BatchedDQNDriver:
     """B envs of DQN self-play on one GPU; one call of step() = one env step
@@ -235,6 +324,7 @@ class BatchedDQNDriver:
         # k_dqn_transition: observation + shaping + replay write in one kernel
         # (the 198-float observation only; the torch restatement otherwise)
         self.fused = bool(fused) and obs == "tesauro198"
+        self.fused_learner = bool(fused)
         self.seed = seed
         self.tag_t = torch.zeros((), dtype=torch.int64, **z)
         self.steps = 0
@@ -401,6 +491,42 @@ class BatchedDQNDriver:
     def _update_body(self):
         if self.replay.size < self.train_batch:
             return None
+        if self.fused_learner:
+            return self._update_fused()
+        return self._update_torch()
+
+    def _update_fused(self):
+        """_update_torch with the non-GEMM chains as HIP kernels
+        (csrc/dqn_learner.hip): sample, gather, target move-2 max, loss +
+        grads, priorities + epsilon.  ~40 fewer launches per update."""
+        rp = self.replay
+        idx, w = rp.sample_fused(self.train_batch, self.seed)
+        s, ns, a, r, d = rp.gather(idx)
+        f = self.model.features(s)
+        q1 = self.model.move1_head(f).gather(1, a[:, :1]).squeeze(1)
+        q2 = self.model.move2_from_features(f, a[:, 0]).gather(1, a[:, 1:]).squeeze(1)
+        with torch.no_grad():
+            tf = self.target.features(ns)
+            m1, am1 = self.target.move1_head(tf).max(1)
+            wt = self.target.move2_head.weight
+            base2 = torch.nn.functional.linear(tf, wt[:, :256], self.target.move2_head.bias)
+            m2 = rowmax_addend(base2, wt[:, 256:].t().contiguous(), am1)
+        td = torch.empty_like(r)
+        loss = DQNLoss.apply(q1, q2, m1, m2, r, d, w, self.gamma, td, self.loss_t)
+        self.opt.zero_grad(set_to_none=True)
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=10.0)
+        self.opt.step()
+        rp.update_fused(idx, td, self.eps_t, self.epsilon_min, self.epsilon_decay)
+        if self._capturing:
+            return self.loss_t
+        self._after_update()
+        return self.loss_t
+
+    def _update_torch(self):
+        """DQNAgent.replay (train_deepq_pytorch.py:602-750), decomposed
+        branch, in torch ops (the restatement the fused path is tested
+        against)."""
         idx, w = self.replay.sample(self.train_batch, generator=self.gen)
         s, ns = self.replay.obs[idx], self.replay.next_obs[idx]
         a, r, d = self.replay.action[idx], self.replay.reward[idx], self.replay.done[idx]

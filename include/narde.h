@@ -234,6 +234,49 @@ int narde_dqn_transition(narde_env *env, float *state, const int64_t *actions,
                          float *r_prio, const float *max_prio, const int64_t *pos,
                          int64_t capacity, void *stream);
 
+/* ---- DQN learner (gym-narde_amd/csrc/dqn_learner.hip; config 4) ---------
+ * The non-GEMM chains of train_deepq_pytorch.py's replay() (:602-750) and
+ * PrioritizedReplayBuffer (:279-342) at batch scale, fp32, each one kernel.
+ * Device scalars (counter i64, beta f64, max_prio / epsilon f32) are read
+ * and updated in place, so the calls can be captured in a graph. */
+
+/* Prioritized sample of `batch` rows from p f32[n] (priority^alpha) and its
+ * inclusive prefix sum cdf f32[n]: u_j = Philox4x32-10({*counter, j, 0, 7},
+ * seed) (24-bit uniform, written to u if non-NULL), idx_j = first k with
+ * cdf[k] > u_j * cdf[n-1] (clamped to n-1), w_j = (n p[idx_j] /
+ * cdf[n-1])^-beta / max_j; then beta = min(1, beta + beta_inc), counter += 1.
+ * scratch: u32[2] of zeros, left zeroed (the grid's max and finish ticket). */
+int narde_per_sample(int device, const float *p, const float *cdf, int64_t n, int64_t batch,
+                     uint64_t seed, int64_t *counter, double *beta, double beta_inc, int64_t *idx,
+                     float *w, float *u, uint32_t *scratch, void *stream);
+
+/* Minibatch rows idx i64[batch] of the replay ring: s/ns f32[batch][state_size]
+ * from obs/next_obs, a i64[batch][2], r/d f32[batch]. */
+int narde_gather_batch(int device, const int64_t *idx, int64_t batch, int state_size,
+                       const float *obs, const float *next_obs, const int64_t *action,
+                       const float *reward, const float *done, float *s, float *ns, int64_t *a,
+                       float *r, float *d, void *stream);
+
+/* out[i] = max_c base[i][c] + tab[rows[i]][c] over the 576 codes (the target
+ * move-2 head's max with its one-hot column added on the fly). */
+int narde_rowmax_addend(int device, const float *base, int64_t ld, const float *tab,
+                        int64_t ld_tab, const int64_t *rows, int64_t n, float *out, void *stream);
+
+/* The decomposed DQN loss (train_deepq_pytorch.py:653-720) on batch rows:
+ * t = r + (1 - d) * gamma * m (m1/m2 the target heads' maxima), td =
+ * clamp(|t1 - q1| + |t2 - q2|, 0, 100), *loss = mean(w (q1 - t1)^2) +
+ * mean(w (q2 - t2)^2) (also to *loss_copy if non-NULL), g1/g2 = dloss/dq1,
+ * dloss/dq2. */
+int narde_dqn_loss(int device, const float *q1, const float *q2, const float *m1, const float *m2,
+                   const float *r, const float *d, const float *w, int64_t batch, float gamma,
+                   float *td, float *loss, float *loss_copy, float *g1, float *g2, void *stream);
+
+/* prio[idx_j] = td_j + eps; *max_prio = max(*max_prio, max_j); then, if
+ * epsilon is non-NULL, *epsilon *= eps_decay when *epsilon > eps_min. */
+int narde_prio_update(int device, const int64_t *idx, const float *td, int64_t batch, float eps,
+                      float *prio, float *max_prio, float *epsilon, float eps_min,
+                      float eps_decay, void *stream);
+
 /* Stateless: Narde._violates_block_rule on n perspective boards i8[n][24]. */
 int narde_violates_block_rule(int device, const int8_t *boards, int64_t n, uint8_t *out,
                               void *stream);

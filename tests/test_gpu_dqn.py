@@ -182,8 +182,8 @@ def test_policy_kernel_device_scalars_and_fused_addend():
     assert torch.equal(got, masked_argmax(q + tab[rows], m))
 
 
-@pytest.mark.parametrize("shaping", [True, False])
-def test_fused_transition_matches_torch_restatement(shaping):
+@pytest.mark.parametrize("shaping,pos", [(True, "wrap"), (False, "wrap"), (True, "aligned")])
+def test_fused_transition_matches_torch_restatement(shaping, pos):
     """k_dqn_transition (observation + reward shaping + replay write + s <- s')
     is bit-exact against the driver's torch restatement on the same step,
     including a replay-ring wrap and games that end in the step."""
@@ -199,7 +199,8 @@ def test_fused_transition_matches_torch_restatement(shaping):
     off0 = torch.randint(0, 16, (n, 2), device="cuda:0", generator=g).float()
     state0 = drv.state.clone()
     rp = drv.replay
-    rp.pos_t.fill_(3 * n - 100)
+    p0 = 3 * n - 100 if pos == "wrap" else n  # ring wrap (per-float path) / 16-B rows (vector path)
+    rp.pos_t.fill_(p0)
     rp.max_prio.fill_(2.5)
     a = drv.act(drv.state)
     _, reward, term, trunc, _ = env.step(a.to(torch.int16))
@@ -211,7 +212,7 @@ def test_fused_transition_matches_torch_restatement(shaping):
         drv.off_seen.copy_(off0)
         for t in (rp.obs, rp.next_obs, rp.action, rp.reward, rp.done, rp.prio):
             t.zero_()
-        rp.pos_t.fill_(3 * n - 100)
+        rp.pos_t.fill_(p0)
         fn()
         return [t.clone() for t in (drv.state, drv.off_seen, rp.obs, rp.next_obs, rp.action, rp.reward,
                                     rp.done, rp.prio, rp.pos_t)]
@@ -221,5 +222,146 @@ def test_fused_transition_matches_torch_restatement(shaping):
     names = ["state", "off_seen", "obs", "next_obs", "action", "reward", "done", "prio", "pos"]
     for nm, x, y in zip(names, fused, ref):
         assert torch.equal(x, y), nm
-    # the wrap really happened: rows at both ends of the ring were written
-    assert float(ref[7][0]) == 2.5 and float(ref[7][3 * n - 1]) == 2.5
+    if pos == "wrap":  # rows at both ends of the ring were written
+        assert float(ref[7][0]) == 2.5 and float(ref[7][3 * n - 1]) == 2.5
+    else:
+        assert float(ref[7][n]) == 2.5 and float(ref[7][2 * n - 1]) == 2.5 and float(ref[7][2 * n]) == 0.0
+
+
+# ------------------------------------------------ fused learner kernels
+def test_per_sample_kernel_vs_torch():
+    """k_per_sample: for its own uniforms u, idx == torch.searchsorted(cdf,
+    u * total, right=True) clamped, weights == (N p[idx] / total)^-beta / max
+    (fp32, 1 ulp of powf), beta annealed and the counter advanced."""
+    from gym_narde.dqn import DeviceReplay
+
+    n, B = 300000, 4096
+    rp = DeviceReplay(n, 4, "cuda:0")
+    g = torch.Generator(device="cuda:0").manual_seed(3)
+    rp.prio.copy_(torch.rand(n, device="cuda:0", generator=g) * 3 + 0.01)
+    rp.prio[:1000] = 50.0  # a heavy head
+    rp.size = n
+    u = torch.empty(B, device="cuda:0")
+    beta0 = float(rp.beta_t)
+    idx, w = rp.sample_fused(B, seed=11, u_out=u)
+    p = rp.prio ** rp.alpha
+    cdf = torch.cumsum(p, 0)
+    total = cdf[-1]
+    want = torch.searchsorted(cdf, u * total, right=True).clamp_(max=n - 1)
+    assert torch.equal(idx, want)
+    x = (n * (p[want] / total)) ** (-beta0)
+    assert torch.allclose(w, x / x.max(), rtol=2e-6, atol=0)
+    assert float(rp.beta_t) == pytest.approx(beta0 + rp.beta_increment)
+    assert int(rp.sample_ctr) == 1
+    idx2, _ = rp.sample_fused(B, seed=11)
+    assert not torch.equal(idx, idx2)  # a new counter, new draws
+    # proportional to priority^alpha over many draws
+    counts = torch.zeros(n, device="cuda:0")
+    for _ in range(20):
+        i, _ = rp.sample_fused(B, seed=11)
+        counts += torch.bincount(i, minlength=n).float()
+    head = float(counts[:1000].sum() / counts.sum())
+    assert head == pytest.approx(float(p[:1000].sum() / total), rel=0.05)
+
+
+def test_gather_batch_and_rowmax_addend_exact():
+    from gym_narde.dqn import DeviceReplay, rowmax_addend
+
+    rp = DeviceReplay(5000, 198, "cuda:0")
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    for t in (rp.obs, rp.next_obs, rp.reward, rp.done):
+        t.copy_(torch.rand(t.shape, device="cuda:0", generator=g))
+    rp.action.copy_(torch.randint(0, 576, rp.action.shape, device="cuda:0", generator=g))
+    idx = torch.randint(0, 5000, (4096,), device="cuda:0", generator=g)
+    s, ns, a, r, d = rp.gather(idx)
+    for got, src in ((s, rp.obs), (ns, rp.next_obs), (a, rp.action), (r, rp.reward), (d, rp.done)):
+        assert torch.equal(got, src[idx])
+    base = torch.randn((4096, 576), device="cuda:0", generator=g)
+    tab = torch.randn((576, 576), device="cuda:0", generator=g)
+    rows = torch.randint(0, 576, (4096,), device="cuda:0", generator=g)
+    assert torch.equal(rowmax_addend(base, tab, rows), (base + tab[rows]).max(1).values)
+
+
+def test_dqn_loss_kernel_vs_torch_autograd():
+    """k_dqn_loss: TD errors and dloss/dq bit-exact against torch's autograd
+    of the reference loss (batch a power of two), the loss to fp32 summation
+    order."""
+    from gym_narde.dqn import DQNLoss
+
+    B, gamma = 4096, 0.99
+    g = torch.Generator(device="cuda:0").manual_seed(9)
+    rnd = lambda: torch.randn(B, device="cuda:0", generator=g)  # noqa: E731
+    q1, q2, m1, m2 = rnd(), rnd(), rnd(), rnd()
+    r = (torch.rand(B, device="cuda:0", generator=g) < 0.1).float() * 2
+    d = (torch.rand(B, device="cuda:0", generator=g) < 0.2).float()
+    w = torch.rand(B, device="cuda:0", generator=g)
+    q1r, q2r = q1.clone().requires_grad_(), q2.clone().requires_grad_()
+    t1 = r + (1 - d) * gamma * m1
+    t2 = r + (1 - d) * gamma * m2
+    td_ref = torch.clamp((t1 - q1r).abs() + (t2 - q2r).abs(), 0.0, 100.0).detach()
+    loss_ref = (w * (q1r - t1) ** 2).mean() + (w * (q2r - t2) ** 2).mean()
+    loss_ref.backward()
+    q1f, q2f = q1.clone().requires_grad_(), q2.clone().requires_grad_()
+    td = torch.empty(B, device="cuda:0")
+    copy = torch.zeros((), device="cuda:0")
+    loss = DQNLoss.apply(q1f, q2f, m1, m2, r, d, w, gamma, td, copy)
+    loss.backward()
+    assert torch.equal(td, td_ref)
+    assert torch.equal(q1f.grad, q1r.grad) and torch.equal(q2f.grad, q2r.grad)
+    assert float(loss.detach()) == pytest.approx(float(loss_ref.detach()), rel=1e-6)
+    assert float(copy) == float(loss)
+
+
+def test_prio_update_kernel_exact():
+    from gym_narde.dqn import DeviceReplay
+
+    rp = DeviceReplay(10000, 4, "cuda:0")
+    g = torch.Generator(device="cuda:0").manual_seed(2)
+    idx = torch.randperm(10000, device="cuda:0", generator=g)[:4096]
+    td = torch.rand(4096, device="cuda:0", generator=g) * 7
+    eps = torch.full((), 0.5, device="cuda:0")
+    rp.update_fused(idx, td, eps, 0.01, 0.995)
+    pr = td + rp.epsilon
+    assert torch.equal(rp.prio[idx], pr)
+    assert float(rp.max_prio) == float(torch.maximum(torch.ones((), device="cuda:0"), pr.max()))
+    want = torch.where(torch.full((), 0.5, device="cuda:0") > 0.01,
+                       torch.full((), 0.5, device="cuda:0") * 0.995, torch.full((), 0.5, device="cuda:0"))
+    assert float(eps) == float(want)
+
+
+def test_fused_and_torch_learners_agree_on_one_update():
+    """One update from the same state: the fused learner (its own sampler)
+    and the torch restatement given the fused learner's minibatch produce
+    the same loss and parameters to fp32 rounding."""
+    from gym_narde.dqn import BatchedDQNDriver
+    from gym_narde.vector import VecNardeEnv
+
+    env = VecNardeEnv(4096, device="cuda:0", seed=41)
+    drv = BatchedDQNDriver(env, capacity=1 << 14, train_batch=1024, seed=3)
+    for _ in range(5):
+        drv.step()
+    torch.cuda.synchronize()
+    rp = drv.replay
+    state = {k: v.clone() for k, v in drv.model.state_dict().items()}
+    sample_state = (rp.sample_ctr.clone(), rp.beta_t.clone(), rp.prio.clone())
+    loss_f = drv._update_fused().clone()
+    after_f = {k: v.clone() for k, v in drv.model.state_dict().items()}
+    assert torch.isfinite(loss_f)
+    assert any(not torch.equal(state[k], after_f[k]) for k in state)
+    # the fused minibatch, replayed through torch ops on a copy of the model
+    rp.sample_ctr.copy_(sample_state[0]); rp.beta_t.copy_(sample_state[1]); rp.prio.copy_(sample_state[2])
+    idx, w = rp.sample_fused(drv.train_batch, drv.seed)
+    s, ns, a, r, d = (rp.obs[idx], rp.next_obs[idx], rp.action[idx], rp.reward[idx], rp.done[idx])
+    import copy as _copy
+    model = _copy.deepcopy(drv.model)
+    model.load_state_dict(state)
+    f = model.features(s)
+    q1 = model.move1_head(f).gather(1, a[:, :1]).squeeze(1)
+    q2 = model.move2_from_features(f, a[:, 0]).gather(1, a[:, 1:]).squeeze(1)
+    with torch.no_grad():
+        tf = drv.target.features(ns)
+        nq1 = drv.target.move1_head(tf)
+        t1 = r + (1 - d) * drv.gamma * nq1.max(1)[0]
+        t2 = r + (1 - d) * drv.gamma * drv.target.move2_from_features(tf, nq1.argmax(1)).max(1)[0]
+    loss_t = (w * (q1 - t1) ** 2).mean() + (w * (q2 - t2) ** 2).mean()
+    assert float(loss_f) == pytest.approx(float(loss_t), rel=1e-5)
