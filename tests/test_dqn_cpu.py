@@ -94,3 +94,13 @@ def test_replay_priority_rules():
     # new transitions get the running max priority
     r.add(obs[:1], torch.zeros(1, 2, dtype=torch.int64), torch.ones(1), obs[:1], torch.zeros(1))
     assert float(r.prio[2]) == pytest.approx(5.01)
+
+
+def test_features_nograd_matches_module():
+    from gym_narde.dqn import DecomposedDQN
+
+    torch.manual_seed(0)
+    m = DecomposedDQN(198)
+    x = torch.randn(64, 198)
+    with torch.no_grad():
+        assert torch.allclose(m.features_nograd(x), m.features(x), rtol=1e-6, atol=1e-6)
