@@ -319,7 +319,11 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   // not fast: a chain bound >= 7 still keeps every first sub-move (one
   // sub-move lowers it by <= 4) with M = 4
   const int cb0 = (dbl && bf && !fast) ? f4_chain_bound(s.O, s.S1o, s.P, dh, hl0) : 0;
-  const bool srch = dbl && !fast && Lh != 0u && cb0 < 7;
+  // block-free with bear-off fixed: M exactly from the chains and every
+  // C_k = L_k (f4_exact_moves) -- ~3/4 of the doubles turns the bounds miss
+  const bool exact = dbl && bf && !fast && cb0 < 7 && Lh != 0u && f4_bearoff_fixed(s);
+  const int Mx = exact ? f4_exact_moves(s, dh, hl0) : 0;
+  const bool srch = dbl && !fast && Lh != 0u && cb0 < 7 && !exact;
   // one cooperative pass for every lane's first-sub-move checks
   uint32_t r0[3];
   {
@@ -349,6 +353,7 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
     Cl = 0u;
     if (fast || (cb0 >= 7 && Lh)) { Ch = Lh; M = 4; }
     else if (!Lh) { Ch = 0u; M = 0; }
+    else if (exact) { Ch = Lh; M = Mx; }
     else if (r0[2]) { Ch = r0[2]; M = 4; }  // some source leaves 3 more
     else if (r0[1]) { Ch = r0[1]; M = 3; }
     else if (r0[0]) { Ch = r0[0]; M = 2; }
@@ -387,7 +392,7 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
     uint32_t Lk = act ? legal1(s, low, dk, bf) : 0u;
     if (hl <= 0) Lk &= ~HEAD;
     const int need = M - k - 1;
-    const bool direct = !dbl || fast || need <= 0 ||
+    const bool direct = !dbl || fast || exact || need <= 0 ||
                         (act && bf && f4_chain_bound(s.O, s.S1o, s.P, dk, hl) >= need + 4);
     uint32_t rk[3];
 #if NARDE_DIAG_ABLATE & 2

@@ -658,6 +658,65 @@ NARDE_FN int f4_chain_bound(uint32_t O, uint32_t S1, uint32_t P, int d, int hl) 
   return lb;
 }
 
+// own points holding >= 3 / >= 4 checkers (24-bit masks from the nibbles)
+NARDE_FN uint32_t nib_ge3_ge4(const Nib& b, uint32_t& ge4) {
+  uint32_t m3 = 0u, m4 = 0u;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const uint32_t w = b.w[k];
+    const uint32_t hi = ((w >> 2) | (w >> 3)) & 0x11111111u;  // v >= 4
+    const uint32_t lo = w & (w >> 1) & 0x11111111u;          // bits 0 and 1 set
+    m4 |= compact4(hi) << (8 * k);
+    m3 |= compact4(hi | lo) << (8 * k);
+  }
+  ge4 = m4;
+  return m3;
+}
+
+// Can bear-off change during a doubles turn?  Not if every own checker is
+// home already (it stays allowed) or at least 4 are outside (each sub-move
+// brings at most one home: after k sub-moves >= 4 - k are still out, so no
+// bear-off before the turn ends).
+NARDE_FN bool f4_bearoff_fixed(const Side& s) {
+  if ((s.O >> 6) == 0u) return true;
+  uint32_t x = s.own.w[0] & 0xFFFFFFu;  // points 0..5
+  x = (x & 0x0F0F0Fu) + ((x >> 4) & 0x0F0F0Fu);
+  const uint32_t home = ((x * 0x010101u) >> 16) & 0xFFu;
+  return 15u - s.off_own - home >= 4u;
+}
+
+// Exact sub-move count of a block-free doubles turn whose bear-off status
+// is fixed (f4_bearoff_fixed): each checker walks its own chain of die-d
+// steps (free landings, and a final bear-off when all are home), chains of
+// different checkers never interact, and only hl checkers may leave the
+// head.  So M = min(4, sum over checkers of their chain lengths), and any
+// legal sub-move lowers that sum by exactly one: every C_k = L_k.
+NARDE_FN int f4_exact_moves(const Side& s, int d, int hl) {
+  const uint32_t O = s.O, P = s.P;
+  const uint32_t gn = (~P << d) & (MASK24 << d) & MASK24;       // y: y - d on the board, free
+  const uint32_t go = ((O >> 6) == 0u) ? ((1u << d) - 1u) : 0u;  // y: bears off
+  const uint32_t a = gn | go;
+  const uint32_t keep = hl > 0 ? O : (O & ~HEAD);
+  const uint32_t g1 = gn & (gn << d), g2 = g1 & (gn << (2 * d));
+  const uint32_t c1 = keep & a;                   // chain >= 1
+  const uint32_t c2 = keep & gn & (a << d);       // >= 2
+  const uint32_t c3 = keep & g1 & (a << (2 * d)); // >= 3
+  const uint32_t c4 = keep & g2 & (a << (3 * d)); // >= 4
+  uint32_t ge4;
+  const uint32_t ge3 = nib_ge3_ge4(s.own, ge4) & ~HEAD;
+  ge4 &= ~HEAD;
+  const uint32_t ge1 = O & ~HEAD, ge2 = O & ~s.S1o & ~HEAD;
+  int t = 0;
+  const uint32_t cs[4] = {c1, c2, c3, c4};
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    t += __builtin_popcount(cs[j] & ge1) + __builtin_popcount(cs[j] & ge2) + __builtin_popcount(cs[j] & ge3) +
+         __builtin_popcount(cs[j] & ge4);
+  const int hm = (hl >= 2 && !(s.S1o & HEAD)) ? 2 : 1;  // head leavers (keep drops the head at hl <= 0)
+  t += hm * (int)(((c1 >> 23) & 1u) + ((c2 >> 23) & 1u) + ((c3 >> 23) & 1u) + ((c4 >> 23) & 1u));
+  return t < 4 ? t : 4;
+}
+
 // the sources of L (die d) after which NEED more sub-moves stay playable:
 // block-free turns try the lower bound first, the exact search only where
 // it falls short
@@ -811,9 +870,14 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, con
     // block-free with a lower bound of >= 4 sub-moves: M = 4, and as each
     // sub-move lowers the bound by at most one, every C_k = L_k (no search)
     const bool fast = bf && f4_lower_bound(s.O, s.S1o, s.P, d, hl) >= 4;
+    // block-free with bear-off fixed: M exactly from the chains, every C_k = L_k
+    const bool exact = !fast && bf && f4_bearoff_fixed(s);
     if (fast) {
       C = L;
       M = 4;
+    } else if (exact) {
+      C = L;
+      M = L ? f4_exact_moves(s, d, hl) : 0;
     } else if (L) {
       C = f4_keep<3>(s, low, d, hl, L, bf);
       M = 4;
@@ -826,7 +890,7 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, con
       if (k > 0) {
         L = legal1(s, low, d, bf);
         if (hl <= 0) L &= ~HEAD;
-        C = fast ? L : f4_keep_rt(s, low, d, hl, fast ? 0u : L, M - k - 1, bf);
+        C = (fast || exact) ? L : f4_keep_rt(s, low, d, hl, L, M - k - 1, bf);
       }
       int p;
       if (play) {

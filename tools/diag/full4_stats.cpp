@@ -1,0 +1,98 @@
+// DIAGNOSTIC (host): how FULL4 doubles turns of random self-play split over
+// the device turn's shortcuts -- which ones still need a search.
+//   hipcc -O2 -std=c++17 -o /tmp/full4_stats tools/diag/full4_stats.cpp && /tmp/full4_stats
+#include <cstdio>
+
+#include "../../gym-narde_amd/csrc/narde_rules.h"
+
+using namespace narde;
+
+// exact own-checker count per point class: counts >= j masks
+static uint32_t ge_mask(const Nib& b, uint32_t j) {
+  uint32_t m = 0;
+  for (int p = 0; p < 24; ++p) m |= (nib_get(b, p) >= j ? 1u : 0u) << p;
+  return m;
+}
+
+// sum over checkers of their chain length (block-free, no bear-off change)
+static int chain_total(const Side& s, int d, int hl) {
+  int tot = 0;
+  for (int p = 0; p < 24; ++p) {
+    int c = nib_get(s.own, p);
+    if (!c) continue;
+    int ch = 0;
+    for (int q = p - d; ch < 4; q -= d) {
+      if (q < 0) {
+        if ((s.O >> 6) == 0u) ++ch;  // bears off: only if all home already
+        break;
+      }
+      if ((s.P >> q) & 1u) break;
+      ++ch;
+    }
+    if (p == 23) c = c < hl ? c : hl;
+    tot += c * ch;
+  }
+  return tot;
+}
+
+int main() {
+  const int n = 4096, plies = 400;
+  long dbl = 0, fast = 0, cb7 = 0, searched = 0, s_bf = 0, s_exact = 0, s_exact4 = 0, nobf = 0;
+  long bad_fixed = 0, bad_exact = 0;
+  for (int e = 0; e < n; ++e) {
+    Side s = side_start(e & 1);
+    s.t = 0;
+    int4 st = make_int4(0, 0, 0, 0);
+    for (int p = 0; p < plies; ++p) {
+      uint32_t R[4], r[4];
+      ply_block(s.t, (uint32_t)e, 1u, 2u, R);
+      ply_words_of(R, s.t, 0, r);
+      int d0, d1;
+      dice_from(r[0], 0, d0, d1);
+      if (d0 == d1) {
+        ++dbl;
+        const uint32_t low = block_lowmask(s.P);
+        const bool bf = turn_block_free(s.O, s.P, low, d0, d0);
+        const int hl0 = (s.ft_own && (d0 == 3 || d0 == 4 || d0 == 6)) ? 2 : 1;
+        const bool f = bf && f4_lower_bound(s.O, s.S1o, s.P, d0, hl0) >= 4;
+        const int cb0 = (bf && !f) ? f4_chain_bound(s.O, s.S1o, s.P, d0, hl0) : 0;
+        const uint32_t L = legal1(s, low, d0, bf);
+        if (!bf) ++nobf;
+        if (f) ++fast;
+        else if (cb0 >= 7 && L) ++cb7;
+        else if (L) {
+          ++searched;
+          if (bf) {
+            ++s_bf;
+            // outside-home checkers (points >= 6)
+            int outside = 0;
+            for (int q = 6; q < 24; ++q) outside += nib_get(s.own, q);
+            const bool nob = (s.O >> 6) == 0u || outside >= 4;
+            if (nob != f4_bearoff_fixed(s)) ++bad_fixed;
+            if (nob) {
+              ++s_exact;
+              const int T = chain_total(s, d0, hl0);
+              if (T >= 4) ++s_exact4;
+              // the search's M and C_0 against the exact count
+              uint32_t C = f4_keep<3>(s, low, d0, hl0, L, bf);
+              int M = 4;
+              if (!C) { C = f4_keep<2>(s, low, d0, hl0, L, bf); M = 3; }
+              if (!C) { C = f4_keep<1>(s, low, d0, hl0, L, bf); M = 2; }
+              if (!C) { C = L; M = 1; }
+              const int Me = f4_exact_moves(s, d0, hl0);
+              if (Me != M || C != L || (T < 4 ? T : 4) != Me) ++bad_exact;
+            }
+          }
+        }
+      }
+      TurnOut o;
+      int tm, tr;
+      env_ply_full(s, st, r, (uint32_t)e, 1u, 2u, false, 0, 0, 0, false, 0ull, 1000, true, o, tm, tr);
+    }
+  }
+  printf("doubles turns %ld: fast %ld, chain>=7 %ld, searched %ld (non-bf lanes overall %ld)\n", dbl, fast, cb7,
+         searched, nobf);
+  printf("searched & block-free %ld: exact-chain applicable %ld, of which total>=4 %ld\n", s_bf, s_exact, s_exact4);
+  printf("mismatches: bearoff_fixed %ld, exact M/C vs search %ld\n", bad_fixed, bad_exact);
+  return 0;
+}
