@@ -393,7 +393,8 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
     if (hl <= 0) Lk &= ~HEAD;
     const int need = M - k - 1;
     const bool direct = !dbl || fast || exact || need <= 0 ||
-                        (act && bf && f4_chain_bound(s.O, s.S1o, s.P, dk, hl) >= need + 4);
+                        (act && bf && (f4_bearoff_fixed(s, need + 1) ||
+                                       f4_chain_bound(s.O, s.S1o, s.P, dk, hl) >= need + 4));
     uint32_t rk[3];
 #if NARDE_DIAG_ABLATE & 2
     rk[0] = rk[1] = rk[2] = Lk;

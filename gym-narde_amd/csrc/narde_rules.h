@@ -673,16 +673,16 @@ NARDE_FN uint32_t nib_ge3_ge4(const Nib& b, uint32_t& ge4) {
   return m3;
 }
 
-// Can bear-off change during a doubles turn?  Not if every own checker is
-// home already (it stays allowed) or at least 4 are outside (each sub-move
-// brings at most one home: after k sub-moves >= 4 - k are still out, so no
-// bear-off before the turn ends).
-NARDE_FN bool f4_bearoff_fixed(const Side& s) {
+// Can bear-off change within the next `rem` sub-moves of a doubles turn?
+// Not if every own checker is home already (it stays allowed) or at least
+// rem are outside (each sub-move brings at most one home, so one stays out
+// until the last of them).
+NARDE_FN bool f4_bearoff_fixed(const Side& s, int rem = 4) {
   if ((s.O >> 6) == 0u) return true;
   uint32_t x = s.own.w[0] & 0xFFFFFFu;  // points 0..5
   x = (x & 0x0F0F0Fu) + ((x >> 4) & 0x0F0F0Fu);
   const uint32_t home = ((x * 0x010101u) >> 16) & 0xFFu;
-  return 15u - s.off_own - home >= 4u;
+  return (int)(15u - s.off_own - home) >= rem;
 }
 
 // Exact sub-move count of a block-free doubles turn whose bear-off status
@@ -890,7 +890,10 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, con
       if (k > 0) {
         L = legal1(s, low, d, bf);
         if (hl <= 0) L &= ~HEAD;
-        C = (fast || exact) ? L : f4_keep_rt(s, low, d, hl, L, M - k - 1, bf);
+        // block-free with bear-off fixed for the rest of the turn: every
+        // legal sub-move lowers the exact chain count by one (f4_exact_moves)
+        const bool direct = fast || exact || (bf && f4_bearoff_fixed(s, M - k));
+        C = direct ? L : f4_keep_rt(s, low, d, hl, L, M - k - 1, bf);
       }
       int p;
       if (play) {

@@ -38,7 +38,7 @@ static int chain_total(const Side& s, int d, int hl) {
 int main() {
   const int n = 4096, plies = 400;
   long dbl = 0, fast = 0, cb7 = 0, searched = 0, s_bf = 0, s_exact = 0, s_exact4 = 0, nobf = 0;
-  long bad_fixed = 0, bad_exact = 0;
+  long bad_fixed = 0, bad_exact = 0, two = 0, pair_tasks = 0, pair_nobf = 0, pair_n = 0;
   for (int e = 0; e < n; ++e) {
     Side s = side_start(e & 1);
     s.t = 0;
@@ -49,6 +49,20 @@ int main() {
       ply_words_of(R, s.t, 0, r);
       int d0, d1;
       dice_from(r[0], 0, d0, d1);
+      if (d0 != d1) {
+        ++two;
+        const uint32_t low = block_lowmask(s.P);
+        const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
+        const bool bf = turn_block_free(s.O, s.P, low, dh, dl);
+        const uint32_t Lh = legal1(s, low, dh, bf), Ll = legal1(s, low, dl, bf);
+        const bool all_h = bf && f4_lower_bound(s.O, s.S1o, s.P, dl, 1) >= 2;
+        const bool all_l = bf && f4_lower_bound(s.O, s.S1o, s.P, dh, 1) >= 2;
+        if ((!all_h && Lh) || (!all_l && Ll)) {
+          ++pair_tasks;
+          if (!bf) ++pair_nobf;
+          pair_n += (!all_h ? __builtin_popcount(Lh) : 0) + (!all_l ? __builtin_popcount(Ll) : 0);
+        }
+      }
       if (d0 == d1) {
         ++dbl;
         const uint32_t low = block_lowmask(s.P);
@@ -93,6 +107,7 @@ int main() {
   printf("doubles turns %ld: fast %ld, chain>=7 %ld, searched %ld (non-bf lanes overall %ld)\n", dbl, fast, cb7,
          searched, nobf);
   printf("searched & block-free %ld: exact-chain applicable %ld, of which total>=4 %ld\n", s_bf, s_exact, s_exact4);
+  printf("two-dice turns %ld: needing pair checks %ld (non-bf %ld), tasks %ld\n", two, pair_tasks, pair_nobf, pair_n);
   printf("mismatches: bearoff_fixed %ld, exact M/C vs search %ld\n", bad_fixed, bad_exact);
   return 0;
 }
