@@ -728,7 +728,11 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Planes pl, int n, Rng g, int
 constexpr int kPcEnvs = 256;                  // envs per workgroup
 constexpr int kPcSets = NARDE_PC_SETS;        // consumer waves per producer wave
 constexpr int kPcThreads = (1 + kPcSets) * kPcEnvs;  // producers + consumers
-constexpr int kPcR = 4;                       // plies per barrier block
+// plies per barrier block (tuning knob: 3, 4 and 5 time the same)
+#ifndef NARDE_PC_R
+#define NARDE_PC_R 4
+#endif
+constexpr int kPcR = NARDE_PC_R;                       // plies per barrier block
 
 struct PcLds {
   uint2 draw[2][kPcR][kPcEnvs];               // the ply's (wa, wb) per env and ply

@@ -7,6 +7,23 @@
 
 using namespace narde;
 
+// windows i..i+5 (bit i) with at most 2 points missing from O (bit-sliced
+// count of the holes over the 6 shifted masks)
+static uint32_t windows_le2_holes(uint32_t O) {
+  const uint32_t h = ~O & MASK24;
+  uint32_t s0 = 0, s1 = 0, s2 = 0;  // 3-bit counter per window start
+  for (int k = 0; k < 6; ++k) {
+    const uint32_t x = (h >> k);
+    const uint32_t c0 = s0 & x;
+    s0 ^= x;
+    const uint32_t c1 = s1 & c0;
+    s1 ^= c0;
+    s2 |= c1;
+  }
+  // count <= 2: s2 == 0 and not (s1 && s0)
+  return ~s2 & ~(s1 & s0) & MASK24;
+}
+
 // exact own-checker count per point class: counts >= j masks
 static uint32_t ge_mask(const Nib& b, uint32_t j) {
   uint32_t m = 0;
@@ -38,7 +55,7 @@ static int chain_total(const Side& s, int d, int hl) {
 int main() {
   const int n = 4096, plies = 400;
   long dbl = 0, fast = 0, cb7 = 0, searched = 0, s_bf = 0, s_exact = 0, s_exact4 = 0, nobf = 0;
-  long bad_fixed = 0, bad_exact = 0, two = 0, pair_tasks = 0, pair_nobf = 0, pair_n = 0;
+  long nobf2_all = 0, nobf_but_bf2 = 0, bad_fixed = 0, bad_exact = 0, two = 0, pair_tasks = 0, pair_nobf = 0, pair_n = 0;
   for (int e = 0; e < n; ++e) {
     Side s = side_start(e & 1);
     s.t = 0;
@@ -57,6 +74,13 @@ int main() {
         const uint32_t Lh = legal1(s, low, dh, bf), Ll = legal1(s, low, dl, bf);
         const bool all_h = bf && f4_lower_bound(s.O, s.S1o, s.P, dl, 1) >= 2;
         const bool all_l = bf && f4_lower_bound(s.O, s.S1o, s.P, dh, 1) >= 2;
+        if (!bf) {
+          ++nobf2_all;
+          const uint32_t A = s.O | land_step(s.O, s.P, dh) | land_step(s.O, s.P, dl);
+          const uint32_t U = A | land_step(A, s.P, dh) | land_step(A, s.P, dl);
+          const bool bf2 = (runs6(U) & low & windows_le2_holes(s.O)) == 0u;
+          if (bf2) ++nobf_but_bf2;
+        }
         if ((!all_h && Lh) || (!all_l && Ll)) {
           ++pair_tasks;
           if (!bf) ++pair_nobf;
@@ -108,6 +132,7 @@ int main() {
          searched, nobf);
   printf("searched & block-free %ld: exact-chain applicable %ld, of which total>=4 %ld\n", s_bf, s_exact, s_exact4);
   printf("two-dice turns %ld: needing pair checks %ld (non-bf %ld), tasks %ld\n", two, pair_tasks, pair_nobf, pair_n);
+  printf("two-dice non-bf %ld, of which block-free by the 2-hole window test %ld\n", nobf2_all, nobf_but_bf2);
   printf("mismatches: bearoff_fixed %ld, exact M/C vs search %ld\n", bad_fixed, bad_exact);
   return 0;
 }
