@@ -1,0 +1,64 @@
+// device_common.h -- env planes, launch shape and the device RNG draws
+// Part of the one translation unit narde.hip (included there, in order);
+// not a standalone header.
+#pragma once
+
+// ---- build knobs (-D...; the defaults are the product build) -------------
+// REF2 rollout kernel: 1 = producer/consumer k_rollout_pc, 0 = one wave per
+// 64 envs (k_rollout; A/B diagnostic builds only)
+#ifndef NARDE_ROLLOUT_PC
+#define NARDE_ROLLOUT_PC 1
+#endif
+
+// Output store strategy (tools/diag/variants.sh):
+//   0: each lane stores its own 96-B obs row (6 x 16 B at a 96-B lane stride:
+//      every wave-instruction touches ~48 partial 128-B lines);
+//   1: the wave transposes its 64 rows (6 KiB) through LDS so each
+//      wave-instruction stores one contiguous 1 KiB (8 whole lines);
+//   2: as 1 with non-temporal (streaming) stores for every per-ply output.
+#ifndef NARDE_OBS_STORE
+#define NARDE_OBS_STORE 2
+#endif
+
+// wave priority in k_rollout_pc: 0 none (age decides), 1 consumers first,
+// 2 producers first
+#ifndef NARDE_PC_PRIO
+#define NARDE_PC_PRIO 0
+#endif
+
+// DIAGNOSTIC ablations (timing only; results are wrong): FULL4 turn bits
+// 1 no first-sub-move pass, 2 no later doubles passes, 4 all turns treated as
+// block-free; REF2 consumer bits 8 no obs arithmetic, 16 no Philox
+#ifndef NARDE_DIAG_ABLATE
+#define NARDE_DIAG_ABLATE 0
+#endif
+
+namespace {
+
+constexpr int kBlock = 256;
+
+struct Planes {
+  uint4* p0;
+  uint4* p1;
+  int4* stats;
+};
+
+struct Rng {
+  uint32_t env0, k0, k1;
+  int dice_mode;
+};
+
+__device__ __forceinline__ void draw(const Rng& g, uint32_t t, uint32_t i, uint32_t stream,
+                                     uint32_t r[4]) {
+  philox4x32_10(t, g.env0 + i, 0u, stream, g.k0, g.k1, r);
+}
+
+// the four words of ply t of env i (narde_rules.h ply_words: one Philox
+// block per two plies; a kernel that runs consecutive plies keeps the block)
+__device__ __forceinline__ void ply_draw(const Rng& g, uint32_t t, uint32_t i, uint32_t r[4]) {
+  uint32_t R[4];
+  ply_block(t, g.env0 + i, g.k0, g.k1, R);
+  ply_words_of(R, t, g.dice_mode, r);
+}
+
+}  // namespace

@@ -1,0 +1,329 @@
+// kernels_agent.h -- what agents read and write: observations, move masks, the policy kernel and the DQN transition
+// Part of the one translation unit narde.hip (included there, in order);
+// not a standalone header.
+#pragma once
+
+namespace {
+
+__global__ void __launch_bounds__(kBlock) k_observe(Planes pl, int n, int32_t* __restrict__ obs,
+                                                    float* __restrict__ tes) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const uint4 a = pl.p0[i], b = pl.p1[i];
+  if (obs) {
+    const Side s = side_from_record(a, b);
+    store_obs(obs, i, s);
+  }
+  if (tes) {
+    // README.md:42-102 layout, absolute points: [white 24x4, bar, off,
+    // black 24x4, bar, off, player one-hot]
+    const Nib w{{a.x, a.y, b.x}};
+    const Nib k{{a.z, a.w, b.y}};
+    float2* o = reinterpret_cast<float2*>(tes + (size_t)i * 198);
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const Nib& c = side == 0 ? w : k;
+#pragma unroll
+      for (int p = 0; p < 24; ++p) {
+        const uint32_t v = nib_get(c, p);
+        const int base = side * 49 + p * 2;  // in float2 units
+        o[base] = make_float2(v >= 1u ? 1.0f : 0.0f, v >= 2u ? 1.0f : 0.0f);
+        o[base + 1] = make_float2(v >= 3u ? 1.0f : 0.0f, v >= 3u ? (float)(v - 3u) / 2.0f : 0.0f);
+      }
+      const uint32_t offc = side == 0 ? (b.z & 15u) : ((b.z >> 4) & 15u);
+      o[side * 49 + 48] = make_float2(0.0f, (float)offc / 15.0f);
+    }
+    const bool black = (b.z >> 10) & 1u;
+    o[98] = make_float2(black ? 0.0f : 1.0f, black ? 1.0f : 0.0f);
+  }
+}
+
+// One DQN transition for every env, fused (config 4, gym_narde/dqn.py
+// BatchedDQNDriver): the 198-float observation of the post-step record
+// (k_observe's encoding), the reference trainer's reward shaping
+// (train_deepq_pytorch.py:885-908), the prioritized-replay write of
+// (s, a, r', s', done) at ring slot (pos + i) % capacity with the running max
+// priority, and s <- s'.  One thread per observation float (coalesced rows;
+// the 32 B record is an L1 hit for the row's 198 threads); column 0 also
+// writes the env's scalars.  HBM per env: 792 B read (s) + 3 x 792 B written.
+struct TransArgs {
+  Planes pl;
+  int n;
+  int shaping;
+  float* state;                 // (n,198) in: s, out: s'
+  const int64_t* actions;       // (n,2)
+  const int32_t* reward;        // (n,)
+  const uint8_t* term;          // (n,)
+  const uint8_t* trunc;         // (n,)
+  float* off_seen;              // (n,2) borne-off trackers, white/black
+  float* r_obs;                 // replay (capacity,198)
+  float* r_next;                // replay (capacity,198)
+  int64_t* r_action;            // replay (capacity,2)
+  float* r_reward;              // replay (capacity,)
+  float* r_done;                // replay (capacity,)
+  float* r_prio;                // replay (capacity,)
+  const float* max_prio;        // device scalar
+  const int64_t* pos;           // device scalar: ring write cursor
+  int64_t capacity;
+};
+
+// value of column col of the 198-float observation of a record (k_observe's
+// layout), branch-free: the 64 lanes of a wave hold 64 consecutive columns,
+// so per-column branches would run every case on every wave
+__device__ __forceinline__ float tes_value(uint4 a, uint4 b, int col) {
+  const bool black = (b.z >> 10) & 1u;
+  const float player = (col == 196) != black ? 1.0f : 0.0f;
+  const int side = col >= 98 ? 1 : 0;
+  const int cc = col - 98 * side;
+  const float offv = (float)(side ? ((b.z >> 4) & 15u) : (b.z & 15u)) / 15.0f;
+  const int pt = cc < 96 ? (cc >> 2) : 0;
+  const uint32_t w0 = side ? a.z : a.x, w1 = side ? a.w : a.y, w2 = side ? b.y : b.x;
+  const int k = pt >> 3;
+  const uint32_t word = k == 0 ? w0 : (k == 1 ? w1 : w2);
+  const uint32_t v = (word >> (4 * (pt & 7))) & 15u;
+  const int j = cc & 3;
+  const float thr = v >= (uint32_t)(j + 1) ? 1.0f : 0.0f;  // j = 0, 1, 2: v >= 1, 2, 3
+  const float over = v >= 3u ? (float)(v - 3u) / 2.0f : 0.0f;
+  const float board = j == 3 ? over : thr;
+  const float pv = cc == 96 ? 0.0f : (cc == 97 ? offv : board);
+  return col >= 196 ? player : pv;
+}
+
+// the env scalars of one transition (the thread holding column 0 of row i)
+__device__ __forceinline__ void trans_scalars(const TransArgs& t, int i, int64_t slot, uint4 b) {
+  const float done = (t.term[i] | t.trunc[i]) ? 1.0f : 0.0f;
+  float r = (float)t.reward[i];
+  if (t.shaping) {
+    // +1 per checker newly borne off and +0.1 x total off, for the player
+    // to move AFTER the step (the reference reads the post-flip player);
+    // the trackers restart at 0 with a new episode.  Same fp32 ops as the
+    // torch restatement (BatchedDQNDriver._transition_torch).
+    const int black = (int)((b.z >> 10) & 1u);
+    const float now = (float)(black ? ((b.z >> 4) & 15u) : (b.z & 15u));
+    const float before = t.off_seen[2 * i + black];
+    {
+#pragma clang fp contract(off)  // torch rounds the product and the sum separately: no FMA
+      r = (r + fmaxf(now - before, 0.0f)) + 0.1f * now;
+    }
+    const float keep = 1.0f - done;
+    const float o0 = black ? t.off_seen[2 * i] : now;
+    const float o1 = black ? now : t.off_seen[2 * i + 1];
+    t.off_seen[2 * i] = o0 * keep;
+    t.off_seen[2 * i + 1] = o1 * keep;
+  }
+  t.r_action[2 * slot] = t.actions[2 * i];
+  t.r_action[2 * slot + 1] = t.actions[2 * i + 1];
+  t.r_reward[slot] = r;
+  t.r_done[slot] = done;
+  t.r_prio[slot] = *t.max_prio;
+}
+
+// Each thread owns 4 consecutive floats of the flat (n, 198) arrays, so the
+// state load and the three row stores are 16 B per lane (1 KiB per wave
+// instruction; the two replay rows are written once and read only when
+// sampled: non-temporal).  That needs the ring rows pos .. pos + n - 1
+// contiguous and 16-B aligned (pos * 198 % 4 == 0, no wrap -- the steady
+// state when the capacity is a multiple of n); otherwise each float goes
+// on its own.
+__global__ void __launch_bounds__(kBlock) k_dqn_transition(TransArgs t) {
+  const uint32_t total = (uint32_t)t.n * 198u;  // n * 198 < 2^31 (checked on the host)
+  const uint32_t e0 = 4u * (blockIdx.x * kBlock + threadIdx.x);
+  if (e0 >= total) return;
+  const int64_t pos = *t.pos;  // pos < capacity and i < n <= capacity: one wrap at most
+  const bool vec = (pos * 198) % 4 == 0 && pos + t.n <= t.capacity && e0 + 4u <= total;
+  const int i0 = (int)(e0 / 198u);
+  const int c0 = (int)(e0 - (uint32_t)i0 * 198u);
+  const uint4 a0 = t.pl.p0[i0], b0 = t.pl.p1[i0];
+  // the 4 floats span rows i0 and (if c0 > 194) i0 + 1
+  const bool split = c0 > 194 && i0 + 1 < t.n;
+  uint4 a1 = a0, b1 = b0;
+  if (split) { a1 = t.pl.p0[i0 + 1]; b1 = t.pl.p1[i0 + 1]; }
+  float nv[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = c0 + q;
+    nv[q] = c < 198 ? tes_value(a0, b0, c) : tes_value(a1, b1, c - 198);
+  }
+  if (vec) {
+    float4* st4 = reinterpret_cast<float4*>(t.state + e0);
+    const float4 ov = *st4;
+    const size_t d = (size_t)pos * 198 + e0;
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f o = {ov.x, ov.y, ov.z, ov.w};
+    const v4f nn = {nv[0], nv[1], nv[2], nv[3]};
+    __builtin_nontemporal_store(o, reinterpret_cast<v4f*>(t.r_obs + d));
+    __builtin_nontemporal_store(nn, reinterpret_cast<v4f*>(t.r_next + d));
+    *st4 = make_float4(nv[0], nv[1], nv[2], nv[3]);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t e = e0 + (uint32_t)q;
+      if (e >= total) break;
+      const int i = (int)(e / 198u);
+      const int col = (int)(e - (uint32_t)i * 198u);
+      int64_t slot = pos + i;
+      if (slot >= t.capacity) slot -= t.capacity;
+      t.r_obs[slot * 198 + col] = t.state[e];
+      t.r_next[slot * 198 + col] = nv[q];
+      t.state[e] = nv[q];
+    }
+  }
+  // column 0 of a row lies in at most one thread's 4 floats
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t e = e0 + (uint32_t)q;
+    if (e >= total) break;
+    const int i = (int)(e / 198u);
+    if (e - (uint32_t)i * 198u != 0u) continue;
+    int64_t slot = pos + i;
+    if (slot >= t.capacity) slot -= t.capacity;
+    trans_scalars(t, i, slot, i == i0 ? b0 : b1);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock) k_mask576(Planes pl, int n, Rng g,
+                                                    uint64_t* __restrict__ mask) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const Side s = side_from_record(pl.p0[i], pl.p1[i]);
+  uint32_t r[4];
+  ply_draw(g, s.t, (uint32_t)i, r);
+  int d0, d1;
+  dice_from(r[0], g.dice_mode, d0, d1);
+  Legal l;
+  legal2(s, d0, d1, l);
+  uint64_t m[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int k = 0; k < l.n; ++k) {
+    uint32_t b = l.L[k];
+    while (b) {
+      const int f = __builtin_ctz(b);
+      b &= b - 1u;
+      const int to = f - l.d[k] < 0 ? OFF : f - l.d[k];
+      if (to == 0 && f <= 5) continue;  // (f, 0) cannot be requested by a code
+      const int c = encode_move(f, to);
+      m[c >> 6] |= 1ull << (c & 63);
+    }
+  }
+  for (int q = 0; q < 9; ++q) mask[(size_t)i * 9 + q] = m[q];
+}
+
+// move-2 acceptance mask given each env's move-1 code, for the next step's
+// device dice: what NardeEnv.step would accept as move2 after move1
+// (narde_env.py:56-93: move1 must be in list #1 with >= 2 entries; the die
+// bookkeeping picks the second die; list #2 = get_valid_moves([die]) on the
+// post-move1 board; the decode quirk makes (f, 0), f <= 5, unrequestable).
+// All zero when move1 would not be played.
+__global__ void __launch_bounds__(kBlock) k_mask576_move2(Planes pl, int n, Rng g,
+                                                          const int16_t* __restrict__ move1,
+                                                          const uint8_t* __restrict__ dice,
+                                                          uint64_t* __restrict__ mask) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  Side s = side_from_record(pl.p0[i], pl.p1[i]);
+  int d0, d1;
+  if (dice) {
+    d0 = dice[2 * i];
+    d1 = dice[2 * i + 1];
+  } else {
+    uint32_t r[4];
+    ply_draw(g, s.t, (uint32_t)i, r);
+    dice_from(r[0], g.dice_mode, d0, d1);
+  }
+  Legal l;
+  legal2(s, d0, d1, l);
+  uint64_t m[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int f1, t1;
+  decode_action(move1[i], f1, t1);
+  if (l.count >= 2 && legal_contains(l, f1, t1)) {
+    apply_move(s, f1, t1);
+    const int dist = t1 == OFF ? f1 + 1 : (f1 > t1 ? f1 - t1 : t1 - f1);
+    const int rem = (d0 == dist) ? d1 : ((d1 == dist) ? d0 : d1);
+    uint32_t L2 = die_filter(s.O, s.S1o, block_info(s.O, s.P), die_candidates(s.O, s.P, rem), rem);
+    while (L2) {
+      const int f = __builtin_ctz(L2);
+      L2 &= L2 - 1u;
+      const int to = f - rem < 0 ? OFF : f - rem;
+      if (to == 0 && f <= 5) continue;  // (f, 0) cannot be requested by a code
+      const int c = encode_move(f, to);
+      m[c >> 6] |= 1ull << (c & 63);
+    }
+  }
+  for (int q = 0; q < 9; ++q) mask[(size_t)i * 9 + q] = m[q];
+}
+
+// Masked epsilon-greedy over the 576 action codes for a Q-value row per env
+// (the policy half of train_deepq_pytorch.py:411-600, batched): one wave per
+// row, lane l reads codes l + 64 j (coalesced), the legal ones are compared
+// and a wave reduction keeps the largest value, lowest code on ties
+// (torch.argmax's first maximum).  With probability epsilon the code is
+// uniform over the legal ones instead; 0 where none is legal (the
+// reference's "no move" code, :504-505).  Draws: Philox4x32-10({tag, row, 0,
+// 5}, seed): r0 < epsilon * 2^32 explores, one shared decision for both
+// heads of a step (same tag); the pick is mulhi(r1 or r2 by head, count).
+__host__ __device__ inline uint64_t eps_to_q32(float epsilon) {
+  const double e = epsilon <= 0.0f ? 0.0 : (epsilon >= 1.0f ? 1.0 : (double)epsilon);
+  return (uint64_t)(e * 4294967296.0);
+}
+
+__global__ void __launch_bounds__(256) k_policy576(const float* __restrict__ q, int64_t ldq,
+                                                   const uint64_t* __restrict__ mask, int n,
+                                                   uint64_t eps_q32, uint32_t k0, uint32_t k1,
+                                                   uint32_t tag, int head, int64_t* __restrict__ out,
+                                                   const float* __restrict__ eps_p,
+                                                   const int64_t* __restrict__ tag_p,
+                                                   const float* __restrict__ add_tab, int64_t ld_add,
+                                                   const int64_t* __restrict__ add_row) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  if (row >= n) return;  // whole waves: the row is uniform over the wave
+  if (eps_p) eps_q32 = eps_to_q32(*eps_p);  // device-resident epsilon / tag (graph replays)
+  if (tag_p) tag = (uint32_t)*tag_p;
+  uint64_t mw[9];
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    mw[j] = mask[(size_t)row * 9 + j];
+    cnt += __builtin_popcountll(mw[j]);
+  }
+  uint32_t r[4];
+  philox4x32_10(tag, (uint32_t)row, 0u, 5u, k0, k1, r);
+  const bool explore = (uint64_t)r[0] < eps_q32;
+  int code = 0;
+  if (cnt > 0 && explore) {
+    int k = (int)mulhi_u32(head ? r[2] : r[1], (uint32_t)cnt);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int c = __builtin_popcountll(mw[j]);
+      if (k >= 0 && k < c) {
+        uint64_t m = mw[j];
+        for (int t = 0; t < k; ++t) m &= m - 1ull;
+        code = 64 * j + __builtin_ctzll(m);
+      }
+      k -= c;
+    }
+  } else if (cnt > 0) {
+    const float* qr = q + (size_t)row * (size_t)ldq;
+    // optional addend row (the move-2 head's one-hot column, DecomposedDQN):
+    // v = q[row][c] + add_tab[add_row[row]][c], the same single fp32 add
+    const float* ar = add_tab ? add_tab + (size_t)add_row[row] * (size_t)ld_add : nullptr;
+    float best = -__builtin_inff();
+    int bi = 0x7FFFFFFF;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      if ((mw[j] >> lane) & 1ull) {
+        const float v = ar ? qr[64 * j + lane] + ar[64 * j + lane] : qr[64 * j + lane];
+        if (v > best) { best = v; bi = 64 * j + lane; }  // j ascending: first max kept
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+    }
+    code = bi;
+  }
+  if (lane == 0) out[row] = code;
+}
+
+}  // namespace

@@ -1,0 +1,289 @@
+// kernels_full4.h -- the wave-cooperative FULL4 turn and its list query
+// Part of the one translation unit narde.hip (included there, in order);
+// not a standalone header.
+#pragma once
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Wave-cooperative FULL4 turn (device only).
+//
+// Same rule and result as env_turn_full (narde_rules.h, which the host check
+// runs; the GPU parity tests hold this one to the oracle), organised for
+// SIMT.  The expensive part of a turn is per source: "after this first
+// sub-move, can the other die still move" (two dice) and "after this
+// sub-move, are M-k-1 more still playable" (doubles, a depth-first search).
+// Run per lane, a wave loops as long as its busiest lane while the others
+// idle: on a typical ply ~10 of the 64 lanes roll doubles, and the rest wait.
+// Here every lane publishes its (lane, source) checks; a wave prefix sum of
+// the per-lane counts places them in one task list in LDS, and all 64 lanes
+// take tasks 64 at a time (the owner's state is read back from LDS, results
+// are OR-ed into the owner's mask with ds_or).  Every call is made with the
+// whole wave converged: the turn below is straight-line code with per-lane
+// masks instead of rule branches around the calls.
+struct CoopLds {
+  uint4 snap[64][2];          // owner state: {own w0..w2, O}, {S1, P, low, params}
+  uint32_t task[64 * 32];     // (lane << 8) | (which << 7) | source; 2 masks x <= 15 sources
+  uint32_t res[64][3];
+};
+
+// exclusive prefix sum of x (0 <= x < 64) over the wave, and the total, from
+// one ballot per bit of x: lane l's prefix adds 2^b for every lower lane with
+// bit b set (v_mbcnt counts them) -- no LDS round trips, unlike shuffles
+__device__ __forceinline__ int wave_prefix(int x, int lane, int& total) {
+  (void)lane;
+  int excl = 0;
+  total = 0;
+#pragma unroll
+  for (int b = 0; b < 6; ++b) {
+    const uint64_t m = __ballot((x >> b) & 1);
+    excl += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
+    total += __builtin_popcountll(m) << b;
+  }
+  return excl;
+}
+
+// One cooperative pass over every lane's per-source checks.  Per lane:
+//   mode 1 (pair, two dice a = d_hi, b = d_lo): m0 = first moves with a,
+//     kept (res 0) iff b still has a move after them; m1 = first moves with
+//     b, kept (res 1) iff a still does.
+//   mode 0 (depth, doubles a): m0 = sources; res j gets the sources after
+//     which at least j + 1 more sub-moves are playable (searched up to
+//     `need`; block-free lanes try the chain bound first).
+__device__ void coop_run(CoopLds& W, const Side& s, uint32_t low, int a, int b, int hl, uint32_t m0,
+                         uint32_t m1, int need, bool bf, int mode, int lane, uint32_t out[3]) {
+  out[0] = out[1] = out[2] = 0u;
+  if (__ballot((m0 | m1) != 0u) == 0ull) return;  // wave-uniform: nothing to check
+  const int c0 = __builtin_popcount(m0), cnt = c0 + __builtin_popcount(m1);
+  int total;
+  const int off = wave_prefix(cnt, lane, total);
+  W.res[lane][0] = W.res[lane][1] = W.res[lane][2] = 0u;
+  if (cnt) {
+    W.snap[lane][0] = make_uint4(s.own.w[0], s.own.w[1], s.own.w[2], s.O);
+    W.snap[lane][1] = make_uint4(s.S1o, s.P, low,
+                                 (uint32_t)a | ((uint32_t)b << 4) | ((uint32_t)(hl + 1) << 8) |
+                                     ((uint32_t)need << 12) | ((uint32_t)bf << 16) |
+                                     ((uint32_t)mode << 17) | (s.off_own << 20));
+    int k = off;
+    for (int which = 0; which < 2; ++which) {
+      uint32_t m = which ? m1 : m0;
+      while (m) {
+        const int p = __builtin_ctz(m);
+        m &= m - 1u;
+        W.task[k++] = ((uint32_t)lane << 8) | ((uint32_t)which << 7) | (uint32_t)p;
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();  // a wave's LDS operations retire in issue order
+  for (int base = 0; base < total; base += 64) {
+    const int t = base + lane;
+    if (t < total) {
+      const uint32_t tk = W.task[t];
+      const int ow = (int)(tk >> 8), which = (int)((tk >> 7) & 1u), p = (int)(tk & 0x7Fu);
+      const uint4 x = W.snap[ow][0], y = W.snap[ow][1];
+      Side c;
+      c.own.w[0] = x.x; c.own.w[1] = x.y; c.own.w[2] = x.z;
+      c.O = x.w; c.S1o = y.x; c.P = y.y;
+      c.opp.w[0] = c.opp.w[1] = c.opp.w[2] = 0u;
+      c.S1p = 0u; c.off_opp = 0u; c.ft_own = 0u; c.ft_opp = 0u; c.black = 0u; c.elapsed = 0u; c.t = 0u;
+      const uint32_t lw = y.z, prm = y.w;
+      c.off_own = prm >> 20;
+      const int pa = (int)(prm & 15u), pb = (int)((prm >> 4) & 15u);
+      const int thl = (int)((prm >> 8) & 15u) - 1, tneed = (int)((prm >> 12) & 15u);
+      const bool tbf = (prm >> 16) & 1u;
+      if ((prm >> 17) & 1u) {
+        const int ta = which ? pb : pa, tb = which ? pa : pb;
+        uint32_t O2, S2;
+        child_masks(c, p, ta, O2, S2);
+        uint32_t L2 = die_candidates(O2, c.P, tb);
+        if (!tbf) L2 = die_filter(O2, S2, block_info_low(O2, lw), L2, tb);
+        if (p == 23) L2 &= ~HEAD;
+        if (L2) atomicOr(&W.res[ow][which], 1u << p);
+      } else {
+        const int hl2 = thl - (p == 23 ? 1 : 0);
+        int dep = 0;
+        if (tbf) {
+          uint32_t O2, S2;
+          child_masks(c, p, pa, O2, S2);
+          const int lb = f4_chain_bound(O2, S2, c.P, pa, hl2);
+          dep = lb >= tneed ? tneed : 0;
+        }
+        if (dep < tneed) {
+          apply_die(c, p, pa);
+          dep = tneed == 1 ? f4_depth<1>(c, lw, pa, hl2, tbf)
+                           : (tneed == 2 ? f4_depth<2>(c, lw, pa, hl2, tbf) : f4_depth<3>(c, lw, pa, hl2, tbf));
+        }
+        for (int j = 0; j < dep; ++j) atomicOr(&W.res[ow][j], 1u << p);
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  out[0] = W.res[lane][0];
+  out[1] = W.res[lane][1];
+  out[2] = W.res[lane][2];
+}
+
+// env_turn_full with the per-source checks done cooperatively (see above)
+__device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, const uint32_t w[4],
+                               TurnOut& o, CoopLds& W, int lane) {
+  const uint32_t low = block_lowmask(s.P);
+  const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
+  const bool dbl = dh == dl;
+#if NARDE_DIAG_ABLATE & 4
+  const bool bf = true;  // DIAGNOSTIC timing only: wrong results
+#else
+  const bool bf = turn_block_free(s.O, s.P, low, dh, dl);
+#endif
+  // first sub-move: the lists, the shortcuts, then every lane's checks at once
+  const uint32_t Lh = legal1(s, low, dh, bf);
+  const uint32_t Ll = dbl ? 0u : legal1(s, low, dl, bf);
+  const bool all_h = !dbl && bf && f4_lower_bound(s.O, s.S1o, s.P, dl, 1) >= 2;
+  const bool all_l = !dbl && bf && f4_lower_bound(s.O, s.S1o, s.P, dh, 1) >= 2;
+  const int hl0 = (dbl && s.ft_own && (dh == 3 || dh == 4 || dh == 6)) ? 2 : 1;
+  const bool fast = dbl && bf && f4_lower_bound(s.O, s.S1o, s.P, dh, hl0) >= 4;
+  // not fast: a chain bound >= 7 still keeps every first sub-move (one
+  // sub-move lowers it by <= 4) with M = 4
+  const int cb0 = (dbl && bf && !fast) ? f4_chain_bound(s.O, s.S1o, s.P, dh, hl0) : 0;
+  // block-free with bear-off fixed: M exactly from the chains and every
+  // C_k = L_k (f4_exact_moves) -- ~3/4 of the doubles turns the bounds miss
+  const bool exact = dbl && bf && !fast && cb0 < 7 && Lh != 0u && f4_bearoff_fixed(s);
+  const int Mx = exact ? f4_exact_moves(s, dh, hl0) : 0;
+  const bool srch = dbl && !fast && Lh != 0u && cb0 < 7 && !exact;
+  // one cooperative pass for every lane's first-sub-move checks
+  uint32_t r0[3];
+  {
+    const bool pair = !dbl;
+    const uint32_t m0 = pair ? (all_h ? 0u : Lh) : (srch ? Lh : 0u);
+    const uint32_t m1 = pair ? (all_l ? 0u : Ll) : 0u;
+#if NARDE_DIAG_ABLATE & 3
+    r0[0] = Lh; r0[1] = Ll; r0[2] = Lh;  // DIAGNOSTIC timing only: wrong results
+    (void)m0; (void)m1; (void)pair;
+#else
+    coop_run(W, s, low, dh, dl, pair ? 1 : hl0, m0, m1, 3, bf, pair ? 1 : 0, lane, r0);
+#endif
+  }
+  uint32_t Ch, Cl;
+  int M;
+  if (!dbl) {
+    Ch = all_h ? Lh : r0[0];
+    Cl = all_l ? Ll : r0[1];
+    if (Ch | Cl) {
+      M = 2;
+    } else {
+      M = (Lh | Ll) ? 1 : 0;
+      Ch = Lh;  // only one die playable: the higher one if it can
+      Cl = Lh ? 0u : Ll;
+    }
+  } else {
+    Cl = 0u;
+    if (fast || (cb0 >= 7 && Lh)) { Ch = Lh; M = 4; }
+    else if (!Lh) { Ch = 0u; M = 0; }
+    else if (exact) { Ch = Lh; M = Mx; }
+    else if (r0[2]) { Ch = r0[2]; M = 4; }  // some source leaves 3 more
+    else if (r0[1]) { Ch = r0[1]; M = 3; }
+    else if (r0[0]) { Ch = r0[0]; M = 2; }
+    else { Ch = Lh; M = 1; }
+  }
+  o.legal = (uint64_t)Ch | ((uint64_t)Cl << 24) | ((uint64_t)dh << 48) | ((uint64_t)dl << 52) |
+            ((uint64_t)M << 56);
+  uint64_t played = ~0ull;
+  int hl = hl0;
+  bool go = M >= 1;
+  int d = dh;
+  if (go) {
+    const int nh = __builtin_popcount(Ch), n = nh + __builtin_popcount(Cl);
+    int p;
+    if (play) {
+      p = play_byte(pw, 0);
+      d = play_byte(pw, 1);
+      go = p >= 0 && p < 24 && ((d == dh && ((Ch >> p) & 1u)) || (!dbl && d == dl && ((Cl >> p) & 1u)));
+    } else {
+      const int idx = (int)mulhi_u32(w[0], (uint32_t)n);
+      const bool hi = idx < nh;
+      d = hi ? dh : dl;
+      p = select_bit(hi ? Ch : Cl, hi ? idx : idx - nh);
+    }
+    if (go) {
+      apply_die(s, p, d);
+      played = played_set(played, 0, p, d);
+      hl -= p == 23 ? 1 : 0;
+    }
+  }
+  // sub-moves 1..3 (two dice: only k = 1, with the other die)
+  for (int k = 1; k < 4; ++k) {
+    const bool act = go && k < M;
+    if (__ballot(act) == 0ull) break;  // wave-uniform: no lane has sub-move k
+    const int dk = dbl ? dh : (d == dh ? dl : dh);
+    uint32_t Lk = act ? legal1(s, low, dk, bf) : 0u;
+    if (hl <= 0) Lk &= ~HEAD;
+    const int need = M - k - 1;
+    const bool direct = !dbl || fast || exact || need <= 0 ||
+                        (act && bf && (f4_bearoff_fixed(s, need + 1) ||
+                                       f4_chain_bound(s.O, s.S1o, s.P, dk, hl) >= need + 4));
+    uint32_t rk[3];
+#if NARDE_DIAG_ABLATE & 2
+    rk[0] = rk[1] = rk[2] = Lk;
+#else
+    coop_run(W, s, low, dk, 0, hl, (act && !direct) ? Lk : 0u, 0u, need > 0 ? need : 1, bf, 0, lane, rk);
+#endif
+    const uint32_t C = direct ? Lk : (need >= 2 ? rk[1] : rk[0]);
+    if (act) {
+      int p;
+      bool ok = true;
+      if (play) {
+        p = play_byte(pw, 2 * k);
+        ok = play_byte(pw, 2 * k + 1) == dk && p >= 0 && p < 24 && ((C >> p) & 1u);
+      } else {
+        const uint32_t wk = k == 1 ? w[1] : (k == 2 ? w[2] : w[3]);
+        p = select_bit(C, (int)mulhi_u32(wk, (uint32_t)__builtin_popcount(C)));
+      }
+      if (ok) {
+        apply_die(s, p, dk);
+        played = played_set(played, k, p, dk);
+        hl -= p == 23 ? 1 : 0;
+      } else {
+        go = false;
+      }
+    }
+  }
+  o.played = played;
+  o.max_dice = M;
+  o.term = s.off_own == 15u;
+  o.reward = o.term ? (s.off_opp > 0u ? 1 : 2) : 0;
+  if (!o.term) side_flip(s);
+}
+
+// this wave's slice of the block's cooperative scratch
+#define COOP_LDS_DECL                                  \
+  __shared__ CoopLds coop_lds[kBlock / 64];           \
+  CoopLds& wave_coop = coop_lds[threadIdx.x >> 6];
+
+// FULL4 first-sub-move set C_0 and max dice M for the given (or the next
+// device) dice: the turn engine run on a copy with a play whose first
+// sub-move is invalid, so nothing is applied.
+__global__ void __launch_bounds__(kBlock) k_legal_full(Planes pl, int n, Rng g,
+                                                       const uint8_t* __restrict__ dice2,
+                                                       uint64_t* __restrict__ out) {
+  COOP_LDS_DECL
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = i < n;  // no early exit: the turn is wave-cooperative
+  Side s = valid ? side_from_record(pl.p0[i], pl.p1[i]) : side_start(0u);
+  int d0 = 1, d1 = 2;
+  if (dice2) {
+    if (valid) {
+      d0 = dice2[2 * i];
+      d1 = dice2[2 * i + 1];
+    }
+  } else {
+    uint32_t r[4];
+    ply_draw(g, s.t, (uint32_t)i, r);
+    dice_from(r[0], g.dice_mode, d0, d1);
+  }
+  const uint32_t w[4] = {0u, 0u, 0u, 0u};
+  TurnOut o;
+  // play word of -1s: nothing is applied
+  coop_turn_full(s, d0, d1, true, ~0ull, w, o, wave_coop, (int)(threadIdx.x & 63));
+  if (valid) out[i] = o.legal;
+}
+
+}  // namespace

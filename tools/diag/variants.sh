@@ -7,7 +7,7 @@ mkdir -p tools/diag/build
 if [ "$1" != "run" ]; then
   for v in 0 1 2; do
     /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -shared -DNARDE_OBS_STORE=$v \
-      -o tools/diag/build/libnarde_v$v.so gym-narde_amd/csrc/narde.hip
+      -o tools/diag/build/libnarde_v$v.so gym-narde_amd/csrc/narde.hip gym-narde_amd/csrc/dqn_learner.hip
   done
 fi
 if [ "$1" != "build" ]; then
