@@ -309,7 +309,7 @@ def test_dqn_loss_kernel_vs_torch_autograd():
     assert torch.equal(td, td_ref)
     assert torch.equal(q1f.grad, q1r.grad) and torch.equal(q2f.grad, q2r.grad)
     assert float(loss.detach()) == pytest.approx(float(loss_ref.detach()), rel=1e-6)
-    assert float(copy) == float(loss)
+    assert float(copy) == float(loss.detach())
 
 
 def test_prio_update_kernel_exact():
