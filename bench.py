@@ -266,7 +266,9 @@ def main():
     # masks -> DecomposedDQN -> env step -> device replay -> one PER update)
     dqn = None
     if args.dqn_steps > 0 and not is_full4:
-        from gym_narde.dqn import BatchedDQNDriver
+        from gym_narde.dqn import BatchedDQNDriver, use_tuned_gemms
+
+        tuned = use_tuned_gemms()  # TunableOp GEMM choices measured on MI355X
 
         env_q = VecNardeEnv(per, device=dev, seed=args.seed + 1, env_id_offset=first,
                             max_episode_steps=1000)
@@ -314,6 +316,7 @@ def main():
             "train_batch": args.dqn_train_batch,
             "updates_per_step": 1,
             "dtype": "f32",
+            "gemms": "TunableOp results (gym_narde/tunableop_gfx950.csv)" if tuned else "torch heuristics",
             "final_loss": float(drv.last_loss) if drv.last_loss is not None else None,
         }
         env_q.close()

@@ -33,6 +33,7 @@ W = [Wf | Wm]: mathematically identical to the reference's one-hot concat,
 equal in fp32 up to summation order (tests/test_dqn_cpu.py).
 """
 import ctypes
+import os
 
 import torch
 import torch.nn as nn
@@ -130,6 +131,24 @@ def policy_576(q, mask576, epsilon, seed, tag, head, out=None, add=None):
         *args, float(epsilon), int(seed) & (2 ** 64 - 1), int(tag) & 0xFFFFFFFF, int(head), _lib.ptr(out),
         stream), "narde_policy_masked_argmax576")
     return out
+
+
+TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop_gfx950.csv")
+
+
+def use_tuned_gemms(path=TUNED_GEMMS):
+    """Select the driver's fp32 GEMMs (hipBLASLt / rocBLAS solutions per
+    shape) from a TunableOp results file measured on MI355X (tools/diag/
+    gpu_tunable.sh; torch validates the ROCm / hipBLASLt versions in it and
+    falls back to its heuristics on a mismatch).  Process-wide torch state,
+    so an application opt-in (bench.py), not a side effect of the driver.
+    Returns whether the file was loaded."""
+    if not os.path.exists(path):
+        return False
+    torch.cuda.tunable.enable(True)
+    torch.cuda.tunable.tuning_enable(False)
+    torch.cuda.tunable.set_filename(path, insert_device_ordinal=False)
+    return bool(torch.cuda.tunable.read_file(path))
 
 
 def _stream(dev):

@@ -7,12 +7,14 @@ import time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gym-narde_amd"))
 import torch  # noqa: E402
 
-from gym_narde.dqn import BatchedDQNDriver  # noqa: E402
+from gym_narde.dqn import BatchedDQNDriver, use_tuned_gemms  # noqa: E402
 from gym_narde.vector import VecNardeEnv  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 N = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 eager = len(sys.argv) > 3 and sys.argv[3] == "eager"
+if os.environ.get("NARDE_TUNED_GEMMS", "1") == "1":
+    use_tuned_gemms()
 env = VecNardeEnv(B, device="cuda:0", seed=1)
 drv = BatchedDQNDriver(env, train_batch=4096, capacity=max(1 << 20, 4 * B))
 if not eager:
