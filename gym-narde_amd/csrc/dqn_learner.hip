@@ -268,6 +268,99 @@ __global__ void __launch_bounds__(kLearnThreads) k_prio_update(const int64_t* __
   }
 }
 
+// ------------------------------------------------ grad clip + Adam, fused
+// clip_grad_norm_(max_norm) followed by Adam (torch.optim.Adam's update:
+// m <- lerp(m, g, 1 - b1), v <- b2 v + (1 - b2) g^2, p -= lr / bc1 * m /
+// (sqrt(v) / sqrt(bc2) + eps)) over up to 8 parameter tensors, in two
+// kernels with enough blocks to fill the chip (torch's multi-tensor kernels
+// run one block per 64 K-element chunk: ~12 blocks for this network).
+constexpr int kMaxTensors = 8;
+constexpr int kNormBlocks = 1024;
+
+struct ParamTable {
+  float* p[kMaxTensors];
+  const float* g[kMaxTensors];
+  float* m[kMaxTensors];
+  float* v[kMaxTensors];
+  int64_t off[kMaxTensors + 1];  // prefix sums of the sizes
+  int count;
+};
+
+__device__ __forceinline__ int tensor_of(const ParamTable& t, int64_t e) {
+  int k = 0;
+#pragma unroll
+  for (int j = 1; j < kMaxTensors; ++j) k += (j < t.count && e >= t.off[j]) ? 1 : 0;
+  return k;
+}
+
+// pass 1: sum of g^2 per block -> partial[]; the last block to finish sums
+// the partials in a fixed order, writes the clip coefficient min(1,
+// max_norm / (norm + 1e-6)), advances the Adam step and clears the ticket
+__global__ void __launch_bounds__(256) k_grad_sqnorm(ParamTable t, float* __restrict__ partial,
+                                                     uint32_t* __restrict__ ticket, float* __restrict__ coef,
+                                                     int64_t* __restrict__ step, float max_norm) {
+  __shared__ float red[4];
+  __shared__ bool last;
+  const int64_t total = t.off[t.count];
+  float acc = 0.0f;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int k = tensor_of(t, e);
+    const float g = t.g[k][e - t.off[k]];
+    acc += g * g;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    __threadfence();
+    last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  float s = 0.0f;
+  for (int b = threadIdx.x; b < (int)gridDim.x; b += 256) s += partial[b];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
+    const float c = max_norm / (norm + 1e-6f);
+    *coef = c < 1.0f ? c : 1.0f;
+    *step += 1;
+    *ticket = 0u;
+  }
+}
+
+// pass 2: the Adam update of every element with the clipped gradient
+__global__ void __launch_bounds__(256) k_adam(ParamTable t, const float* __restrict__ coef,
+                                              const int64_t* __restrict__ step, float lr, float b1, float b2,
+                                              float eps) {
+  __shared__ float sc[3];
+  if (threadIdx.x == 0) {
+    const float st = (float)*step;
+    const float bc1 = 1.0f - powf(b1, st), bc2 = 1.0f - powf(b2, st);
+    sc[0] = lr / bc1;
+    sc[1] = sqrtf(bc2);
+    sc[2] = *coef;
+  }
+  __syncthreads();
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= t.off[t.count]) return;
+  const int k = tensor_of(t, e);
+  const int64_t i = e - t.off[k];
+  const float g = t.g[k][i] * sc[2];
+  float m = t.m[k][i], v = t.v[k][i];
+  m = m + (1.0f - b1) * (g - m);
+  v = b2 * v + (1.0f - b2) * (g * g);
+  t.m[k][i] = m;
+  t.v[k][i] = v;
+  t.p[k][i] -= sc[0] * m / (sqrtf(v) / sc[1] + eps);
+}
+
 }  // namespace
 
 extern "C" {
@@ -328,6 +421,40 @@ int narde_prio_update(int device, const int64_t* idx, const float* td, int64_t b
   k_prio_update<<<1, kLearnThreads, 0, (hipStream_t)stream>>>(idx, td, (int)batch, eps, prio, max_prio, epsilon,
                                                               eps_min, eps_decay);
   return check_launch("k_prio_update");
+}
+
+
+int narde_adam_clip(int device, int n_tensors, float* const* params, const float* const* grads, float* const* m,
+                    float* const* v, const int64_t* sizes, int64_t* step, float lr, float beta1, float beta2,
+                    float eps, float max_norm, float* scratch, void* stream) {
+  if (n_tensors <= 0 || n_tensors > kMaxTensors) return bad("1..8 tensors");
+  if (!params || !grads || !m || !v || !sizes || !step || !scratch) return bad("NULL argument");
+  ParamTable t{};
+  t.count = n_tensors;
+  t.off[0] = 0;
+  for (int k = 0; k < n_tensors; ++k) {
+    if (!params[k] || !grads[k] || !m[k] || !v[k] || sizes[k] <= 0) return bad("bad tensor");
+    t.p[k] = params[k];
+    t.g[k] = grads[k];
+    t.m[k] = m[k];
+    t.v[k] = v[k];
+    t.off[k + 1] = t.off[k] + sizes[k];
+  }
+  for (int k = n_tensors; k < kMaxTensors; ++k) t.off[k + 1] = t.off[n_tensors];
+  const int64_t total = t.off[n_tensors];
+  if (total >= (int64_t(1) << 31)) return bad("too many parameters");
+  // scratch: kNormBlocks partial sums, the clip coefficient, the ticket
+  float* partial = scratch;
+  float* coef = scratch + kNormBlocks;
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(scratch + kNormBlocks + 1);
+  DeviceGuard dg(device);
+  int nb = (int)((total + 256 * 4 - 1) / (256 * 4));
+  nb = nb < kNormBlocks ? nb : kNormBlocks;
+  k_grad_sqnorm<<<nb, 256, 0, (hipStream_t)stream>>>(t, partial, ticket, coef, step, max_norm);
+  const int rc = check_launch("k_grad_sqnorm");
+  if (rc != NARDE_OK) return rc;
+  k_adam<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(t, coef, step, lr, beta1, beta2, eps);
+  return check_launch("k_adam");
 }
 
 }  // extern "C"

@@ -277,6 +277,16 @@ int narde_prio_update(int device, const int64_t *idx, const float *td, int64_t b
                       float *prio, float *max_prio, float *epsilon, float eps_min,
                       float eps_decay, void *stream);
 
+/* torch.nn.utils.clip_grad_norm_(max_norm) + one torch.optim.Adam step
+ * (train_deepq_pytorch.py's optimizer) over n_tensors <= 8 fp32 parameter
+ * tensors (params/grads/m/v: arrays of n_tensors device pointers, sizes in
+ * elements).  *step (device i64) is advanced first; scratch: >= 1026 floats
+ * of device memory, its last word zero before the first call (left zero). */
+int narde_adam_clip(int device, int n_tensors, float *const *params, const float *const *grads,
+                    float *const *m, float *const *v, const int64_t *sizes, int64_t *step, float lr,
+                    float beta1, float beta2, float eps, float max_norm, float *scratch,
+                    void *stream);
+
 /* Stateless: Narde._violates_block_rule on n perspective boards i8[n][24]. */
 int narde_violates_block_rule(int device, const int8_t *boards, int64_t n, uint8_t *out,
                               void *stream);

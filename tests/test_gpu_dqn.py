@@ -365,3 +365,30 @@ def test_fused_and_torch_learners_agree_on_one_update():
         t2 = r + (1 - d) * drv.gamma * drv.target.move2_from_features(tf, nq1.argmax(1)).max(1)[0]
     loss_t = (w * (q1 - t1) ** 2).mean() + (w * (q2 - t2) ** 2).mean()
     assert float(loss_f) == pytest.approx(float(loss_t), rel=1e-5)
+
+
+@pytest.mark.parametrize("scale", [1e-3, 50.0])  # clip inactive / active
+def test_fused_adam_clip_matches_torch(scale):
+    """narde_adam_clip == clip_grad_norm_(10) + torch.optim.Adam over three
+    steps, to fp32 rounding (operation order differs)."""
+    import copy
+
+    from gym_narde.dqn import DecomposedDQN, FusedAdamClip
+
+    torch.manual_seed(0)
+    a = DecomposedDQN(198).cuda()
+    b = copy.deepcopy(a)
+    ref = torch.optim.Adam(a.parameters(), lr=1e-3)
+    fus = FusedAdamClip(b.parameters(), lr=1e-3, max_norm=10.0)
+    g = torch.Generator(device="cuda:0").manual_seed(1)
+    for _ in range(3):
+        grads = [torch.randn(p.shape, device="cuda:0", generator=g) * scale for p in a.parameters()]
+        for p, q, gr in zip(a.parameters(), b.parameters(), grads):
+            p.grad = gr.clone()
+            q.grad = gr.clone()
+        torch.nn.utils.clip_grad_norm_(a.parameters(), max_norm=10.0)
+        ref.step()
+        fus.step()
+    for p, q in zip(a.parameters(), b.parameters()):
+        assert torch.allclose(p, q, rtol=1e-5, atol=1e-6)
+    assert int(fus.step_t) == 3
