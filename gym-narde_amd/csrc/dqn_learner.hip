@@ -448,7 +448,7 @@ int narde_adam_clip(int device, int n_tensors, float* const* params, const float
   float* coef = scratch + kNormBlocks;
   uint32_t* ticket = reinterpret_cast<uint32_t*>(scratch + kNormBlocks + 1);
   DeviceGuard dg(device);
-  int nb = (int)((total + 256 * 4 - 1) / (256 * 4));
+  int nb = (int)((total + 256 * 16 - 1) / (256 * 16));  // ~16 elements per thread
   nb = nb < kNormBlocks ? nb : kNormBlocks;
   k_grad_sqnorm<<<nb, 256, 0, (hipStream_t)stream>>>(t, partial, ticket, coef, step, max_norm);
   const int rc = check_launch("k_grad_sqnorm");
