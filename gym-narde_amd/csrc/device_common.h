@@ -26,6 +26,12 @@
 #define NARDE_PC_PRIO 0
 #endif
 
+// unroll the rule waves' plies of a full barrier block (k_rollout_pc;
+// measured within noise, +-2 %: off)
+#ifndef NARDE_PC_UNROLL
+#define NARDE_PC_UNROLL 0
+#endif
+
 // DIAGNOSTIC ablations (timing only; results are wrong): FULL4 turn bits
 // 1 no first-sub-move pass, 2 no later doubles passes, 4 all turns treated as
 // block-free; REF2 consumer bits 8 no obs arithmetic, 16 no Philox

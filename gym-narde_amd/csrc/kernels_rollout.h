@@ -370,7 +370,7 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
     const int np = min(kPcR, plies - p0);
     if (producer) {
       if (valid) {
-        for (int k = 0; k < np; ++k) {
+        auto one_ply = [&](int k) {
           const uint2 rv = L.draw[b & 1][k][le];
           uint32_t r[4];
           ply_words(rv.x, rv.y, g.dice_mode, r);
@@ -378,7 +378,17 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
           int term, trunc;
           env_ply(s, st, r, false, 0, 0, g.dice_mode, true, 0, 0, max_steps, true, o, term, trunc);
           if (kOut) pc_put(L, b & 1, k, le, s, o, term, trunc);
+        };
+#if NARDE_PC_UNROLL
+        if (np == kPcR) {
+#pragma unroll
+          for (int k = 0; k < kPcR; ++k) one_ply(k);
+        } else {
+          for (int k = 0; k < np; ++k) one_ply(k);
         }
+#else
+        for (int k = 0; k < np; ++k) one_ply(k);
+#endif
       }
     } else {
       if (b + 1 < nb) draw_block(b + 1);
