@@ -188,6 +188,8 @@ def main():
 
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
+        if dist.get_backend() == "gloo":  # D.rehearsal(): host tensors
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_ms = float(t[0]), float(t[1])
     total_steps = world * per * K

@@ -21,15 +21,23 @@ def env_shard(global_envs, rank, world):
     return rank * per, per
 
 
+def rehearsal():
+    """NARDE_REHEARSAL=1: run every rank on GPU 0 over gloo, so the N-rank
+    bench path can be exercised on a one-GPU box (tools/diag/gpu_rehearse.sh).
+    Never set for measurements."""
+    return os.environ.get("NARDE_REHEARSAL", "0") == "1"
+
+
 def init_from_env(backend=None):
     """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/
-    LOCAL_RANK/MASTER_*).  Returns (rank, world, local_rank)."""
+    LOCAL_RANK/MASTER_*).  Returns (rank, world, local_rank); local_rank is the
+    GPU index to use (0 for every rank under rehearsal())."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if rehearsal() else int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            backend = "gloo" if rehearsal() or not torch.cuda.is_available() else "nccl"
         if backend == "nccl":
             torch.cuda.set_device(local)
             dist.init_process_group(backend, device_id=torch.device("cuda", local))
@@ -44,10 +52,12 @@ def gather_stats(local_stats):
     if not dist.is_initialized() or dist.get_world_size() == 1:
         return local_stats
     world = dist.get_world_size()
-    out = torch.empty((world * local_stats.shape[0],) + tuple(local_stats.shape[1:]),
-                      dtype=local_stats.dtype, device=local_stats.device)
-    dist.all_gather_into_tensor(out, local_stats.contiguous())
-    return out
+    src = local_stats.contiguous()
+    if dist.get_backend() == "gloo" and src.is_cuda:  # gloo gathers host tensors
+        src = src.cpu()
+    out = torch.empty((world * src.shape[0],) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+    dist.all_gather_into_tensor(out, src)
+    return out.to(local_stats.device)
 
 
 def summarize(stats):
