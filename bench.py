@@ -202,14 +202,17 @@ def main():
         env.step()
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(S)]
-    a0 = time.perf_counter()
-    for i in range(S):
+    for i in range(S):  # per-launch kernel time (events cost host time: not in the rate below)
         ev[i][0].record()
         env.step()
         ev[i][1].record()
     torch.cuda.synchronize()
-    api_eager = per * S / (time.perf_counter() - a0)
     step_ms = sum(x.elapsed_time(y) for x, y in ev) / S
+    a0 = time.perf_counter()
+    for i in range(S):
+        env.step()
+    torch.cuda.synchronize()
+    api_eager = per * S / (time.perf_counter() - a0)
     G = 50
     graph = torch.cuda.CUDAGraph()
     cap = torch.cuda.Stream()
