@@ -103,12 +103,22 @@ class VecNardeEnv:
         self.legal = torch.zeros(B, dtype=torch.int64, **z)
         self.actions_used = torch.zeros((B, 2), dtype=torch.int16, **z)
         self.played = torch.zeros(B, dtype=torch.int64, **z)
+        # per-call plumbing of step(), resolved once: the bound entry point and
+        # the output buffers' pointers (they never move)
+        lib = self.handle.lib
+        self._step_fn = lib.narde_step_full if self.full else lib.narde_step
+        self._step_out = tuple(_lib.ptr(t) for t in (
+            (self.obs, self.reward, self.terminated, self.truncated, self.legal, self.played) if self.full else
+            (self.obs, self.reward, self.terminated, self.truncated, self.legal, self.actions_used)))
 
     # ------------------------------------------------------------ plumbing
     def _s(self):
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
     def _dev(self, x, dtype, shape):
+        if (isinstance(x, self.torch.Tensor) and x.dtype == dtype and x.device == self.device
+                and x.is_contiguous() and tuple(x.shape) == tuple(shape)):
+            return x  # already a device tensor of the right layout
         t = self.torch.as_tensor(x, device=self.device).to(dtype).contiguous()
         if tuple(t.shape) != tuple(shape):
             raise ValueError(f"expected shape {tuple(shape)}, got {tuple(t.shape)}")
@@ -228,20 +238,17 @@ class VecNardeEnv:
         B = self.num_envs
         if self.full:
             a = None if actions is None else self._dev(actions, self.torch.int8, (B, 4, 2))
-            d = None if dice is None else self._dev(dice, self.torch.uint8, (B, 2))
-            self.handle.call("narde_step_full", _lib.ptr(a), _lib.ptr(d), _lib.ptr(self.obs),
-                             _lib.ptr(self.reward), _lib.ptr(self.terminated),
-                             _lib.ptr(self.truncated), _lib.ptr(self.legal), _lib.ptr(self.played),
-                             int(self.autoreset), self._s())
+        else:
+            a = None if actions is None else self._dev(actions, self.torch.int16, (B, 2))
+        d = None if dice is None else self._dev(dice, self.torch.uint8, (B, 2))
+        rc = self._step_fn(self.handle.h, None if a is None else _lib.ptr(a), None if d is None else _lib.ptr(d),
+                           *self._step_out, int(self.autoreset), self._s())
+        if rc:
+            _lib.check(rc, "narde_step_full" if self.full else "narde_step")
+        if self.full:
             self._keep = (a, d)
             return (self.obs, self.reward, self.terminated, self.truncated,
                     {"legal": self.legal, "played": self.played})
-        a = None if actions is None else self._dev(actions, self.torch.int16, (B, 2))
-        d = None if dice is None else self._dev(dice, self.torch.uint8, (B, 2))
-        self.handle.call("narde_step", _lib.ptr(a), _lib.ptr(d), _lib.ptr(self.obs),
-                         _lib.ptr(self.reward), _lib.ptr(self.terminated), _lib.ptr(self.truncated),
-                         _lib.ptr(self.legal), _lib.ptr(self.actions_used), int(self.autoreset),
-                         self._s())
         return (self.obs, self.reward, self.terminated, self.truncated,
                 {"legal": self.legal, "actions": self.actions_used})
 
