@@ -51,3 +51,33 @@ def test_create_fails_loudly_without_gpu():
         pytest.skip("GPU present")
     with pytest.raises(_lib.NardeLibraryError):
         _lib.Handle(0, 16)
+
+
+def test_argument_errors_are_einval_before_any_device_call():
+    """Every entry point validates its arguments first: NULL handles and
+    pointers, bad sizes and counts return NARDE_EINVAL (-1) with a message,
+    without touching a GPU (this runs on the CPU-only container)."""
+    lib = _lib.load()
+    N = None
+    cases = [
+        ("narde_step", (N, N, N, N, N, N, N, N, N, 1, N)),
+        ("narde_step_full", (N, N, N, N, N, N, N, N, N, 1, N)),
+        ("narde_rollout", (N, 10, N, N, N, N, N, N, N)),
+        ("narde_reset", (N, N, N)),
+        ("narde_legal_full", (N, N, N, N)),
+        ("narde_legal_mask576_move2", (N, N, N, N, N)),
+        ("narde_dqn_transition", (N, N, N, N, N, N, N, 1, N, N, N, N, N, N, N, N, 16, N)),
+        ("narde_policy_masked_argmax576", (0, N, 576, N, 16, 0.1, 0, 0, 0, N, N)),
+        ("narde_policy_masked_argmax576_dev", (0, N, 576, N, 16, N, 0, N, 0, N, 0, N, N, N)),
+        ("narde_violates_block_rule", (0, N, 4, N, N)),
+        ("narde_per_sample", (0, N, N, 100, 64, 0, N, N, 0.001, N, N, N, N, N)),
+        ("narde_gather_batch", (0, N, 64, 198, N, N, N, N, N, N, N, N, N, N, N)),
+        ("narde_rowmax_addend", (0, N, 576, N, 576, N, 64, N, N)),
+        ("narde_dqn_loss", (0, N, N, N, N, N, N, N, 64, 0.99, N, N, N, N, N, N)),
+        ("narde_prio_update", (0, N, N, 64, 0.01, N, N, N, 0.01, 0.995, N)),
+        ("narde_adam_clip", (0, 0, N, N, N, N, N, N, 1e-3, 0.9, 0.999, 1e-8, 10.0, N, N)),
+    ]
+    for name, args in cases:
+        rc = getattr(lib, name)(*args)
+        assert rc == -1, f"{name} returned {rc}"
+        assert lib.narde_last_error(), name
