@@ -14,7 +14,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "libnarde_oracle.so")
+# NARDE_ORACLE_LIB: an alternative build of the same source (tools/sanitize.sh)
+LIB_PATH = os.environ.get("NARDE_ORACLE_LIB", os.path.join(HERE, "build", "libnarde_oracle.so"))
 MAXM = 64
 OFF = 24
 

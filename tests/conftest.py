@@ -26,7 +26,8 @@ def hostcheck():
     """Test-only host build of the device rules engine (tests/hostcheck)."""
     import ctypes
 
-    path = os.path.join(ROOT, "tests", "hostcheck", "build", "libhostcheck.so")
+    path = os.environ.get("NARDE_HOSTCHECK_LIB",  # tools/sanitize.sh: an ASan/UBSan build
+                          os.path.join(ROOT, "tests", "hostcheck", "build", "libhostcheck.so"))
     if not os.path.exists(path):
         import __graft_entry__ as g
 
