@@ -106,13 +106,16 @@ def load_traffic(path, envs, plies):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10000)
-    ap.add_argument("--warmup", type=int, default=1000)
+    # 200 launches of 1,000 plies timed, after 100 untimed: the device needs
+    # ~100 back-to-back 0.14-ms launches to reach its sustained rate
+    # (tools/diag/ramp_rollout.py)
+    ap.add_argument("--steps", type=int, default=200000)
+    ap.add_argument("--warmup", type=int, default=100000)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--plies-per-launch", type=int, default=100)
+    ap.add_argument("--plies-per-launch", type=int, default=1000)
     ap.add_argument("--api-steps", type=int, default=200)
-    ap.add_argument("--fused-plies", type=int, default=100)
+    ap.add_argument("--fused-plies", type=int, default=1000)
     ap.add_argument("--fused-launches", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--cpu-cores", type=int, default=min(16, os.cpu_count() or 1))
@@ -155,19 +158,15 @@ def main():
     P = max(1, min(args.plies_per_launch, args.steps))
     bufs = env.rollout_buffers(P)
 
-    def run_plies(k, events=None):
+    def run_plies(k):
+        launches = []
         done = 0
         while done < k:
             p = min(P, k - done)
-            if events is not None:
-                s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                s_.record()
-                env.rollout(p, bufs)
-                e_.record()
-                events.append((s_, e_, p))
-            else:
-                env.rollout(p, bufs)
+            env.rollout(p, bufs)
+            launches.append(p)
             done += p
+        return launches
 
     run_plies(args.warmup)
     torch.cuda.synchronize()
@@ -175,16 +174,25 @@ def main():
     torch.cuda.synchronize()
 
     K = args.steps
-    events = []
+    # HIP events on the launching stream around the launches of the timed
+    # region (no per-launch event between them): kernel time per launch =
+    # that span / launches, i.e. the launches' durations plus the gaps
+    # between them (an upper bound on the dispatch duration rocprof shows)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    run_plies(K, events)
+    ev0.record()
+    launches = run_plies(K)
+    ev1.record()
     stats = D.gather_stats(env.stats())
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    full = [(s_, e_) for s_, e_, p in events if p == P]
-    kern_ms = sum(s_.elapsed_time(e_) for s_, e_ in full) / max(1, len(full))
+    span_ms = ev0.elapsed_time(ev1)
+    # algorithmic bytes of every launch in the span (a last partial launch
+    # included), and the mean duration of a full-length launch
+    span_bytes = sum(launch_bytes(per, p, is_full4) for p in launches)
+    kern_ms = span_ms * launch_bytes(per, P, is_full4) / span_bytes
 
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:
@@ -328,7 +336,7 @@ def main():
 
     if rank == 0:
         nbytes = launch_bytes(per, P, is_full4)
-        achieved = nbytes / (kern_ms * 1e-3) / 1e9
+        achieved = nbytes / (kern_ms * 1e-3) / 1e9  # = span bytes / span time (max over ranks)
         tj = args.traffic_json or os.path.join(
             ROOT, "profiles", "pmc_k_rollout_full.json" if is_full4 else "pmc_k_rollout.json")
         traffic = load_traffic(tj, per, P)

@@ -34,7 +34,13 @@
 
 // DIAGNOSTIC ablations (timing only; results are wrong): FULL4 turn bits
 // 1 no first-sub-move pass, 2 no later doubles passes, 4 all turns treated as
-// block-free; REF2 consumer bits 8 no obs arithmetic, 16 no Philox
+// block-free; REF2 consumer bits 8 no obs arithmetic, 16 no Philox; REF2
+// k_rollout_pc bits 32 rule waves skip the rules (results from the draws
+// only), 64 consumers compute everything but issue no global store
+#ifndef NARDE_DIAG_CLOCK
+#define NARDE_DIAG_CLOCK 0
+#endif
+
 #ifndef NARDE_DIAG_ABLATE
 #define NARDE_DIAG_ABLATE 0
 #endif

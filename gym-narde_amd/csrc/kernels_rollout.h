@@ -28,8 +28,18 @@ struct StepArgs {
   Outs out;
 };
 
+// (DIAGNOSTIC bit 64: a store guarded by a condition the compiler cannot
+// fold but that never holds at run time)
+#if NARDE_DIAG_ABLATE & 64
+__device__ int g_diag_never;
+#define NARDE_DIAG_STORE_GUARD if (g_diag_never != 12345) return;
+#else
+#define NARDE_DIAG_STORE_GUARD
+#endif
+
 template <class T>
 __device__ __forceinline__ void st_out(T* p, T v) {
+  NARDE_DIAG_STORE_GUARD
 #if NARDE_OBS_STORE == 2
   __builtin_nontemporal_store(v, p);
 #else
@@ -37,6 +47,7 @@ __device__ __forceinline__ void st_out(T* p, T v) {
 #endif
 }
 __device__ __forceinline__ void st_out(int4* p, int4 v) {
+  NARDE_DIAG_STORE_GUARD
 #if NARDE_OBS_STORE == 2
   typedef int v4i __attribute__((ext_vector_type(4)));
   const v4i x = {v.x, v.y, v.z, v.w};
@@ -317,10 +328,21 @@ __device__ __forceinline__ void pc_emit(const PcLds& L, int slot, int np, int p0
   }
 }
 
+// DIAGNOSTIC (-DNARDE_DIAG_CLOCK=1 builds only): per workgroup, wave 0's
+// (s_memtime, s_memrealtime) at entry and exit of the last k_rollout_pc
+// launch, for the in-kernel clock (MI355X_MICROARCH.md, DVFS give-back
+// item 6).  Read by narde_diag_clock; no output depends on it.
+#if NARDE_DIAG_CLOCK
+__device__ unsigned long long g_diag_clock[4096][4];
+#endif
+
 template <bool kOut>
 __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng g, int plies,
                                                            int max_steps, Outs out) {
   __shared__ PcLds L;
+#if NARDE_DIAG_CLOCK
+  const unsigned long long clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool producer = wave < 4;
 #if NARDE_PC_PRIO == 1
@@ -376,7 +398,14 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
           ply_words(rv.x, rv.y, g.dice_mode, r);
           StepOut o;
           int term, trunc;
+#if NARDE_DIAG_ABLATE & 32
+          o.l1.L[0] = r[1] & MASK24; o.l1.L[1] = r[2] & MASK24; o.l1.d[0] = 6; o.l1.d[1] = 1; o.l1.n = 2;
+          o.code1 = (int)(r[1] >> 23); o.code2 = (int)(r[2] >> 23); o.reward = 0; o.term = 0;
+          term = 0; trunc = 0;
+          s.own.w[0] ^= r[1]; s.opp.w[1] ^= r[2]; s.t += 1u;
+#else
           env_ply(s, st, r, false, 0, 0, g.dice_mode, true, 0, 0, max_steps, true, o, term, trunc);
+#endif
           if (kOut) pc_put(L, b & 1, k, le, s, o, term, trunc);
         };
 #if NARDE_PC_UNROLL
@@ -408,6 +437,13 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
     pl.p1[i] = rb;
     add_stats(pl.stats, i, st);
   }
+#if NARDE_DIAG_CLOCK
+  if (threadIdx.x == 0 && blockIdx.x < 4096) {
+    const unsigned long long clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    g_diag_clock[blockIdx.x][0] = clk0; g_diag_clock[blockIdx.x][1] = clk1;
+    g_diag_clock[blockIdx.x][2] = rt0; g_diag_clock[blockIdx.x][3] = rt1;
+  }
+#endif
 }
 
 }  // namespace

@@ -636,3 +636,14 @@ int narde_host_violates_block_rule(narde_env* e, int64_t n, const int8_t* boards
 }
 
 }  // extern "C"
+
+#if NARDE_DIAG_CLOCK
+// DIAGNOSTIC builds only (not in include/narde.h): copy the clock stamps of
+// the last k_rollout_pc launch, int64[4096][4] = {memtime0, memtime1,
+// realtime0, realtime1} per workgroup.
+extern "C" int narde_diag_clock(unsigned long long* host_out) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_diag_clock), sizeof(g_diag_clock)));
+  return NARDE_OK;
+}
+#endif

@@ -412,21 +412,27 @@ NARDE_FN void decode_action(int code, int& f, int& t) {
 }
 
 // execute_rotated_move in mover perspective (narde.py:36-56,108-125)
+// Straight-line (no divergent branch around the bear-off case): a bear-off
+// adds nothing to the board (delta 0, empty target bit) and one to off_own.
+// count==1 mask: the source's bit flips iff it held 1 or 2 checkers, the
+// target's iff it held 0 or 1 (it can never hold the source's checkers:
+// t < f).
 NARDE_FN void apply_move(Side& s, int f, int t) {
+  const bool off = t == OFF;
+  const int tq = off ? 0 : t;
   const uint32_t cf = nib_get(s.own, f);
-  nib_dec(s.own, f);
+  const uint32_t ct = nib_get(s.own, tq);
   const uint32_t bf = 1u << f;
-  s.O = cf == 1u ? (s.O & ~bf) : s.O;
-  s.S1o = cf == 1u ? (s.S1o & ~bf) : (cf == 2u ? (s.S1o | bf) : s.S1o);
-  if (t == OFF) {
-    s.off_own += 1u;
-  } else {
-    const uint32_t ct = nib_get(s.own, t);
-    nib_inc(s.own, t);
-    const uint32_t bt = 1u << t;
-    s.O |= bt;
-    s.S1o = ct == 0u ? (s.S1o | bt) : (ct == 1u ? (s.S1o & ~bt) : s.S1o);
-  }
+  const uint32_t bt = off ? 0u : (1u << tq);
+  const uint32_t vf = 0xFFFFFFFFu << (4 * (f & 7));
+  const uint32_t vt = (off ? 0u : 1u) << (4 * (tq & 7));
+  const int kf = f >> 3, kt = tq >> 3;
+  s.own.w[0] += (kf == 0 ? vf : 0u) + (kt == 0 ? vt : 0u);
+  s.own.w[1] += (kf == 1 ? vf : 0u) + (kt == 1 ? vt : 0u);
+  s.own.w[2] += (kf == 2 ? vf : 0u) + (kt == 2 ? vt : 0u);
+  s.O = (s.O & (cf == 1u ? ~bf : ~0u)) | bt;
+  s.S1o ^= (cf - 1u < 2u ? bf : 0u) ^ (ct < 2u ? bt : 0u);
+  s.off_own += off ? 1u : 0u;
   s.ft_own = 0u;
 }
 
@@ -461,7 +467,8 @@ NARDE_FN void env_step(Side& s, int d0, int d1, int code1, int code2, bool polic
   if (policy) {
     // the drawn entry is its own code; decode(encode(f, t)) differs from (f, t)
     // only for a normal move (f, 0) with f <= 5, which decodes to (f, 'off')
-    legal2_entry(o.l1, n1 >= 2 ? (int)mulhi_u32(r1, (uint32_t)n1) : 0, f1, t1);
+    // (mulhi(r1, n1) is 0 for n1 <= 1: no branch around it)
+    legal2_entry(o.l1, (int)mulhi_u32(r1, (uint32_t)n1), f1, t1);
     code1 = n1 >= 2 ? encode_move(f1, t1) : 0;
     code2 = 0;
     play1 = n1 >= 1;
@@ -479,7 +486,8 @@ NARDE_FN void env_step(Side& s, int d0, int d1, int code1, int code2, bool polic
   if (play1) apply_move(s, f1, t1);
   if (n1 >= 2 && play1) {
     // die bookkeeping, narde_env.py:63-83: remove dist if rolled, else pop(0)
-    const int dist = t1 == OFF ? f1 + 1 : (f1 > t1 ? f1 - t1 : t1 - f1);
+    // (a played move is a listed one: t1 = f1 - die < f1, so |f1 - t1| = f1 - t1)
+    const int dist = t1 == OFF ? f1 + 1 : f1 - t1;
     const int rem = (d0 == dist) ? d1 : ((d1 == dist) ? d0 : d1);
     // second get_valid_moves([rem]) (:88): one die, first_turn already cleared
     const Blocks bl = block_info_low(s.O, low);

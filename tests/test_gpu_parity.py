@@ -230,18 +230,19 @@ def test_full_batch_subset_and_invariants():
 
 
 def test_bench_launch_window_and_invariants():
-    """The exact launch bench.py times (k_rollout_pc<true>: B = 65,536, 100
-    plies, every output), twice: a 2,048-env window of every output equals
-    the oracle on those global ids; over the whole batch the outputs obey
-    the rules' invariants (at most 15 checkers a side, reward only on a
-    finished game (1 or 2), no truncation within 200 plies of a fresh start)."""
-    B, P, seed, lo, m = 65536, 100, 99, 50000, 2048
+    """The exact launch bench.py times (k_rollout_pc<true>: B = 65,536, 1,000
+    plies, every output), then a 100-ply one: a 2,048-env window of every
+    output equals the oracle on those global ids; over the whole batch the
+    outputs obey the rules' invariants (at most 15 checkers a side, reward
+    only on a finished game (1 or 2), no truncation: no random game lasts
+    1,000 plies)."""
+    B, seed, lo, m = 65536, 99, 50000, 2048
     env = vec(B, seed=seed)
-    bufs = env.rollout_buffers(P)
     ref = O.SelfPlay(m, seed=seed, env0=lo)
     ref.reset(0)
     sl = slice(lo, lo + m)
-    for _ in range(2):
+    for P in (1000, 100):
+        bufs = env.rollout_buffers(P)
         env.rollout(P, bufs)
         rec = ref.run(P)
         assert np.array_equal(np_(bufs["obs"][:, sl]), rec["obs"].astype(np.int32))
@@ -257,8 +258,9 @@ def test_bench_launch_window_and_invariants():
         assert bool(((rew == 0) | (((rew == 1) | (rew == 2)) & term)).all())
         assert bool((rew[term] > 0).all())
         assert not bool(trunc.any())
+        del bufs, obs, rew, term, trunc
     assert np.array_equal(np_(env.stats())[sl], ref.stats)
-    assert env.ply == 2 * P
+    assert env.ply == 1100
 
 
 def test_sharded_handles_equal_single():

@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--write", required=True, help="dir of the WRITE_SIZE pass")
     ap.add_argument("--kernel", default="k_rollout_pc<true>")
     ap.add_argument("--envs", type=int, default=65536)
-    ap.add_argument("--plies", type=int, default=100)
+    ap.add_argument("--plies", type=int, default=1000)
     ap.add_argument("--bytes-per-ply", type=int, default=114, help="114 REF2, 118 FULL4")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles",
                                                   "pmc_k_rollout.json"))

@@ -23,8 +23,8 @@ from gym_narde.vector import VecNardeEnv  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=65536)
-    ap.add_argument("--plies", type=int, default=100)
-    ap.add_argument("--launches", type=int, default=5)
+    ap.add_argument("--plies", type=int, default=1000)
+    ap.add_argument("--launches", type=int, default=3)
     ap.add_argument("--rules", choices=("ref2", "full4"), default="ref2")
     a = ap.parse_args()
     env = VecNardeEnv(a.envs, device="cuda:0", seed=0, rules=a.rules)
