@@ -15,9 +15,13 @@
 //      every wave-instruction touches ~48 partial 128-B lines);
 //   1: the wave transposes its 64 rows (6 KiB) through LDS so each
 //      wave-instruction stores one contiguous 1 KiB (8 whole lines);
-//   2: as 1 with non-temporal (streaming) stores for every per-ply output.
+//   2: as 1 with non-temporal (streaming) stores for every per-ply output;
+//   3: non-temporal obs only; 4: non-temporal narrow outputs only.
+// Sustained 1,000-ply REF2 rollouts (tools/diag/gpu_sus_libs.sh, one box):
+// 1 and 4 0.1265 ms per 100 plies, 2 and 3 0.135 -- non-temporal obs
+// stores cost 6 %.
 #ifndef NARDE_OBS_STORE
-#define NARDE_OBS_STORE 2
+#define NARDE_OBS_STORE 1
 #endif
 
 // wave priority in k_rollout_pc: 0 none (age decides), 1 consumers first,

@@ -40,7 +40,7 @@ __device__ int g_diag_never;
 template <class T>
 __device__ __forceinline__ void st_out(T* p, T v) {
   NARDE_DIAG_STORE_GUARD
-#if NARDE_OBS_STORE == 2
+#if NARDE_OBS_STORE == 2 || NARDE_OBS_STORE == 4
   __builtin_nontemporal_store(v, p);
 #else
   *p = v;
@@ -48,7 +48,7 @@ __device__ __forceinline__ void st_out(T* p, T v) {
 }
 __device__ __forceinline__ void st_out(int4* p, int4 v) {
   NARDE_DIAG_STORE_GUARD
-#if NARDE_OBS_STORE == 2
+#if NARDE_OBS_STORE == 2 || NARDE_OBS_STORE == 3
   typedef int v4i __attribute__((ext_vector_type(4)));
   const v4i x = {v.x, v.y, v.z, v.w};
   __builtin_nontemporal_store(x, reinterpret_cast<v4i*>(p));
@@ -262,21 +262,23 @@ constexpr int kPcR = NARDE_PC_R;                       // plies per barrier bloc
 
 struct PcLds {
   uint2 draw[2][kPcR][kPcEnvs];               // the ply's (wa, wb) per env and ply
-  uint4 res[2][kPcR][3][kPcEnvs];             // ply results (kOut only)
+  // ply results (kOut only), structure-of-arrays (a wave's reads of one
+  // field are contiguous; 1 % faster than three uint4 per env, and 8 KiB
+  // less LDS):
+  uint4 nib0[2][kPcR][kPcEnvs];               // {own w0, own w1, own w2, opp w0}
+  uint2 nib1[2][kPcR][kPcEnvs];               // {opp w1, opp w2}  (next mover's view)
+  uint2 legal[2][kPcR][kPcEnvs];              // compact legal set (lo, hi)
+  uint2 cf[2][kPcR][kPcEnvs];                 // {code1 | code2 << 16, reward | term << 8 | trunc << 16}
 };
 
-// results of one ply of one env, as the consumers read them:
-//   res[.][.][0] = {own w0, own w1, own w2, opp w0}  (next mover's view)
-//   res[.][.][1] = {opp w1, opp w2, legal lo, legal hi}
-//   res[.][.][2] = {code1 | code2 << 16, reward | term << 8 | trunc << 16, 0, 0}
 __device__ __forceinline__ void pc_put(PcLds& L, int slot, int k, int le, const Side& s,
                                        const StepOut& o, int term, int trunc) {
   const uint64_t lg = compact_legal(o.l1);
-  L.res[slot][k][0][le] = make_uint4(s.own.w[0], s.own.w[1], s.own.w[2], s.opp.w[0]);
-  L.res[slot][k][1][le] = make_uint4(s.opp.w[1], s.opp.w[2], (uint32_t)lg, (uint32_t)(lg >> 32));
-  L.res[slot][k][2][le] =
-      make_uint4(((uint32_t)(uint16_t)o.code1) | ((uint32_t)(uint16_t)o.code2 << 16),
-                 (uint32_t)o.reward | ((uint32_t)term << 8) | ((uint32_t)trunc << 16), 0u, 0u);
+  L.nib0[slot][k][le] = make_uint4(s.own.w[0], s.own.w[1], s.own.w[2], s.opp.w[0]);
+  L.nib1[slot][k][le] = make_uint2(s.opp.w[1], s.opp.w[2]);
+  L.legal[slot][k][le] = make_uint2((uint32_t)lg, (uint32_t)(lg >> 32));
+  L.cf[slot][k][le] = make_uint2(((uint32_t)(uint16_t)o.code1) | ((uint32_t)(uint16_t)o.code2 << 16),
+                                 (uint32_t)o.reward | ((uint32_t)term << 8) | ((uint32_t)trunc << 16));
 }
 
 // consumer: outputs of plies p0 .. p0+np-1 for the 64 envs of consumer wave cw
@@ -298,12 +300,11 @@ __device__ __forceinline__ void pc_emit(const PcLds& L, int slot, int np, int p0
         if (g0 + el >= n) continue;
         const int wi = qq >> 1, sh = (qq & 1) * 16;
         // read only the two words this quad needs: own word wi is dword wi
-        // of group 0, opponent word wi is dword 3 of group 0 or wi - 1 of
-        // group 1 (2 x ds_read_b32 instead of 2 x ds_read_b128)
-        const uint32_t* g0w = reinterpret_cast<const uint32_t*>(&L.res[slot][k][0][e0 + el]);
-        const uint32_t* g1w = reinterpret_cast<const uint32_t*>(&L.res[slot][k][1][e0 + el]);
-        const uint32_t own = g0w[wi];
-        const uint32_t opp = wi == 0 ? g0w[3] : g1w[wi - 1];
+        // of nib0, opponent word wi is dword 3 of nib0 or wi - 1 of nib1
+        const uint32_t* n0w = reinterpret_cast<const uint32_t*>(&L.nib0[slot][k][e0 + el]);
+        const uint32_t* n1w = reinterpret_cast<const uint32_t*>(&L.nib1[slot][k][e0 + el]);
+        const uint32_t own = n0w[wi];
+        const uint32_t opp = wi == 0 ? n0w[3] : n1w[wi - 1];
         int4 v;
 #if NARDE_DIAG_ABLATE & 8
         st_out(dst + j, make_int4(own, opp, 0, 0)); continue;
@@ -316,13 +317,13 @@ __device__ __forceinline__ void pc_emit(const PcLds& L, int slot, int np, int p0
       }
     }
     if (mine) {
-      const uint4 b = L.res[slot][k][1][e0 + lane];
-      const uint4 c = L.res[slot][k][2][e0 + lane];
+      const uint2 lg = L.legal[slot][k][e0 + lane];
+      const uint2 c = L.cf[slot][k][e0 + lane];
       const size_t ix = row0 + lane;
       if (out.reward) st_out(out.reward + ix, (int32_t)(c.y & 0xFFu));
       if (out.term) st_out(out.term + ix, (uint8_t)((c.y >> 8) & 1u));
       if (out.trunc) st_out(out.trunc + ix, (uint8_t)((c.y >> 16) & 1u));
-      if (out.legal) st_out(out.legal + ix, (uint64_t)b.z | ((uint64_t)b.w << 32));
+      if (out.legal) st_out(out.legal + ix, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
       if (out.act_out) st_out(reinterpret_cast<uint32_t*>(out.act_out) + ix, c.x);
     }
   }

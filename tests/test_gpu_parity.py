@@ -160,11 +160,18 @@ def test_rollout_vs_oracle_and_step(n):
     leave partial workgroups and waves (ragged tails)."""
     seed, env0 = 0xABCDEF, 777
     env = vec(n, seed=seed, env_id_offset=env0, max_episode_steps=150)
+    stepper = vec(n, seed=seed, env_id_offset=env0, max_episode_steps=150)
     ref = O.SelfPlay(n, seed=seed, env0=env0, max_steps=150)
     ref.reset(0)
     for plies in (1, 64, 235):
         rec = ref.run(plies)
         bufs = env.rollout(plies)
+        # the compact legal sets and codes, bit for bit, against the per-ply
+        # API kernel (k_step), whose outputs are per env (no packed rows)
+        for p in range(plies):
+            _, _, _, _, info = stepper.step()
+            assert np.array_equal(np_(bufs["legal"][p]), np_(info["legal"])), p
+            assert np.array_equal(np_(bufs["actions"][p]), np_(info["actions"])), p
         assert np.array_equal(np_(bufs["obs"]), rec["obs"].astype(np.int32))
         assert np.array_equal(np_(bufs["reward"]), rec["reward"].astype(np.int32))
         assert np.array_equal(np_(bufs["terminated"]), rec["terminated"])
