@@ -40,7 +40,9 @@
 // 1 no first-sub-move pass, 2 no later doubles passes, 4 all turns treated as
 // block-free; REF2 consumer bits 8 no obs arithmetic, 16 no Philox; REF2
 // k_rollout_pc bits 32 rule waves skip the rules (results from the draws
-// only), 64 consumers compute everything but issue no global store
+// only), 64 consumers compute everything but issue no global store; FULL4
+// pass tasks 128 skip the doubles search, 256 skip the pair check; REF2
+// k_rollout_pc 512 consumers store the obs rows only
 #ifndef NARDE_DIAG_CLOCK
 #define NARDE_DIAG_CLOCK 0
 #endif

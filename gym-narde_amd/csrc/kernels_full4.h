@@ -92,6 +92,9 @@ __device__ void coop_run(CoopLds& W, const Side& s, uint32_t low, int a, int b, 
       const int thl = (int)((prm >> 8) & 15u) - 1, tneed = (int)((prm >> 12) & 15u);
       const bool tbf = (prm >> 16) & 1u;
       if ((prm >> 17) & 1u) {
+#if NARDE_DIAG_ABLATE & 256
+        if (true) { atomicOr(&W.res[ow][which], 1u << p); continue; }  // DIAGNOSTIC: no pair checks
+#endif
         const int ta = which ? pb : pa, tb = which ? pa : pb;
         uint32_t O2, S2;
         child_masks(c, p, ta, O2, S2);
@@ -108,6 +111,9 @@ __device__ void coop_run(CoopLds& W, const Side& s, uint32_t low, int a, int b, 
           const int lb = f4_chain_bound(O2, S2, c.P, pa, hl2);
           dep = lb >= tneed ? tneed : 0;
         }
+#if NARDE_DIAG_ABLATE & 128
+        dep = tneed;  // DIAGNOSTIC timing only: no doubles search in the passes
+#endif
         if (dep < tneed) {
           apply_die(c, p, pa);
           dep = tneed == 1 ? f4_depth<1>(c, lw, pa, hl2, tbf)
@@ -137,8 +143,11 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   // first sub-move: the lists, the shortcuts, then every lane's checks at once
   const uint32_t Lh = legal1(s, low, dh, bf);
   const uint32_t Ll = dbl ? 0u : legal1(s, low, dl, bf);
-  const bool all_h = !dbl && bf && f4_lower_bound(s.O, s.S1o, s.P, dl, 1) >= 2;
-  const bool all_l = !dbl && bf && f4_lower_bound(s.O, s.S1o, s.P, dh, 1) >= 2;
+  // two dice, block-free: the pair checks of every source from the masks
+  // (f4_keep_pair_bf) -- only non-block-free lanes publish pair tasks
+  const bool pbf = !dbl && bf;
+  const uint32_t kh = pbf ? f4_keep_pair_bf(s.O, s.S1o, s.P, dh, dl, Lh) : 0u;
+  const uint32_t kl = pbf ? f4_keep_pair_bf(s.O, s.S1o, s.P, dl, dh, Ll) : 0u;
   const int hl0 = (dbl && s.ft_own && (dh == 3 || dh == 4 || dh == 6)) ? 2 : 1;
   const bool fast = dbl && bf && f4_lower_bound(s.O, s.S1o, s.P, dh, hl0) >= 4;
   // not fast: a chain bound >= 7 still keeps every first sub-move (one
@@ -153,8 +162,8 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   uint32_t r0[3];
   {
     const bool pair = !dbl;
-    const uint32_t m0 = pair ? (all_h ? 0u : Lh) : (srch ? Lh : 0u);
-    const uint32_t m1 = pair ? (all_l ? 0u : Ll) : 0u;
+    const uint32_t m0 = pair ? (bf ? 0u : Lh) : (srch ? Lh : 0u);
+    const uint32_t m1 = pair ? (bf ? 0u : Ll) : 0u;
 #if NARDE_DIAG_ABLATE & 3
     r0[0] = Lh; r0[1] = Ll; r0[2] = Lh;  // DIAGNOSTIC timing only: wrong results
     (void)m0; (void)m1; (void)pair;
@@ -165,8 +174,8 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   uint32_t Ch, Cl;
   int M;
   if (!dbl) {
-    Ch = all_h ? Lh : r0[0];
-    Cl = all_l ? Ll : r0[1];
+    Ch = bf ? kh : r0[0];
+    Cl = bf ? kl : r0[1];
     if (Ch | Cl) {
       M = 2;
     } else {

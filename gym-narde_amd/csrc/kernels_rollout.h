@@ -316,7 +316,11 @@ __device__ __forceinline__ void pc_emit(const PcLds& L, int slot, int np, int p0
         st_out(dst + j, v);
       }
     }
+#if NARDE_DIAG_ABLATE & 512
+    if (false) {  // DIAGNOSTIC timing only: obs rows only
+#else
     if (mine) {
+#endif
       const uint2 lg = L.legal[slot][k][e0 + lane];
       const uint2 c = L.cf[slot][k][e0 + lane];
       const size_t ix = row0 + lane;

@@ -544,6 +544,28 @@ constexpr uint32_t HEAD = 1u << 23;
 // ~80 % of doubles turns of random self-play.
 NARDE_FN uint32_t land_step(uint32_t S, uint32_t P, int d) { return (S >> d) & ~P; }
 
+// 6-windows (bit i = points i..i+5) holding at most k (2 or 4) points that
+// are not own: a bit-sliced count of the holes over the six shifted masks
+NARDE_FN uint32_t windows_few_holes(uint32_t O, int k) {
+  const uint32_t h = ~O & MASK24;
+  uint32_t s0 = 0u, s1 = 0u, s2 = 0u;  // 3-bit counter per window start
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    const uint32_t x = h >> j;
+    const uint32_t c0 = s0 & x;
+    s0 ^= x;
+    const uint32_t c1 = s1 & c0;
+    s1 ^= c0;
+    s2 |= c1;
+  }
+  return k >= 4 ? ~(s2 & (s1 | s0)) : ~s2 & ~(s1 & s0);
+}
+
+// A window can only fill during the turn if the turn's landings can cover
+// its holes: each sub-move adds at most one new own point, so a window the
+// block rule could see full has at most 2 (two dice) or 4 (doubles) holes
+// in O.  (turn_block_free keeps only allowed windows inside U that pass
+// this count.)
 NARDE_FN bool turn_block_free(uint32_t O, uint32_t P, uint32_t low, int dh, int dl) {
   uint32_t U;
   if (dh == dl) {
@@ -558,7 +580,7 @@ NARDE_FN bool turn_block_free(uint32_t O, uint32_t P, uint32_t low, int dh, int 
     const uint32_t A = O | land_step(O, P, dh) | land_step(O, P, dl);
     U = A | land_step(A, P, dh) | land_step(A, P, dl);
   }
-  return (runs6(U) & low) == 0u;
+  return (runs6(U) & low & windows_few_holes(O, dh == dl ? 4 : 2)) == 0u;
 }
 
 // get_valid_moves([d], mover) (narde.py:58-92 with one die: the head filter
@@ -784,6 +806,38 @@ NARDE_FN uint32_t f4_keep_pair(const Side& s, uint32_t low, int a, int b, uint32
   return C;
 }
 
+// f4_keep_pair for a block-free turn, all sources at once (no per-source
+// loop).  After first move p -> q = p - a (a bear-off if q < 0), the
+// child's die-b list (get_valid_moves([b]) on it: no block filter can bite)
+// is non-empty iff one of:
+//   E1  a die-b normal source of the current board survives: X = O's normal
+//       b-sources; p leaves X only if it held one checker (S1), and after a
+//       head move (p = 23) the head cannot move again (one head move a turn);
+//   E2  the landed checker moves on: q >= b and q - b is not an opponent
+//       point (q is own after the move whatever it held);
+//   E3  a bear-off with b: bear-off is allowed on the child (all own
+//       checkers home: already so, or p was the single checker outside and
+//       lands home) and some own checker sits below b -- one from the
+//       current board (p only if it held >= 2) or the landed one (q < b).
+// `nz1(Y, S1)`: the sources p for which Y minus {p if S1(p)} is non-empty.
+NARDE_FN uint32_t nz1(uint32_t Y, uint32_t S1) {
+  const int c = __builtin_popcount(Y);
+  return c >= 2 ? MASK24 : (c == 1 ? (~(Y & S1) & MASK24) : 0u);
+}
+NARDE_FN uint32_t f4_keep_pair_bf(uint32_t O, uint32_t S1, uint32_t P, int a, int b, uint32_t L) {
+  const uint32_t G = ~(P << b) & (MASK24 << b) & MASK24;  // y: y - b on the board, not an opponent point
+  const uint32_t X = O & G;
+  const uint32_t e1 = (nz1(X, S1) & ~HEAD) | (((X & ~HEAD) != 0u) ? HEAD : 0u);
+  const uint32_t e2 = (G << a) & MASK24;                  // p: q = p - a in G (so q >= b >= 1)
+  const uint32_t LB = (1u << b) - 1u;
+  const uint32_t out = O & ~0x3Fu;
+  // home after the move: already home, or p = the lone outside checker landing home
+  const uint32_t homep = out == 0u ? MASK24
+                         : ((out & (out - 1u)) == 0u && (out & S1) != 0u && __builtin_ctz(out) - a < 6 ? out : 0u);
+  const uint32_t e3 = homep & (nz1(O & LB, S1) | ((LB << a) & MASK24));  // own below b, or q in [0, b)
+  return L & (e1 | e2 | e3);
+}
+
 struct TurnOut {
   uint64_t legal;   // C_0: C_hi | C_lo<<24 | d_hi<<48 | d_lo<<52 | M<<56
   uint64_t played;  // byte 2k = from, 2k+1 = die of sub-move k; 0xFF = none
@@ -815,14 +869,11 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, con
   int M = 0;
   if (dh != dl) {
     const uint32_t Lh = legal1(s, low, dh, bf), Ll = legal1(s, low, dl, bf);
-    // block-free: a first move lowers the other die's lower bound by at most
-    // one, so a bound >= 2 keeps every first move (no per-source loop)
-    const bool all_h = bf && f4_lower_bound(s.O, s.S1o, s.P, dl, 1) >= 2;
-    const bool all_l = bf && f4_lower_bound(s.O, s.S1o, s.P, dh, 1) >= 2;
-    // (lanes that skip pass an empty mask: the wave's loop runs only as long
-    // as the lanes that need it)
-    uint32_t Ch = all_h ? Lh : f4_keep_pair(s, low, dh, dl, all_h ? 0u : Lh, bf);
-    uint32_t Cl = all_l ? Ll : f4_keep_pair(s, low, dl, dh, all_l ? 0u : Ll, bf);
+    // block-free: every source at once from the masks (f4_keep_pair_bf);
+    // else the per-source loop (lanes that skip pass an empty mask: the
+    // wave's loop runs only as long as the lanes that need it)
+    uint32_t Ch = bf ? f4_keep_pair_bf(s.O, s.S1o, s.P, dh, dl, Lh) : f4_keep_pair(s, low, dh, dl, bf ? 0u : Lh, bf);
+    uint32_t Cl = bf ? f4_keep_pair_bf(s.O, s.S1o, s.P, dl, dh, Ll) : f4_keep_pair(s, low, dl, dh, bf ? 0u : Ll, bf);
     if (Ch | Cl) {
       M = 2;
     } else {
