@@ -193,3 +193,54 @@ void hc_selfplay_full(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int p
 }
 
 }  // extern "C"
+
+// f4_keep_pair_bf (all sources from the masks) against f4_keep_pair (the
+// per-source child check) on n random block-free two-dice positions, both
+// dice orders; random boards with a split-home / head-heavy / endgame mix.
+// Returns the number of mismatches; *nontrivial = checks where C != L.
+extern "C" int64_t hc_pair_bf_random(int64_t n, uint32_t seed, int64_t* nontrivial) {
+  uint64_t x = 0x9E3779B97F4A7C15ull ^ seed;
+  auto rnd = [&x](uint32_t m) {  // xorshift64*, value in [0, m)
+    x ^= x >> 12; x ^= x << 25; x ^= x >> 27;
+    return (uint32_t)(((x * 0x2545F4914F6CDD1Dull) >> 32) % m);
+  };
+  int64_t bad = 0, nt = 0, done = 0;
+  while (done < n) {
+    Side s = side_start(0u);
+    for (int k = 0; k < 3; ++k) { s.own.w[k] = 0u; s.opp.w[k] = 0u; }
+    const uint32_t mode = rnd(4);
+    const int off = mode == 3 ? (int)rnd(14) : 0;
+    int left = 15 - off;
+    uint32_t used = 0u;
+    while (left > 0) {
+      int p = mode >= 2 ? (int)rnd(8) : (int)rnd(24);
+      if (mode == 1 && rnd(3) == 0) p = 23;
+      const int c = 1 + (int)rnd(left < 4 ? left : 4);
+      for (int j = 0; j < c; ++j) nib_inc(s.own, p);
+      used |= 1u << p;
+      left -= c;
+    }
+    for (int lo = 15; lo > 0;) {
+      const int p = (int)rnd(24);
+      if ((used >> p) & 1u) continue;
+      nib_inc(s.opp, p);
+      --lo;
+    }
+    s.off_own = (uint32_t)off;
+    side_masks(s);
+    const int a = 1 + (int)rnd(6), b = 1 + (int)rnd(6);
+    if (a == b) continue;
+    const uint32_t low = block_lowmask(s.P);
+    if (!turn_block_free(s.O, s.P, low, a > b ? a : b, a > b ? b : a)) continue;
+    ++done;
+    for (int w = 0; w < 2; ++w) {
+      const int u = w ? b : a, v = w ? a : b;
+      const uint32_t L = legal1(s, low, u, true);
+      const uint32_t ref = f4_keep_pair(s, low, u, v, L, true);
+      bad += ref != f4_keep_pair_bf(s.O, s.S1o, s.P, u, v, L);
+      nt += ref != L;
+    }
+  }
+  *nontrivial = nt;
+  return bad;
+}

@@ -180,3 +180,15 @@ def test_oracle_full4_selfplay_invariants():
     assert np.array_equal(nplayed.astype(np.int64), M)
     # FULL4 games are shorter than REF2 ones (doubles move 4 checkers)
     assert sp.stats[:, 0].sum() > 0
+
+
+def test_hostcheck_pair_bf_matches_per_source(hostcheck):
+    """Block-free two-dice turns: the all-sources mask form of the pair check
+    (narde_rules.h f4_keep_pair_bf) equals the per-source child check
+    (f4_keep_pair) on 300,000 random positions x both dice orders."""
+    f = hostcheck.hc_pair_bf_random
+    f.restype = ctypes.c_int64
+    nt = ctypes.c_int64(0)
+    bad = f(ctypes.c_int64(300000), ctypes.c_uint32(7), ctypes.byref(nt))
+    assert bad == 0
+    assert nt.value > 10000  # the check removes first moves often enough to matter
