@@ -43,12 +43,13 @@
 // only), 64 consumers compute everything but issue no global store; FULL4
 // pass tasks 128 skip the doubles search, 256 skip the pair check; REF2
 // k_rollout_pc 512 consumers store the obs rows only
-#ifndef NARDE_DIAG_CLOCK
-#define NARDE_DIAG_CLOCK 0
-#endif
-
 #ifndef NARDE_DIAG_ABLATE
 #define NARDE_DIAG_ABLATE 0
+#endif
+
+// DIAGNOSTIC in-kernel clock stamps of k_rollout_pc (narde_diag_clock)
+#ifndef NARDE_DIAG_CLOCK
+#define NARDE_DIAG_CLOCK 0
 #endif
 
 namespace {

@@ -155,9 +155,13 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   const int cb0 = (dbl && bf && !fast) ? f4_chain_bound(s.O, s.S1o, s.P, dh, hl0) : 0;
   // block-free with bear-off fixed: M exactly from the chains and every
   // C_k = L_k (f4_exact_moves) -- ~3/4 of the doubles turns the bounds miss
-  const bool exact = dbl && bf && !fast && cb0 < 7 && Lh != 0u && f4_bearoff_fixed(s);
-  const int Mx = exact ? f4_exact_moves(s, dh, hl0) : 0;
-  const bool srch = dbl && !fast && Lh != 0u && cb0 < 7 && !exact;
+  const bool cand = dbl && bf && !fast && cb0 < 7 && Lh != 0u;
+  const bool exact = cand && f4_bearoff_fixed(s);
+  const int Mx = cand ? f4_exact_moves(s, dh, hl0) : 0;
+  // block-free, bear-off not allowed yet: >= 4 normal chain steps give M = 4
+  // and every C_k = L_k (env_turn_full's ex4)
+  const bool ex4 = cand && !exact && Mx >= 4;
+  const bool srch = dbl && !fast && Lh != 0u && cb0 < 7 && !exact && !ex4;
   // one cooperative pass for every lane's first-sub-move checks
   uint32_t r0[3];
   {
@@ -185,7 +189,7 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
     }
   } else {
     Cl = 0u;
-    if (fast || (cb0 >= 7 && Lh)) { Ch = Lh; M = 4; }
+    if (fast || ex4 || (cb0 >= 7 && Lh)) { Ch = Lh; M = 4; }
     else if (!Lh) { Ch = 0u; M = 0; }
     else if (exact) { Ch = Lh; M = Mx; }
     else if (r0[2]) { Ch = r0[2]; M = 4; }  // some source leaves 3 more
@@ -226,9 +230,13 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
     uint32_t Lk = act ? legal1(s, low, dk, bf) : 0u;
     if (hl <= 0) Lk &= ~HEAD;
     const int need = M - k - 1;
-    const bool direct = !dbl || fast || exact || need <= 0 ||
-                        (act && bf && (f4_bearoff_fixed(s, need + 1) ||
-                                       f4_chain_bound(s.O, s.S1o, s.P, dk, hl) >= need + 4));
+    bool direct = !dbl || fast || exact || ex4 || need <= 0;
+    // the bounds only where a lane would otherwise search (rare): a
+    // wave-uniform test keeps the other waves off them
+    const bool maybe = act && bf && !direct;
+    if (__ballot(maybe) != 0ull)
+      direct = direct || (maybe && (f4_bearoff_fixed(s, need + 1) ||
+                                    f4_chain_bound(s.O, s.S1o, s.P, dk, hl) >= need + 4));
     uint32_t rk[3];
 #if NARDE_DIAG_ABLATE & 2
     rk[0] = rk[1] = rk[2] = Lk;

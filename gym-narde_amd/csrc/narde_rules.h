@@ -931,7 +931,12 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, con
     const bool fast = bf && f4_lower_bound(s.O, s.S1o, s.P, d, hl) >= 4;
     // block-free with bear-off fixed: M exactly from the chains, every C_k = L_k
     const bool exact = !fast && bf && f4_bearoff_fixed(s);
-    if (fast) {
+    // block-free, bear-off not allowed yet (so every listed sub-move is a
+    // normal one): >= 4 normal chain steps (f4_exact_moves counts no
+    // bear-off then) give M = 4, and a normal sub-move lowers that count by
+    // at most one, so every C_k = L_k (bear-off opening later only adds)
+    const bool ex4 = !fast && !exact && bf && L && f4_exact_moves(s, d, hl) >= 4;
+    if (fast || ex4) {
       C = L;
       M = 4;
     } else if (exact) {
@@ -951,7 +956,7 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, con
         if (hl <= 0) L &= ~HEAD;
         // block-free with bear-off fixed for the rest of the turn: every
         // legal sub-move lowers the exact chain count by one (f4_exact_moves)
-        const bool direct = fast || exact || (bf && f4_bearoff_fixed(s, M - k));
+        const bool direct = fast || exact || ex4 || (bf && f4_bearoff_fixed(s, M - k));
         C = direct ? L : f4_keep_rt(s, low, d, hl, L, M - k - 1, bf);
       }
       int p;

@@ -192,3 +192,30 @@ def test_hostcheck_pair_bf_matches_per_source(hostcheck):
     bad = f(ctypes.c_int64(300000), ctypes.c_uint32(7), ctypes.byref(nt))
     assert bad == 0
     assert nt.value > 10000  # the check removes first moves often enough to matter
+
+
+def test_hostcheck_full4_random_positions(hostcheck):
+    """Run-heavy and bear-off positions for both colours, random first-turn
+    flags, half doubles: the host engine's turn (block-free shortcuts, mask
+    pair checks, exact chain counts, then the search) equals the oracle's
+    exhaustive composition on C_0, M, the played sub-moves and the board."""
+    from fuzz_positions import random_positions
+
+    n = 6000
+    b, off, ft, pl, rng = random_positions(n, 303)
+    d0 = rng.integers(1, 7, n)
+    d1 = np.where(rng.random(n) < 0.5, d0, rng.integers(1, 7, n))
+    dice = np.stack([d0, d1], 1).astype(np.uint8)
+    words = rng.integers(0, 2 ** 32, (n, 4), dtype=np.uint64).astype(np.uint32)
+    ro = O.full4_turn(b, off, ft, pl, dice, words)
+    legal = np.empty(n, np.uint64)
+    played = np.empty(n, np.uint64)
+    rw = np.empty(n, np.int8)
+    dn = np.empty(n, np.uint8)
+    b2, off2, ft2 = b.copy(), off.copy(), ft.copy()
+    hostcheck.hc_full4_batch(ctypes.c_int64(n), P(b2), P(off2), P(ft2), P(pl), P(dice), P(words),
+                             P(legal), P(played), P(rw), P(dn))
+    assert np.array_equal(legal, compact_c0({"dice": dice, "cmask": ro["cmask"], "max_dice": ro["max_dice"]}))
+    assert np.array_equal(played, played_u64(ro["played"]))
+    assert np.array_equal(b2, ro["board"]) and np.array_equal(off2, ro["off"])
+    assert all((ro["max_dice"] == m).any() for m in range(5))
