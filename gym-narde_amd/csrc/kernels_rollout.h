@@ -82,10 +82,19 @@ __device__ __forceinline__ void store_obs_wave(int32_t* __restrict__ obs, size_t
   __builtin_amdgcn_wave_barrier();
 }
 
+// obs rows through the wave's LDS slice (whole 1-KiB store instructions) or
+// straight from each lane (6 x 16 B at a 96-B lane stride).  FULL4 takes
+// the direct path: its turn is issue-bound far below the store rate, and the
+// LDS round trip costs more than the scattered stores (sustained 1,000-ply
+// rollouts, one box: 0.592 vs 0.614 ms per 100 plies); REF2's k_step keeps
+// the LDS path (6.1 vs 6.7 us per launch).
+#ifndef NARDE_FULL4_OBS_LDS
+#define NARDE_FULL4_OBS_LDS 0
+#endif
 __device__ __forceinline__ void store_common(const Outs& out, size_t ix, const Side& s, int reward,
-                                             int term, int trunc, int4* lds, bool wave_full) {
+                                             int term, int trunc, int4* lds, bool via_lds) {
   if (out.obs) {
-    if (NARDE_OBS_STORE != 0 && wave_full) store_obs_wave(out.obs, ix, s, lds);
+    if (via_lds) store_obs_wave(out.obs, ix, s, lds);
     else store_obs(out.obs, ix, s);
   }
   if (out.reward) st_out(out.reward + ix, (int32_t)reward);
@@ -96,7 +105,7 @@ __device__ __forceinline__ void store_common(const Outs& out, size_t ix, const S
 __device__ __forceinline__ void store_outs(const Outs& out, size_t ix, const Side& s,
                                            const StepOut& o, int term, int trunc, int4* lds,
                                            bool wave_full) {
-  store_common(out, ix, s, o.reward, term, trunc, lds, wave_full);
+  store_common(out, ix, s, o.reward, term, trunc, lds, NARDE_OBS_STORE != 0 && wave_full);
   if (out.legal) st_out(out.legal + ix, (uint64_t)compact_legal(o.l1));
   if (out.act_out)
     st_out(reinterpret_cast<uint32_t*>(out.act_out) + ix,
@@ -106,7 +115,8 @@ __device__ __forceinline__ void store_outs(const Outs& out, size_t ix, const Sid
 __device__ __forceinline__ void store_outs(const Outs& out, size_t ix, const Side& s,
                                            const TurnOut& o, int term, int trunc, int4* lds,
                                            bool wave_full) {
-  store_common(out, ix, s, o.reward, term, trunc, lds, wave_full);
+  store_common(out, ix, s, o.reward, term, trunc, lds,
+               NARDE_FULL4_OBS_LDS && NARDE_OBS_STORE != 0 && wave_full);
   if (out.legal) st_out(out.legal + ix, o.legal);
   if (out.played) st_out(out.played + ix, o.played);
 }
