@@ -43,6 +43,86 @@ __device__ __forceinline__ int wave_prefix(int x, int lane, int& total) {
   return excl;
 }
 
+// The same pass transposed (for at most NARDE_COOP_XPOSE owners): no task list.
+// The wave walks the lanes that have checks (a scalar loop over a ballot);
+// for each such owner its state is broadcast with v_readlane and every lane
+// takes one source of the owner's masks (lanes 0-23: m0 bit `lane`, lanes
+// 32-55: m1 bit `lane - 32`); the results come back as ballots.  No LDS,
+// no prefix sums, no per-bit task-writing loop: a wave with few owners --
+// ~2 on a ply, often none in the later sub-moves -- pays per owner, not a
+// fixed pass.
+#ifndef NARDE_COOP_XPOSE
+#define NARDE_COOP_XPOSE 2
+#endif
+__device__ __forceinline__ uint32_t rl(uint32_t v, int l) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ void coop_run_x(const Side& s, uint32_t low, int a, int b, int hl, uint32_t m0, uint32_t m1,
+                           int need, bool bf, int mode, int lane, uint32_t out[3]) {
+  out[0] = out[1] = out[2] = 0u;
+  uint64_t owners = __ballot((m0 | m1) != 0u);
+  const int which = lane >> 5, p = lane & 31;
+  while (owners) {
+    const int ow = (int)__builtin_ctzll(owners);
+    owners &= owners - 1ull;
+    // the owner's state and parameters (wave-uniform from here on)
+    Side c;
+    c.own.w[0] = rl(s.own.w[0], ow); c.own.w[1] = rl(s.own.w[1], ow); c.own.w[2] = rl(s.own.w[2], ow);
+    c.O = rl(s.O, ow); c.S1o = rl(s.S1o, ow); c.P = rl(s.P, ow);
+    c.off_own = rl(s.off_own, ow);
+    c.opp.w[0] = c.opp.w[1] = c.opp.w[2] = 0u;
+    c.S1p = 0u; c.off_opp = 0u; c.ft_own = 0u; c.ft_opp = 0u; c.black = 0u; c.elapsed = 0u; c.t = 0u;
+    const uint32_t lw = rl(low, ow), om0 = rl(m0, ow), om1 = rl(m1, ow);
+    const int pa = (int)rl((uint32_t)a, ow), pb = (int)rl((uint32_t)b, ow);
+    const int thl = (int)rl((uint32_t)hl, ow), tneed = (int)rl((uint32_t)need, ow);
+    const bool tbf = rl(bf ? 1u : 0u, ow) != 0u;
+    const bool pair = rl((uint32_t)mode, ow) != 0u;
+    const uint32_t m = which == 0 ? om0 : (which == 1 ? om1 : 0u);
+    const bool has = p < 24 && ((m >> p) & 1u);
+    bool k0 = false, k1 = false, k2 = false;
+    if (pair) {
+      if (has) {
+        const int ta = which ? pb : pa, tb = which ? pa : pb;
+        uint32_t O2, S2;
+        child_masks(c, p, ta, O2, S2);
+        uint32_t L2 = die_candidates(O2, c.P, tb);
+        if (!tbf) L2 = die_filter(O2, S2, block_info_low(O2, lw), L2, tb);
+        if (p == 23) L2 &= ~HEAD;
+        k0 = L2 != 0u;
+      }
+      const uint64_t r = __ballot(k0);
+      const uint32_t r0 = (uint32_t)r & MASK24, r1 = (uint32_t)(r >> 32) & MASK24;
+      out[0] = lane == ow ? r0 : out[0];
+      out[1] = lane == ow ? r1 : out[1];
+    } else {
+      if (has) {
+        const int hl2 = thl - (p == 23 ? 1 : 0);
+        int dep = 0;
+        if (tbf) {
+          uint32_t O2, S2;
+          child_masks(c, p, pa, O2, S2);
+          const int lb = f4_chain_bound(O2, S2, c.P, pa, hl2);
+          dep = lb >= tneed ? tneed : 0;
+        }
+#if NARDE_DIAG_ABLATE & 128
+        dep = tneed;  // DIAGNOSTIC timing only: no doubles search in the passes
+#endif
+        if (dep < tneed) {
+          Side cc = c;
+          apply_die(cc, p, pa);
+          dep = tneed == 1 ? f4_depth<1>(cc, lw, pa, hl2, tbf)
+                           : (tneed == 2 ? f4_depth<2>(cc, lw, pa, hl2, tbf) : f4_depth<3>(cc, lw, pa, hl2, tbf));
+        }
+        k0 = dep >= 1; k1 = dep >= 2; k2 = dep >= 3;
+      }
+      const uint32_t r0 = (uint32_t)__ballot(k0), r1 = (uint32_t)__ballot(k1), r2 = (uint32_t)__ballot(k2);
+      out[0] = lane == ow ? r0 : out[0];
+      out[1] = lane == ow ? r1 : out[1];
+      out[2] = lane == ow ? r2 : out[2];
+    }
+  }
+}
+
 // One cooperative pass over every lane's per-source checks.  Per lane:
 //   mode 1 (pair, two dice a = d_hi, b = d_lo): m0 = first moves with a,
 //     kept (res 0) iff b still has a move after them; m1 = first moves with
@@ -53,7 +133,15 @@ __device__ __forceinline__ int wave_prefix(int x, int lane, int& total) {
 __device__ void coop_run(CoopLds& W, const Side& s, uint32_t low, int a, int b, int hl, uint32_t m0,
                          uint32_t m1, int need, bool bf, int mode, int lane, uint32_t out[3]) {
   out[0] = out[1] = out[2] = 0u;
-  if (__ballot((m0 | m1) != 0u) == 0ull) return;  // wave-uniform: nothing to check
+  const uint64_t any = __ballot((m0 | m1) != 0u);
+  if (any == 0ull) return;  // wave-uniform: nothing to check
+#if NARDE_COOP_XPOSE
+  // few owners: the transposed walk; many: one packed task list
+  if (__builtin_popcountll(any) <= NARDE_COOP_XPOSE) {
+    coop_run_x(s, low, a, b, hl, m0, m1, need, bf, mode, lane, out);
+    return;
+  }
+#endif
   const int c0 = __builtin_popcount(m0), cnt = c0 + __builtin_popcount(m1);
   int total;
   const int off = wave_prefix(cnt, lane, total);
