@@ -261,7 +261,12 @@ __global__ void __launch_bounds__(kBlock) k_rollout(Planes pl, int n, Rng g, int
 #ifndef NARDE_PC_SETS
 #define NARDE_PC_SETS 1
 #endif
-constexpr int kPcEnvs = 256;                  // envs per workgroup
+// rule (producer) waves per workgroup, each with its consumer wave(s)
+#ifndef NARDE_PC_GROUPS
+#define NARDE_PC_GROUPS 4
+#endif
+constexpr int kPcGroups = NARDE_PC_GROUPS;
+constexpr int kPcEnvs = 64 * kPcGroups;        // envs per workgroup
 constexpr int kPcSets = NARDE_PC_SETS;        // consumer waves per producer wave
 constexpr int kPcThreads = (1 + kPcSets) * kPcEnvs;  // producers + consumers
 // plies per barrier block (tuning knob: 3, 4 and 5 time the same)
@@ -359,16 +364,16 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
   const unsigned long long clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const bool producer = wave < 4;
+  const bool producer = wave < kPcGroups;
 #if NARDE_PC_PRIO == 1
   if (!producer) __builtin_amdgcn_s_setprio(1);
 #elif NARDE_PC_PRIO == 2
   if (producer) __builtin_amdgcn_s_setprio(1);
 #endif
-  const int le = (wave & 3) * 64 + lane;            // workgroup-local env
+  const int le = (wave % kPcGroups) * 64 + lane;    // workgroup-local env
   // consumer set: with kPcSets > 1 the consumer waves of one env group split
   // the plies of each block (set c takes plies k = c, c + kPcSets, ...)
-  const int cset = producer ? 0 : (wave - 4) >> 2;
+  const int cset = producer ? 0 : (wave - kPcGroups) / kPcGroups;
   const int wg_env0 = blockIdx.x * kPcEnvs;
   const int i = wg_env0 + le;
   const bool valid = i < n;
@@ -437,13 +442,13 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
     } else {
       if (b + 1 < nb) draw_block(b + 1);
       if (kOut && b > 0)
-        pc_emit(L, (b - 1) & 1, kPcR, p0 - kPcR, n, wg_env0, wave & 3, lane, out, cset, kPcSets);
+        pc_emit(L, (b - 1) & 1, kPcR, p0 - kPcR, n, wg_env0, wave % kPcGroups, lane, out, cset, kPcSets);
     }
     __syncthreads();
   }
   if (kOut && !producer && nb > 0) {
     const int p0 = (nb - 1) * kPcR;
-    pc_emit(L, (nb - 1) & 1, plies - p0, p0, n, wg_env0, wave & 3, lane, out, cset, kPcSets);
+    pc_emit(L, (nb - 1) & 1, plies - p0, p0, n, wg_env0, wave % kPcGroups, lane, out, cset, kPcSets);
   }
   if (producer && valid) {
     uint4 ra, rb;
