@@ -275,15 +275,35 @@ constexpr int kPcThreads = (1 + kPcSets) * kPcEnvs;  // producers + consumers
 #endif
 constexpr int kPcR = NARDE_PC_R;                       // plies per barrier block
 
+// Ring slots and the synchronisation of the two roles:
+//   NARDE_PC_FLAGS 0: one workgroup barrier per block, 2 slots;
+//   NARDE_PC_FLAGS 1: each rule wave and its consumer wave (they share
+//     only their own 64 env columns) hand blocks over through three LDS
+//     counters -- drawn, produced, emitted -- with NARDE_PC_SLOTS slots, so
+//     neither role waits for the other pairs.  Bit-exact, but slower:
+//     sustained 1,000-ply rollouts 0.139 (3 slots) / 0.139-0.143 (2) against
+//     0.1315 ms per 100 plies with the barrier on the same box -- the
+//     workgroup-wide lockstep keeps the CU's output stream better formed.
+//     Kept as an A/B knob (default 0).
+#ifndef NARDE_PC_FLAGS
+#define NARDE_PC_FLAGS 0
+#endif
+#ifndef NARDE_PC_SLOTS
+#define NARDE_PC_SLOTS (NARDE_PC_FLAGS ? 3 : 2)
+#endif
+constexpr int kPcSlots = NARDE_PC_SLOTS;
+static_assert(!NARDE_PC_FLAGS || kPcSets == 1, "flag hand-over needs one consumer wave per rule wave");
+static_assert(NARDE_PC_FLAGS || kPcSlots == 2, "barrier hand-over uses two slots");
+
 struct PcLds {
-  uint2 draw[2][kPcR][kPcEnvs];               // the ply's (wa, wb) per env and ply
+  uint2 draw[kPcSlots][kPcR][kPcEnvs];        // the ply's (wa, wb) per env and ply
   // ply results (kOut only), structure-of-arrays (a wave's reads of one
   // field are contiguous; 1 % faster than three uint4 per env, and 8 KiB
   // less LDS):
-  uint4 nib0[2][kPcR][kPcEnvs];               // {own w0, own w1, own w2, opp w0}
-  uint2 nib1[2][kPcR][kPcEnvs];               // {opp w1, opp w2}  (next mover's view)
-  uint2 legal[2][kPcR][kPcEnvs];              // compact legal set (lo, hi)
-  uint2 cf[2][kPcR][kPcEnvs];                 // {code1 | code2 << 16, reward | term << 8 | trunc << 16}
+  uint4 nib0[kPcSlots][kPcR][kPcEnvs];               // {own w0, own w1, own w2, opp w0}
+  uint2 nib1[kPcSlots][kPcR][kPcEnvs];               // {opp w1, opp w2}  (next mover's view)
+  uint2 legal[kPcSlots][kPcR][kPcEnvs];              // compact legal set (lo, hi)
+  uint2 cf[kPcSlots][kPcR][kPcEnvs];                 // {code1 | code2 << 16, reward | term << 8 | trunc << 16}
 };
 
 __device__ __forceinline__ void pc_put(PcLds& L, int slot, int k, int le, const Side& s,
@@ -356,6 +376,25 @@ __device__ __forceinline__ void pc_emit(const PcLds& L, int slot, int np, int p0
 __device__ unsigned long long g_diag_clock[4096][4];
 #endif
 
+// flag hand-over (NARDE_PC_FLAGS): wait until *f >= target (wave-uniform
+// spin with s_sleep; bounded, so a logic error can never hang the device --
+// it would show as wrong results in the parity tests instead)
+__device__ __forceinline__ void pc_wait(volatile uint32_t* f, int target) {
+  if (target <= 0) return;
+  for (int guard = 0; guard < (1 << 21); ++guard) {
+    if (__builtin_amdgcn_readfirstlane((int)*f) >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // no LDS access hoisted above the wait
+}
+// publish *f = v once this wave's LDS reads and writes have retired
+__device__ __forceinline__ void pc_signal(volatile uint32_t* f, int v) {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: stores to HBM stay in flight
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  *f = (uint32_t)v;
+}
+
 template <bool kOut>
 __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng g, int plies,
                                                            int max_steps, Outs out) {
@@ -402,9 +441,57 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
       if (k == cset || (t & 1u) == 0u || kPcSets > 1) ply_block(t, g.env0 + (uint32_t)i, g.k0, g.k1, R);
 #endif
       const bool odd = (t & 1u) != 0u;
-      L.draw[b & 1][k][le] = odd ? make_uint2(R[2], R[3]) : make_uint2(R[0], R[1]);
+      L.draw[b % kPcSlots][k][le] = odd ? make_uint2(R[2], R[3]) : make_uint2(R[0], R[1]);
     }
   };
+  // one ply of the rule wave: block b's draw k, results into b's slot
+  auto one_ply = [&](int b, int k) {
+    const uint2 rv = L.draw[b % kPcSlots][k][le];
+    uint32_t r[4];
+    ply_words(rv.x, rv.y, g.dice_mode, r);
+    StepOut o;
+    int term, trunc;
+#if NARDE_DIAG_ABLATE & 32
+    o.l1.L[0] = r[1] & MASK24; o.l1.L[1] = r[2] & MASK24; o.l1.d[0] = 6; o.l1.d[1] = 1; o.l1.n = 2;
+    o.code1 = (int)(r[1] >> 23); o.code2 = (int)(r[2] >> 23); o.reward = 0; o.term = 0;
+    term = 0; trunc = 0;
+    s.own.w[0] ^= r[1]; s.opp.w[1] ^= r[2]; s.t += 1u;
+#else
+    env_ply(s, st, r, false, 0, 0, g.dice_mode, true, 0, 0, max_steps, true, o, term, trunc);
+#endif
+    if (kOut) pc_put(L, b % kPcSlots, k, le, s, o, term, trunc);
+  };
+#if NARDE_PC_FLAGS
+  __shared__ uint32_t flag_drawn[kPcGroups], flag_prod[kPcGroups], flag_emit[kPcGroups];
+  const int pr = wave % kPcGroups;  // this wave's pair
+  if (producer) flag_prod[pr] = 0u;
+  else { flag_drawn[pr] = 0u; flag_emit[pr] = 0u; }
+  __syncthreads();  // the one workgroup barrier: counters initialised
+  if (producer) {
+    for (int b = 0; b < nb; ++b) {
+      const int np = min(kPcR, plies - b * kPcR);
+      pc_wait(&flag_drawn[pr], b + 1);                     // block b's draws written
+      if (kOut) pc_wait(&flag_emit[pr], b + 1 - kPcSlots);  // the slot's last results read
+      if (valid)
+        for (int k = 0; k < np; ++k) one_ply(b, k);
+      pc_signal(&flag_prod[pr], b + 1);
+    }
+  } else {
+    for (int j = 0; j <= nb; ++j) {
+      if (j < nb) {
+        pc_wait(&flag_prod[pr], j + 1 - kPcSlots);  // the slot's last draws read
+        draw_block(j);
+        pc_signal(&flag_drawn[pr], j + 1);
+      }
+      if (kOut && j >= 1) {
+        const int p0 = (j - 1) * kPcR;
+        pc_wait(&flag_prod[pr], j);  // block j - 1's results written
+        pc_emit(L, (j - 1) % kPcSlots, min(kPcR, plies - p0), p0, n, wg_env0, pr, lane, out, 0, 1);
+        pc_signal(&flag_emit[pr], j);
+      }
+    }
+  }
+#else
   if (!producer) draw_block(0);
   __syncthreads();
   for (int b = 0; b < nb; ++b) {
@@ -412,31 +499,15 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
     const int np = min(kPcR, plies - p0);
     if (producer) {
       if (valid) {
-        auto one_ply = [&](int k) {
-          const uint2 rv = L.draw[b & 1][k][le];
-          uint32_t r[4];
-          ply_words(rv.x, rv.y, g.dice_mode, r);
-          StepOut o;
-          int term, trunc;
-#if NARDE_DIAG_ABLATE & 32
-          o.l1.L[0] = r[1] & MASK24; o.l1.L[1] = r[2] & MASK24; o.l1.d[0] = 6; o.l1.d[1] = 1; o.l1.n = 2;
-          o.code1 = (int)(r[1] >> 23); o.code2 = (int)(r[2] >> 23); o.reward = 0; o.term = 0;
-          term = 0; trunc = 0;
-          s.own.w[0] ^= r[1]; s.opp.w[1] ^= r[2]; s.t += 1u;
-#else
-          env_ply(s, st, r, false, 0, 0, g.dice_mode, true, 0, 0, max_steps, true, o, term, trunc);
-#endif
-          if (kOut) pc_put(L, b & 1, k, le, s, o, term, trunc);
-        };
 #if NARDE_PC_UNROLL
         if (np == kPcR) {
 #pragma unroll
-          for (int k = 0; k < kPcR; ++k) one_ply(k);
+          for (int k = 0; k < kPcR; ++k) one_ply(b, k);
         } else {
-          for (int k = 0; k < np; ++k) one_ply(k);
+          for (int k = 0; k < np; ++k) one_ply(b, k);
         }
 #else
-        for (int k = 0; k < np; ++k) one_ply(k);
+        for (int k = 0; k < np; ++k) one_ply(b, k);
 #endif
       }
     } else {
@@ -450,6 +521,7 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
     const int p0 = (nb - 1) * kPcR;
     pc_emit(L, (nb - 1) & 1, plies - p0, p0, n, wg_env0, wave % kPcGroups, lane, out, cset, kPcSets);
   }
+#endif
   if (producer && valid) {
     uint4 ra, rb;
     side_to_record(s, ra, rb);
