@@ -318,7 +318,9 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
     uint32_t Lk = act ? legal1(s, low, dk, bf) : 0u;
     if (hl <= 0) Lk &= ~HEAD;
     const int need = M - k - 1;
-    bool direct = !dbl || fast || exact || ex4 || need <= 0;
+    // cb0 >= 7: the exact chain count is >= 7 too (the bound counts fewer
+    // checkers per point), so as for ex4 / exact every C_k = L_k
+    bool direct = !dbl || fast || exact || ex4 || cb0 >= 7 || need <= 0;
     // the bounds only where a lane would otherwise search (rare): a
     // wave-uniform test keeps the other waves off them
     const bool maybe = act && bf && !direct;
