@@ -245,10 +245,11 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   // C_k = L_k (f4_exact_moves) -- ~3/4 of the doubles turns the bounds miss
   const bool cand = dbl && bf && !fast && cb0 < 7 && Lh != 0u;
   const bool exact = cand && f4_bearoff_fixed(s);
-  const int Mx = cand ? f4_exact_moves(s, dh, hl0) : 0;
-  // block-free, bear-off not allowed yet: >= 4 normal chain steps give M = 4
-  // and every C_k = L_k (env_turn_full's ex4)
-  const bool ex4 = cand && !exact && Mx >= 4;
+  const int T0 = cand ? f4_exact_moves(s, dh, hl0) : 0;
+  // block-free, bear-off not open yet: M exactly from the chains and the
+  // bear-offs they can open, every C_k = L_k (env_turn_full's ex4)
+  const bool ex4 = cand && !exact;
+  const int Mx = ex4 ? f4_open_moves(s, dh, hl0, T0) : T0;
   const bool srch = dbl && !fast && Lh != 0u && cb0 < 7 && !exact && !ex4;
   // one cooperative pass for every lane's first-sub-move checks
   uint32_t r0[3];
@@ -277,9 +278,9 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
     }
   } else {
     Cl = 0u;
-    if (fast || ex4 || (cb0 >= 7 && Lh)) { Ch = Lh; M = 4; }
+    if (fast || (cb0 >= 7 && Lh)) { Ch = Lh; M = 4; }
     else if (!Lh) { Ch = 0u; M = 0; }
-    else if (exact) { Ch = Lh; M = Mx; }
+    else if (exact || ex4) { Ch = Lh; M = Mx; }
     else if (r0[2]) { Ch = r0[2]; M = 4; }  // some source leaves 3 more
     else if (r0[1]) { Ch = r0[1]; M = 3; }
     else if (r0[0]) { Ch = r0[0]; M = 2; }

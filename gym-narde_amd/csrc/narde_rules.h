@@ -747,6 +747,44 @@ NARDE_FN int f4_exact_moves(const Side& s, int d, int hl) {
   return t < 4 ? t : 4;
 }
 
+// Exact sub-move count of a block-free doubles turn whose bear-off is not
+// open yet (not f4_bearoff_fixed), given T = f4_exact_moves (its normal
+// steps, as bear-off is closed).  Block-free, the checkers never interact:
+// each walks its own chain of die-d steps over free landings; a chain that
+// walks below d ends with a bear-off -- but only once every own checker is
+// home, which the turn can bring about iff each outside checker's chain
+// reaches home (and every head checker may leave).  The longest turn then
+// makes all T normal steps and then the B bear-offs: M = min(4, T + B);
+// else M = min(4, T).  A sub-move lowers T + B (or T) by at most one, so
+// every C_k = L_k.  (At T >= 4, M = 4; below, every chain that matters is
+// at most 3 steps long.)
+NARDE_FN int f4_open_moves(const Side& s, int d, int hl, int T) {
+  if (T >= 4) return 4;
+  const uint32_t O = s.O, fr = ~s.P & MASK24;
+  // chains that end off the board: R0 = below d, R(k+1) = x whose landing
+  // x - d is free and in Rk
+  const uint32_t r0 = (1u << d) - 1u;
+  const uint32_t r1 = ((r0 & fr) << d) & MASK24;
+  const uint32_t r2 = ((r1 & fr) << d) & MASK24;
+  const uint32_t r3 = ((r2 & fr) << d) & MASK24;
+  const uint32_t R = (r0 | r1 | r2 | r3) & O;
+  // chains that reach home (points 0..5) within 3 steps
+  const uint32_t h1 = ((0x3Fu & fr) << d) & MASK24;
+  const uint32_t h2 = ((h1 & fr) << d) & MASK24;
+  const uint32_t h3 = ((h2 & fr) << d) & MASK24;
+  const uint32_t X = O & ~0x3Fu;  // points of the checkers outside home
+  const int head = (int)nib_get(s.own, 23);
+  if ((X & ~(h1 | h2 | h3)) != 0u || ((X & HEAD) && head > hl)) return T;
+  uint32_t ge4;
+  const uint32_t ge3 = nib_ge3_ge4(s.own, ge4);
+  const uint32_t Rb = R & ~HEAD;
+  int B = __builtin_popcount(Rb) + __builtin_popcount(Rb & ~s.S1o) + __builtin_popcount(Rb & ge3) +
+          __builtin_popcount(Rb & ge4);
+  if (R & HEAD) B += head;  // every head checker leaves (checked above)
+  const int t = T + B;
+  return t < 4 ? t : 4;
+}
+
 // the sources of L (die d) after which NEED more sub-moves stay playable:
 // block-free turns try the lower bound first, the exact search only where
 // it falls short
@@ -931,17 +969,18 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, con
     const bool fast = bf && f4_lower_bound(s.O, s.S1o, s.P, d, hl) >= 4;
     // block-free with bear-off fixed: M exactly from the chains, every C_k = L_k
     const bool exact = !fast && bf && f4_bearoff_fixed(s);
-    // block-free, bear-off not allowed yet (so every listed sub-move is a
-    // normal one): >= 4 normal chain steps (f4_exact_moves counts no
-    // bear-off then) give M = 4, and a normal sub-move lowers that count by
-    // at most one, so every C_k = L_k (bear-off opening later only adds)
-    const bool ex4 = !fast && !exact && bf && L && f4_exact_moves(s, d, hl) >= 4;
-    if (fast || ex4) {
+    // block-free, bear-off not open yet: M exactly from the chains and the
+    // bear-offs they can open (f4_open_moves), every C_k = L_k
+    const bool ex4 = !fast && !exact && bf && L;
+    if (fast) {
       C = L;
       M = 4;
     } else if (exact) {
       C = L;
       M = L ? f4_exact_moves(s, d, hl) : 0;
+    } else if (ex4) {
+      C = L;
+      M = f4_open_moves(s, d, hl, f4_exact_moves(s, d, hl));
     } else if (L) {
       C = f4_keep<3>(s, low, d, hl, L, bf);
       M = 4;

@@ -244,3 +244,57 @@ extern "C" int64_t hc_pair_bf_random(int64_t n, uint32_t seed, int64_t* nontrivi
   *nontrivial = nt;
   return bad;
 }
+
+// f4_open_moves (exact count of a block-free doubles turn whose bear-off may
+// open mid-turn, every C_k = L_k) against the depth-first search (f4_keep
+// with NEED 3, 2, 1) on n random such positions: bear-off endgames with
+// 1-3 stragglers outside home.  Returns mismatches; *raised = positions
+// where the opening bear-off raises M above the normal steps.
+extern "C" int64_t hc_open_moves_random(int64_t n, uint32_t seed, int64_t* raised) {
+  uint64_t x = 0xD1B54A32D192ED03ull ^ seed;
+  auto rnd = [&x](uint32_t m) {
+    x ^= x >> 12; x ^= x << 25; x ^= x >> 27;
+    return (uint32_t)(((x * 0x2545F4914F6CDD1Dull) >> 32) % m);
+  };
+  int64_t bad = 0, up = 0, done = 0;
+  while (done < n) {
+    Side s = side_start(0u);
+    for (int k = 0; k < 3; ++k) { s.own.w[k] = 0u; s.opp.w[k] = 0u; }
+    const int off = (int)rnd(14);
+    int strag = 1 + (int)rnd(3);
+    for (int left = 15 - off; left > 0; --left) {
+      const int p = strag > 0 ? 6 + (int)rnd(18) : (int)rnd(6);
+      if (strag > 0) --strag;
+      nib_inc(s.own, p);
+    }
+    uint32_t used = 0u;
+    for (int p = 0; p < 24; ++p) used |= nib_get(s.own, p) ? (1u << p) : 0u;
+    for (int lo = 15; lo > 0;) {
+      const int p = (int)rnd(24);
+      if ((used >> p) & 1u) continue;
+      nib_inc(s.opp, p);
+      --lo;
+    }
+    s.off_own = (uint32_t)off;
+    s.ft_own = rnd(2);
+    side_masks(s);
+    const int d = 1 + (int)rnd(6);
+    const int hl = (s.ft_own && (d == 3 || d == 4 || d == 6)) ? 2 : 1;
+    const uint32_t low = block_lowmask(s.P);
+    if (!turn_block_free(s.O, s.P, low, d, d) || f4_bearoff_fixed(s)) continue;
+    const uint32_t L = legal1(s, low, d, true);
+    if (!L) continue;
+    ++done;
+    uint32_t C = f4_keep<3>(s, low, d, hl, L, true);
+    int M = 4;
+    if (!C) { C = f4_keep<2>(s, low, d, hl, L, true); M = 3; }
+    if (!C) { C = f4_keep<1>(s, low, d, hl, L, true); M = 2; }
+    if (!C) { C = L; M = 1; }
+    const int T = f4_exact_moves(s, d, hl);
+    const int Me = f4_open_moves(s, d, hl, T);
+    bad += (Me != M || C != L);
+    up += Me > T;
+  }
+  *raised = up;
+  return bad;
+}

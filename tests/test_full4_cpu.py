@@ -219,3 +219,15 @@ def test_hostcheck_full4_random_positions(hostcheck):
     assert np.array_equal(played, played_u64(ro["played"]))
     assert np.array_equal(b2, ro["board"]) and np.array_equal(off2, ro["off"])
     assert all((ro["max_dice"] == m).any() for m in range(5))
+
+
+def test_hostcheck_open_moves_matches_search(hostcheck):
+    """Block-free doubles turns whose bear-off may open mid-turn: the exact
+    count (narde_rules.h f4_open_moves, with every C_k = L_k) equals the
+    depth-first search's M and first-sub-move set on 100,000 random
+    endgames with stragglers outside home."""
+    f = hostcheck.hc_open_moves_random
+    f.restype = ctypes.c_int64
+    up = ctypes.c_int64(0)
+    assert f(ctypes.c_int64(100000), ctypes.c_uint32(5), ctypes.byref(up)) == 0
+    assert up.value > 3000  # the opening bear-off decides often enough
