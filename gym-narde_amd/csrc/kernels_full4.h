@@ -226,7 +226,7 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
 #if NARDE_DIAG_ABLATE & 4
   const bool bf = true;  // DIAGNOSTIC timing only: wrong results
 #else
-  const bool bf = turn_block_free(s.O, s.P, low, dh, dl);
+  const bool bf = turn_block_free(s.O, s.S1o, s.P, low, dh, dl);
 #endif
   // first sub-move: the lists, the shortcuts, then every lane's checks at once
   const uint32_t Lh = legal1(s, low, dh, bf);

@@ -564,11 +564,29 @@ NARDE_FN uint32_t windows_few_holes(uint32_t O, int k) {
 // A window can only fill during the turn if the turn's landings can cover
 // its holes: each sub-move adds at most one new own point, so a window the
 // block rule could see full has at most 2 (two dice) or 4 (doubles) holes
-// in O.  (turn_block_free keeps only allowed windows inside U that pass
-// this count.)
-NARDE_FN bool turn_block_free(uint32_t O, uint32_t P, uint32_t low, int dh, int dl) {
+// in O.  The few windows that pass this count (usually none) get a sharper
+// per-window test; the window is harmless unless:
+//   * it is full already (no holes);
+//   * two dice, one hole: the hole is a landing of one die or of both in
+//     turn from a source the window can spare -- outside it, or a point of
+//     >= 2 checkers (a single checker leaving a window point leaves a hole
+//     no other sub-move is left to refill);
+//   * two dice, two holes: each hole is a single-die landing from such a
+//     source, with different dice (each sub-move fills one hole; a checker
+//     moving on from the first hole empties it again);
+//   * doubles: the holes' fewest steps from such sources sum to <= 4 (each
+//     hole's final checker walks its own steps; a single checker that
+//     leaves a window point must be replaced along the same d-chain, which
+//     reaches the hole from the replacement's origin in the same number of
+//     steps).
+// Checked against a depth-first walk of every sub-move sequence
+// (tools/diag/bf_stats.cpp, tests/hostcheck hc_block_free_random): it frees
+// ~2/3 of the two-dice and ~3/5 of the doubles turns the count alone calls
+// block-bound, and never a turn in which the rule removes a candidate.
+NARDE_FN bool turn_block_free(uint32_t O, uint32_t S1, uint32_t P, uint32_t low, int dh, int dl) {
+  const bool dbl = dh == dl;
   uint32_t U;
-  if (dh == dl) {
+  if (dbl) {
     uint32_t S = O;
     U = O;
 #pragma unroll
@@ -580,7 +598,36 @@ NARDE_FN bool turn_block_free(uint32_t O, uint32_t P, uint32_t low, int dh, int 
     const uint32_t A = O | land_step(O, P, dh) | land_step(O, P, dl);
     U = A | land_step(A, P, dh) | land_step(A, P, dl);
   }
-  return (runs6(U) & low & windows_few_holes(O, dh == dl ? 4 : 2)) == 0u;
+  uint32_t win = runs6(U) & low & windows_few_holes(O, dbl ? 4 : 2);
+  while (win) {
+    const int i = __builtin_ctz(win);
+    win &= win - 1u;
+    const uint32_t W = 0x3Fu << i;
+    const uint32_t H = W & ~O;
+    if (!H) return false;
+    const uint32_t src = O & ~(W & S1);
+    if (dbl) {
+      uint32_t T = src, seen = 0u;
+      int cost = 0;
+#pragma unroll
+      for (int k = 1; k <= 4; ++k) {
+        T = land_step(T, P, dh);
+        const uint32_t nw = H & T & ~seen;
+        cost += k * __builtin_popcount(nw);
+        seen |= nw;
+      }
+      if (seen == H && cost <= 4) return false;
+    } else {
+      const uint32_t Lh = land_step(src, P, dh), Ll = land_step(src, P, dl);
+      const uint32_t h1 = H & (0u - H), h2 = H ^ h1;
+      if (!h2) {
+        if (H & (Lh | Ll | land_step(Lh, P, dl) | land_step(Ll, P, dh))) return false;
+      } else if (((h1 & Lh) && (h2 & Ll)) || ((h1 & Ll) && (h2 & Lh))) {
+        return false;
+      }
+    }
+  }
+  return true;
 }
 
 // get_valid_moves([d], mover) (narde.py:58-92 with one die: the head filter
@@ -902,7 +949,7 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, con
                             TurnOut& o) {
   const uint32_t low = block_lowmask(s.P);
   const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
-  const bool bf = turn_block_free(s.O, s.P, low, dh, dl);
+  const bool bf = turn_block_free(s.O, s.S1o, s.P, low, dh, dl);
   uint64_t played = ~0ull;
   int M = 0;
   if (dh != dl) {

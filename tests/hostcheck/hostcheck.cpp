@@ -231,7 +231,7 @@ extern "C" int64_t hc_pair_bf_random(int64_t n, uint32_t seed, int64_t* nontrivi
     const int a = 1 + (int)rnd(6), b = 1 + (int)rnd(6);
     if (a == b) continue;
     const uint32_t low = block_lowmask(s.P);
-    if (!turn_block_free(s.O, s.P, low, a > b ? a : b, a > b ? b : a)) continue;
+    if (!turn_block_free(s.O, s.S1o, s.P, low, a > b ? a : b, a > b ? b : a)) continue;
     ++done;
     for (int w = 0; w < 2; ++w) {
       const int u = w ? b : a, v = w ? a : b;
@@ -281,7 +281,7 @@ extern "C" int64_t hc_open_moves_random(int64_t n, uint32_t seed, int64_t* raise
     const int d = 1 + (int)rnd(6);
     const int hl = (s.ft_own && (d == 3 || d == 4 || d == 6)) ? 2 : 1;
     const uint32_t low = block_lowmask(s.P);
-    if (!turn_block_free(s.O, s.P, low, d, d) || f4_bearoff_fixed(s)) continue;
+    if (!turn_block_free(s.O, s.S1o, s.P, low, d, d) || f4_bearoff_fixed(s)) continue;
     const uint32_t L = legal1(s, low, d, true);
     if (!L) continue;
     ++done;
@@ -296,5 +296,109 @@ extern "C" int64_t hc_open_moves_random(int64_t n, uint32_t seed, int64_t* raise
     up += Me > T;
   }
   *raised = up;
+  return bad;
+}
+
+// ---- turn_block_free against the rule itself ------------------------------
+// does die_filter remove a candidate at any node of the turn's sub-move tree
+// (head rule ignored: a superset of the turn's nodes)?
+static bool hc_binds_at(const Side& s, uint32_t low, int d) {
+  const uint32_t C = die_candidates(s.O, s.P, d);
+  return die_filter(s.O, s.S1o, block_info_low(s.O, low), C, d) != C;
+}
+static bool hc_binds(const Side& s, uint32_t low, int a, int b, int left) {
+  if (left == 0) return false;
+  if (hc_binds_at(s, low, a) || (b != a && hc_binds_at(s, low, b))) return true;
+  for (int k = 0; k < (a == b ? 1 : 2); ++k) {
+    const int x = k ? b : a, y = k ? a : b;
+    uint32_t L = die_candidates(s.O, s.P, x);
+    while (L) {
+      const int p = __builtin_ctz(L);
+      L &= L - 1u;
+      Side c = s;
+      apply_die(c, p, x);
+      // two dice: one sub-move with the other die is left
+      if (a == b ? hc_binds(c, low, a, a, left - 1) : hc_binds_at(c, low, y)) return true;
+    }
+  }
+  return false;
+}
+
+// n random block-prone positions (an own 6-window with 0-4 holes, the
+// opponent mostly past it so the rule applies), half doubles: a turn
+// turn_block_free calls block-free must never have the rule remove a
+// candidate.  Returns such turns; *freed = turns the hole count alone calls
+// block-bound that the per-window test frees; *bound = turns where the rule
+// really binds.
+extern "C" int64_t hc_block_free_random(int64_t n, uint32_t seed, int64_t* freed, int64_t* bound) {
+  uint64_t x = 0x94D049BB133111EBull ^ seed;
+  auto rnd = [&x](uint32_t m) {
+    x ^= x >> 12; x ^= x << 25; x ^= x >> 27;
+    return (uint32_t)(((x * 0x2545F4914F6CDD1Dull) >> 32) % m);
+  };
+  int64_t bad = 0, fr = 0, bd = 0;
+  for (int64_t done = 0; done < n; ++done) {
+    Side s = side_start(0u);
+    for (int k = 0; k < 3; ++k) { s.own.w[k] = 0u; s.opp.w[k] = 0u; }
+    const int i0 = (int)rnd(19);
+    const uint32_t W = 0x3Fu << i0;
+    const int holes = (int)rnd(5);
+    uint32_t Hm = 0u;
+    while (__builtin_popcount(Hm) < holes) Hm |= 1u << (i0 + (int)rnd(6));
+    int left = 15;
+    for (int p = i0; p < i0 + 6; ++p)
+      if (!((Hm >> p) & 1u)) {
+        const int c = 1 + (rnd(3) == 0 ? 1 : 0);
+        for (int j = 0; j < c; ++j) nib_inc(s.own, p);
+        left -= c;
+      }
+    while (left > 0) {
+      const int p = (int)rnd(24);
+      if ((Hm >> p) & 1u && rnd(2)) continue;  // keep most holes open
+      nib_inc(s.own, p);
+      --left;
+    }
+    uint32_t used = 0u;
+    for (int p = 0; p < 24; ++p) used |= nib_get(s.own, p) ? (1u << p) : 0u;
+    // opponent: mostly on points above the window (the rule applies),
+    // sometimes anywhere; a few on the holes' feeder points
+    const int lo_min = rnd(4) == 0 ? 0 : i0 + 1;
+    for (int lo = 15; lo > 0;) {
+      const int p = lo_min + (int)rnd((uint32_t)(24 - lo_min));
+      if ((used >> p) & 1u) {
+        if (lo_min > 0 && !(used & ~(MASK24 >> (24 - p)) & ~W)) { /* no free point */ }
+        bool any = false;
+        for (int q = lo_min; q < 24; ++q) any |= !((used >> q) & 1u);
+        if (!any) break;
+        continue;
+      }
+      nib_inc(s.opp, p);
+      --lo;
+    }
+    s.ft_own = 0u;
+    side_masks(s);
+    const int a = 1 + (int)rnd(6), b = rnd(2) ? a : 1 + (int)rnd(6);
+    const int dh = a > b ? a : b, dl = a > b ? b : a;
+    const uint32_t low = block_lowmask(s.P);
+    const bool bf = turn_block_free(s.O, s.S1o, s.P, low, dh, dl);
+    // the hole count alone (the test before the per-window refinement)
+    uint32_t U;
+    if (dh == dl) {
+      uint32_t S = s.O;
+      U = s.O;
+      for (int k = 0; k < 4; ++k) { S = land_step(S, s.P, dh); U |= S; }
+    } else {
+      const uint32_t A = s.O | land_step(s.O, s.P, dh) | land_step(s.O, s.P, dl);
+      U = A | land_step(A, s.P, dh) | land_step(A, s.P, dl);
+    }
+    const bool coarse = (runs6(U) & low & windows_few_holes(s.O, dh == dl ? 4 : 2)) == 0u;
+    const bool binds = hc_binds(s, low, dh, dl, dh == dl ? 4 : 2);
+    bad += bf && binds;
+    bad += coarse && !bf;  // the refinement only ever frees turns
+    fr += bf && !coarse;
+    bd += binds;
+  }
+  *freed = fr;
+  *bound = bd;
   return bad;
 }

@@ -231,3 +231,15 @@ def test_hostcheck_open_moves_matches_search(hostcheck):
     up = ctypes.c_int64(0)
     assert f(ctypes.c_int64(100000), ctypes.c_uint32(5), ctypes.byref(up)) == 0
     assert up.value > 3000  # the opening bear-off decides often enough
+
+
+def test_hostcheck_block_free_is_sound(hostcheck):
+    """turn_block_free (narde_rules.h) on 200,000 random block-prone turns:
+    a turn it calls block-free never has the block rule remove a candidate
+    anywhere in its sub-move tree (exhaustive walk), and its per-window
+    test frees many turns the hole count alone calls block-bound."""
+    f = hostcheck.hc_block_free_random
+    f.restype = ctypes.c_int64
+    fr, bd = ctypes.c_int64(0), ctypes.c_int64(0)
+    assert f(ctypes.c_int64(200000), ctypes.c_uint32(11), ctypes.byref(fr), ctypes.byref(bd)) == 0
+    assert fr.value > 5000 and bd.value > 5000

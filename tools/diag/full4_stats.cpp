@@ -70,7 +70,7 @@ int main() {
         ++two;
         const uint32_t low = block_lowmask(s.P);
         const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
-        const bool bf = turn_block_free(s.O, s.P, low, dh, dl);
+        const bool bf = turn_block_free(s.O, s.S1o, s.P, low, dh, dl);
         const uint32_t Lh = legal1(s, low, dh, bf), Ll = legal1(s, low, dl, bf);
         const bool all_h = bf && f4_lower_bound(s.O, s.S1o, s.P, dl, 1) >= 2;
         const bool all_l = bf && f4_lower_bound(s.O, s.S1o, s.P, dh, 1) >= 2;
@@ -90,7 +90,7 @@ int main() {
       if (d0 == d1) {
         ++dbl;
         const uint32_t low = block_lowmask(s.P);
-        const bool bf = turn_block_free(s.O, s.P, low, d0, d0);
+        const bool bf = turn_block_free(s.O, s.S1o, s.P, low, d0, d0);
         const int hl0 = (s.ft_own && (d0 == 3 || d0 == 4 || d0 == 6)) ? 2 : 1;
         const bool f = bf && f4_lower_bound(s.O, s.S1o, s.P, d0, hl0) >= 4;
         const int cb0 = (bf && !f) ? f4_chain_bound(s.O, s.S1o, s.P, d0, hl0) : 0;
