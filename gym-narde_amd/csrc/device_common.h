@@ -42,7 +42,8 @@
 // k_rollout_pc bits 32 rule waves skip the rules (results from the draws
 // only), 64 consumers compute everything but issue no global store; FULL4
 // pass tasks 128 skip the doubles search, 256 skip the pair check; REF2
-// k_rollout_pc 512 consumers store the obs rows only
+// k_rollout_pc 512 consumers store the obs rows only; FULL4 1024 two-dice
+// turns treated as block-free, 2048 doubles turns treated as block-free
 #ifndef NARDE_DIAG_ABLATE
 #define NARDE_DIAG_ABLATE 0
 #endif

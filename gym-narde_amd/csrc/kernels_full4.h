@@ -51,6 +51,17 @@ __device__ __forceinline__ int wave_prefix(int x, int lane, int& total) {
 // no prefix sums, no per-bit task-writing loop: a wave with few owners --
 // ~2 on a ply, often none in the later sub-moves -- pays per owner, not a
 // fixed pass.
+// levels of a pass's block-bound doubles search that first test whether
+// the node is block-free for the sub-moves it has left (f4_depth's CUT)
+#ifndef NARDE_F4_CUT
+#define NARDE_F4_CUT 0
+#endif
+// later sub-moves of a block-bound doubles turn: 0 always search, 2 stop at
+// a node block-free for the sub-moves left (1: the old block-free bounds,
+// never true since every block-free doubles lane is direct)
+#ifndef NARDE_F4_LATE
+#define NARDE_F4_LATE 0
+#endif
 #ifndef NARDE_COOP_XPOSE
 #define NARDE_COOP_XPOSE 2
 #endif
@@ -110,8 +121,8 @@ __device__ void coop_run_x(const Side& s, uint32_t low, int a, int b, int hl, ui
         if (dep < tneed) {
           Side cc = c;
           apply_die(cc, p, pa);
-          dep = tneed == 1 ? f4_depth<1>(cc, lw, pa, hl2, tbf)
-                           : (tneed == 2 ? f4_depth<2>(cc, lw, pa, hl2, tbf) : f4_depth<3>(cc, lw, pa, hl2, tbf));
+          dep = tneed == 1 ? f4_depth<1, NARDE_F4_CUT>(cc, lw, pa, hl2, tbf)
+                           : (tneed == 2 ? f4_depth<2, NARDE_F4_CUT>(cc, lw, pa, hl2, tbf) : f4_depth<3, NARDE_F4_CUT>(cc, lw, pa, hl2, tbf));
         }
         k0 = dep >= 1; k1 = dep >= 2; k2 = dep >= 3;
       }
@@ -204,8 +215,8 @@ __device__ void coop_run(CoopLds& W, const Side& s, uint32_t low, int a, int b, 
 #endif
         if (dep < tneed) {
           apply_die(c, p, pa);
-          dep = tneed == 1 ? f4_depth<1>(c, lw, pa, hl2, tbf)
-                           : (tneed == 2 ? f4_depth<2>(c, lw, pa, hl2, tbf) : f4_depth<3>(c, lw, pa, hl2, tbf));
+          dep = tneed == 1 ? f4_depth<1, NARDE_F4_CUT>(c, lw, pa, hl2, tbf)
+                           : (tneed == 2 ? f4_depth<2, NARDE_F4_CUT>(c, lw, pa, hl2, tbf) : f4_depth<3, NARDE_F4_CUT>(c, lw, pa, hl2, tbf));
         }
         for (int j = 0; j < dep; ++j) atomicOr(&W.res[ow][j], 1u << p);
       }
@@ -225,8 +236,14 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   const bool dbl = dh == dl;
 #if NARDE_DIAG_ABLATE & 4
   const bool bf = true;  // DIAGNOSTIC timing only: wrong results
+#elif NARDE_DIAG_ABLATE & 1024
+  const bool bf = dbl ? turn_block_free(s.O, s.S1o, s.P, low, dh, dl) : true;  // DIAGNOSTIC
+#elif NARDE_DIAG_ABLATE & 2048
+  const bool bf = dbl ? true : turn_block_free(s.O, s.S1o, s.P, low, dh, dl);  // DIAGNOSTIC
 #else
-  const bool bf = turn_block_free(s.O, s.S1o, s.P, low, dh, dl);
+  bool bound = false;
+  const uint32_t hs = dbl ? 0u : two_block_holes(s.O, s.S1o, s.P, low, dh, dl, bound);
+  const bool bf = dbl ? dbl_block_free(s.O, s.S1o, s.P, low, dh, 4) : !bound;
 #endif
   // first sub-move: the lists, the shortcuts, then every lane's checks at once
   const uint32_t Lh = legal1(s, low, dh, bf);
@@ -236,6 +253,14 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   const bool pbf = !dbl && bf;
   const uint32_t kh = pbf ? f4_keep_pair_bf(s.O, s.S1o, s.P, dh, dl, Lh) : 0u;
   const uint32_t kl = pbf ? f4_keep_pair_bf(s.O, s.S1o, s.P, dl, dh, Ll) : 0u;
+  // block-bound two dice: the sources sure from the masks (f4_sure_pair)
+  // need no task -- ~3/4 of these lanes have no task left
+#if NARDE_DIAG_ABLATE & (4 | 1024 | 2048)
+  const uint32_t hs = 0u;  // DIAGNOSTIC builds
+#endif
+  const bool nbf2 = !dbl && !bf;
+  const uint32_t sh = nbf2 ? f4_sure_pair(s.O, s.P, dl, Lh, hs) : 0u;
+  const uint32_t sl = nbf2 ? f4_sure_pair(s.O, s.P, dh, Ll, hs) : 0u;
   const int hl0 = (dbl && s.ft_own && (dh == 3 || dh == 4 || dh == 6)) ? 2 : 1;
   const bool fast = dbl && bf && f4_lower_bound(s.O, s.S1o, s.P, dh, hl0) >= 4;
   // not fast: a chain bound >= 7 still keeps every first sub-move (one
@@ -255,8 +280,8 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   uint32_t r0[3];
   {
     const bool pair = !dbl;
-    const uint32_t m0 = pair ? (bf ? 0u : Lh) : (srch ? Lh : 0u);
-    const uint32_t m1 = pair ? (bf ? 0u : Ll) : 0u;
+    const uint32_t m0 = pair ? (bf ? 0u : Lh & ~sh) : (srch ? Lh : 0u);
+    const uint32_t m1 = pair ? (bf ? 0u : Ll & ~sl) : 0u;
 #if NARDE_DIAG_ABLATE & 3
     r0[0] = Lh; r0[1] = Ll; r0[2] = Lh;  // DIAGNOSTIC timing only: wrong results
     (void)m0; (void)m1; (void)pair;
@@ -267,8 +292,8 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   uint32_t Ch, Cl;
   int M;
   if (!dbl) {
-    Ch = bf ? kh : r0[0];
-    Cl = bf ? kl : r0[1];
+    Ch = bf ? kh : (sh | r0[0]);
+    Cl = bf ? kl : (sl | r0[1]);
     if (Ch | Cl) {
       M = 2;
     } else {
@@ -322,12 +347,19 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
     // cb0 >= 7: the exact chain count is >= 7 too (the bound counts fewer
     // checkers per point), so as for ex4 / exact every C_k = L_k
     bool direct = !dbl || fast || exact || ex4 || cb0 >= 7 || need <= 0;
-    // the bounds only where a lane would otherwise search (rare): a
-    // wave-uniform test keeps the other waves off them
+#if NARDE_F4_LATE == 2
+    // (block-free doubles lanes are all direct already.)  A block-bound lane
+    // stops searching once its node is block-free for the need + 1 sub-moves
+    // it has left (env_turn_full): the test only in waves that have one
+    const bool maybe = act && !direct;
+    if (__ballot(maybe) != 0ull)
+      direct = direct || (maybe && dbl_block_free(s.O, s.S1o, s.P, low, dk, need + 1));
+#elif NARDE_F4_LATE == 1
     const bool maybe = act && bf && !direct;
     if (__ballot(maybe) != 0ull)
       direct = direct || (maybe && (f4_bearoff_fixed(s, need + 1) ||
                                     f4_chain_bound(s.O, s.S1o, s.P, dk, hl) >= need + 4));
+#endif
     uint32_t rk[3];
 #if NARDE_DIAG_ABLATE & 2
     rk[0] = rk[1] = rk[2] = Lk;

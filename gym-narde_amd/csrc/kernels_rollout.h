@@ -210,11 +210,19 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
 // record stays in VGPRs, each ply's outputs (if requested) are streamed to
 // [ply][n] rollout buffers.  kOut = false: statistics only (a separate
 // instantiation, so profiles tell the two apart).
+#ifndef NARDE_ROLLOUT_MINW
+#define NARDE_ROLLOUT_MINW 1
+#endif
 template <bool kOut, bool kFull>
-__global__ void __launch_bounds__(kBlock) k_rollout(Planes pl, int n, Rng g, int plies, int max_steps,
+__global__ void __launch_bounds__(kBlock, NARDE_ROLLOUT_MINW) k_rollout(Planes pl, int n, Rng g, int plies, int max_steps,
                                                     Outs out) {
   OBS_LDS_DECL
   COOP_LDS_DECL
+#ifdef NARDE_DIAG_LDS_PAD
+  // DIAGNOSTIC: LDS the kernel never uses, to cap its occupancy
+  __shared__ uint32_t diag_pad[NARDE_DIAG_LDS_PAD / 4];
+  if (n == -12345) ((volatile uint32_t*)diag_pad)[threadIdx.x] = (uint32_t)plies;
+#endif
   const int i = blockIdx.x * kBlock + threadIdx.x;
   const bool valid = i < n;
   if (!kFull && !valid) return;  // FULL4 lanes stay: its turn is wave-cooperative

@@ -583,51 +583,85 @@ NARDE_FN uint32_t windows_few_holes(uint32_t O, int k) {
 // (tools/diag/bf_stats.cpp, tests/hostcheck hc_block_free_random): it frees
 // ~2/3 of the two-dice and ~3/5 of the doubles turns the count alone calls
 // block-bound, and never a turn in which the rule removes a candidate.
-NARDE_FN bool turn_block_free(uint32_t O, uint32_t S1, uint32_t P, uint32_t low, int dh, int dl) {
-  const bool dbl = dh == dl;
-  uint32_t U;
-  if (dbl) {
-    uint32_t S = O;
-    U = O;
+// doubles: block-free for the next k (1..4) sub-moves of die d -- the same
+// test with k landings and a step budget of k (a node inside a block-bound
+// turn is often block-free for the sub-moves it has left)
+NARDE_FN bool dbl_block_free(uint32_t O, uint32_t S1, uint32_t P, uint32_t low, int d, int k) {
+  uint32_t S = O, U = O;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      S = land_step(S, P, dh);
-      U |= S;
-    }
-  } else {
-    const uint32_t A = O | land_step(O, P, dh) | land_step(O, P, dl);
-    U = A | land_step(A, P, dh) | land_step(A, P, dl);
+  for (int j = 0; j < 4; ++j) {
+    S = land_step(S, P, d);
+    U |= j < k ? S : 0u;
   }
-  uint32_t win = runs6(U) & low & windows_few_holes(O, dbl ? 4 : 2);
+  uint32_t win = runs6(U) & low & windows_few_holes(O, k > 2 ? 4 : 2);
   while (win) {
     const int i = __builtin_ctz(win);
     win &= win - 1u;
     const uint32_t W = 0x3Fu << i;
     const uint32_t H = W & ~O;
     if (!H) return false;
-    const uint32_t src = O & ~(W & S1);
-    if (dbl) {
-      uint32_t T = src, seen = 0u;
-      int cost = 0;
+    uint32_t T = O & ~(W & S1), seen = 0u;
+    int cost = 0;
 #pragma unroll
-      for (int k = 1; k <= 4; ++k) {
-        T = land_step(T, P, dh);
-        const uint32_t nw = H & T & ~seen;
-        cost += k * __builtin_popcount(nw);
-        seen |= nw;
-      }
-      if (seen == H && cost <= 4) return false;
-    } else {
-      const uint32_t Lh = land_step(src, P, dh), Ll = land_step(src, P, dl);
-      const uint32_t h1 = H & (0u - H), h2 = H ^ h1;
-      if (!h2) {
-        if (H & (Lh | Ll | land_step(Lh, P, dl) | land_step(Ll, P, dh))) return false;
-      } else if (((h1 & Lh) && (h2 & Ll)) || ((h1 & Ll) && (h2 & Lh))) {
-        return false;
-      }
+    for (int j = 1; j <= 4; ++j) {
+      T = land_step(T, P, d);
+      const uint32_t nw = j <= k ? (H & T & ~seen) : 0u;
+      cost += j * __builtin_popcount(nw);
+      seen |= nw;
     }
+    if (seen == H && cost <= k) return false;
   }
   return true;
+}
+
+// two dice: the per-window test; returns the holes (in O) of the windows
+// that fail it -- the only windows that can ever be full at a node of the
+// turn -- and sets `bound` if there is one (~0u: one of them is full already)
+NARDE_FN uint32_t two_block_holes(uint32_t O, uint32_t S1, uint32_t P, uint32_t low, int dh, int dl,
+                                  bool& bound) {
+  const uint32_t A = O | land_step(O, P, dh) | land_step(O, P, dl);
+  const uint32_t U = A | land_step(A, P, dh) | land_step(A, P, dl);
+  uint32_t win = runs6(U) & low & windows_few_holes(O, 2), hs = 0u;
+  bound = false;
+  while (win) {
+    const int i = __builtin_ctz(win);
+    win &= win - 1u;
+    const uint32_t W = 0x3Fu << i;
+    const uint32_t H = W & ~O;
+    const uint32_t src = O & ~(W & S1);
+    const uint32_t Lh = land_step(src, P, dh), Ll = land_step(src, P, dl);
+    const uint32_t h1 = H & (0u - H), h2 = H ^ h1;
+    const bool fail = !H || (!h2 ? (H & (Lh | Ll | land_step(Lh, P, dl) | land_step(Ll, P, dh))) != 0u
+                                 : (((h1 & Lh) && (h2 & Ll)) || ((h1 & Ll) && (h2 & Lh))));
+    bound = bound || fail;
+    hs |= fail ? (H ? H : ~0u) : 0u;
+  }
+  return hs;
+}
+
+NARDE_FN bool turn_block_free(uint32_t O, uint32_t S1, uint32_t P, uint32_t low, int dh, int dl) {
+  if (dh == dl) return dbl_block_free(O, S1, P, low, dh, 4);
+  bool bound;
+  two_block_holes(O, S1, P, low, dh, dl, bound);
+  return !bound;
+}
+
+// Block-bound two dice: the first moves p of die a (in La) sure to leave die
+// b a move, from the masks.  hs = two_block_holes.  A root candidate x of b
+// stays a candidate after p unless x = p; the rule can only reject a move
+// that fills the last hole of a failing window, i.e. lands on a hole in hs
+// or on p itself (a single checker leaving a window point); the head rule
+// drops x = 23 after p = 23 (x = p again).  So the candidates landing
+// outside hs ("safe") other than p and p + b survive: p is sure if one is
+// left.  On random self-play 73 % of the block-bound two-dice turns have
+// every first move sure (tools/diag/bf_stats.cpp-style count; checked
+// against f4_keep_pair in tests/hostcheck hc_sure_pair_random).
+NARDE_FN uint32_t f4_sure_pair(uint32_t O, uint32_t P, int b, uint32_t La, uint32_t hs) {
+  if (hs == ~0u) return 0u;
+  const uint32_t safe = die_candidates(O, P, b) & ~(hs << b);
+  const int c = __builtin_popcount(safe);
+  const uint32_t ok = c >= 3 ? ~0u : (c == 2 ? ~(safe & (safe >> b)) : (c == 1 ? ~(safe | (safe >> b)) : 0u));
+  return La & ok;
 }
 
 // get_valid_moves([d], mover) (narde.py:58-92 with one die: the head filter
@@ -650,48 +684,6 @@ NARDE_FN void child_masks(const Side& s, int p, int d, uint32_t& O2, uint32_t& S
     // empty -> 1 (set); 1 -> 2 (clear); >= 2 stays (bit already clear)
     S2 = (O2 & bq) ? (S2 & ~bq) : (S2 | bq);
     O2 |= bq;
-  }
-}
-
-// can N more sub-moves of die d be played (hl head moves still allowed)?
-template <int N>
-NARDE_FN bool f4_reach(const Side& s, uint32_t low, int d, int hl, bool bf) {
-  uint32_t L = legal1(s, low, d, bf);
-  if (hl <= 0) L &= ~HEAD;
-  if constexpr (N == 1) {
-    return L != 0u;
-  } else {
-    while (L) {
-      const int p = __builtin_ctz(L);
-      L &= L - 1u;
-      Side c = s;
-      apply_die(c, p, d);
-      if (f4_reach<N - 1>(c, low, d, hl - (p == 23 ? 1 : 0), bf)) return true;
-    }
-    return false;
-  }
-}
-
-// the most sub-moves of die d (up to N) playable from s: depth-first with
-// early exit at N (hl head moves still allowed)
-template <int N>
-NARDE_FN int f4_depth(const Side& s, uint32_t low, int d, int hl, bool bf) {
-  uint32_t L = legal1(s, low, d, bf);
-  if (hl <= 0) L &= ~HEAD;
-  if (!L) return 0;
-  if constexpr (N == 1) {
-    return 1;
-  } else {
-    int best = 1;
-    while (L && best < N) {
-      const int p = __builtin_ctz(L);
-      L &= L - 1u;
-      Side c = s;
-      apply_die(c, p, d);
-      const int v = 1 + f4_depth<N - 1>(c, low, d, hl - (p == 23 ? 1 : 0), bf);
-      best = v > best ? v : best;
-    }
-    return best;
   }
 }
 
@@ -832,6 +824,67 @@ NARDE_FN int f4_open_moves(const Side& s, int d, int hl, int T) {
   return t < 4 ? t : 4;
 }
 
+// Exact sub-move count of a doubles node block-free for its k remaining
+// sub-moves (dbl_block_free): the exact counts above, capped at k.  (Bear-off
+// fixed for k sub-moves: the chains alone; else f4_open_moves -- if the
+// outside checkers cannot all get home with a move to spare, T >= k already.)
+NARDE_FN int f4_bf_moves(const Side& s, int d, int hl, int k) {
+  const int T = f4_exact_moves(s, d, hl);
+  const int M = f4_bearoff_fixed(s, k) ? T : f4_open_moves(s, d, hl, T);
+  return M < k ? M : k;
+}
+
+// can N more sub-moves of die d be played (hl head moves still allowed)?
+// A block-bound search stops at the first node that is block-free for the
+// N sub-moves it has left: the exact count decides there.  (Tested on the
+// top CUT levels: a device search inlines every level, and the test at all
+// of them costs more registers than it saves.)
+template <int N, int CUT = N>
+NARDE_FN bool f4_reach(const Side& s, uint32_t low, int d, int hl, bool bf) {
+  if constexpr (CUT > 0)
+    if (!bf && dbl_block_free(s.O, s.S1o, s.P, low, d, N)) return f4_bf_moves(s, d, hl, N) >= N;
+  uint32_t L = legal1(s, low, d, bf);
+  if (hl <= 0) L &= ~HEAD;
+  if constexpr (N == 1) {
+    return L != 0u;
+  } else {
+    while (L) {
+      const int p = __builtin_ctz(L);
+      L &= L - 1u;
+      Side c = s;
+      apply_die(c, p, d);
+      if (f4_reach<N - 1, (CUT > 0 ? CUT - 1 : 0)>(c, low, d, hl - (p == 23 ? 1 : 0), bf)) return true;
+    }
+    return false;
+  }
+}
+
+// the most sub-moves of die d (up to N) playable from s: depth-first with
+// early exit at N (hl head moves still allowed); block-bound searches stop
+// at block-free nodes as f4_reach does
+template <int N, int CUT = N>
+NARDE_FN int f4_depth(const Side& s, uint32_t low, int d, int hl, bool bf) {
+  if constexpr (CUT > 0)
+    if (!bf && dbl_block_free(s.O, s.S1o, s.P, low, d, N)) return f4_bf_moves(s, d, hl, N);
+  uint32_t L = legal1(s, low, d, bf);
+  if (hl <= 0) L &= ~HEAD;
+  if (!L) return 0;
+  if constexpr (N == 1) {
+    return 1;
+  } else {
+    int best = 1;
+    while (L && best < N) {
+      const int p = __builtin_ctz(L);
+      L &= L - 1u;
+      Side c = s;
+      apply_die(c, p, d);
+      const int v = 1 + f4_depth<N - 1, (CUT > 0 ? CUT - 1 : 0)>(c, low, d, hl - (p == 23 ? 1 : 0), bf);
+      best = v > best ? v : best;
+    }
+    return best;
+  }
+}
+
 // the sources of L (die d) after which NEED more sub-moves stay playable:
 // block-free turns try the lower bound first, the exact search only where
 // it falls short
@@ -957,8 +1010,14 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, con
     // block-free: every source at once from the masks (f4_keep_pair_bf);
     // else the per-source loop (lanes that skip pass an empty mask: the
     // wave's loop runs only as long as the lanes that need it)
-    uint32_t Ch = bf ? f4_keep_pair_bf(s.O, s.S1o, s.P, dh, dl, Lh) : f4_keep_pair(s, low, dh, dl, bf ? 0u : Lh, bf);
-    uint32_t Cl = bf ? f4_keep_pair_bf(s.O, s.S1o, s.P, dl, dh, Ll) : f4_keep_pair(s, low, dl, dh, bf ? 0u : Ll, bf);
+    // block-bound: the sources sure from the masks (f4_sure_pair), the
+    // per-source check for the rest
+    bool bound;
+    const uint32_t hs = bf ? 0u : two_block_holes(s.O, s.S1o, s.P, low, dh, dl, bound);
+    const uint32_t sh = bf ? 0u : f4_sure_pair(s.O, s.P, dl, Lh, hs);
+    const uint32_t sl = bf ? 0u : f4_sure_pair(s.O, s.P, dh, Ll, hs);
+    uint32_t Ch = bf ? f4_keep_pair_bf(s.O, s.S1o, s.P, dh, dl, Lh) : (sh | f4_keep_pair(s, low, dh, dl, Lh & ~sh, bf));
+    uint32_t Cl = bf ? f4_keep_pair_bf(s.O, s.S1o, s.P, dl, dh, Ll) : (sl | f4_keep_pair(s, low, dl, dh, Ll & ~sl, bf));
     if (Ch | Cl) {
       M = 2;
     } else {
@@ -1040,9 +1099,11 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, con
       if (k > 0) {
         L = legal1(s, low, d, bf);
         if (hl <= 0) L &= ~HEAD;
-        // block-free with bear-off fixed for the rest of the turn: every
-        // legal sub-move lowers the exact chain count by one (f4_exact_moves)
-        const bool direct = fast || exact || ex4 || (bf && f4_bearoff_fixed(s, M - k));
+        // block-free turns never search; a block-bound one stops searching
+        // once the node is block-free for the M - k sub-moves it has left:
+        // on an M-path its exact count (f4_bf_moves) is >= M - k and a
+        // sub-move lowers it by at most one, so every C_k = L_k
+        const bool direct = fast || exact || ex4 || (!bf && dbl_block_free(s.O, s.S1o, s.P, low, d, M - k));
         C = direct ? L : f4_keep_rt(s, low, d, hl, L, M - k - 1, bf);
       }
       int p;

@@ -324,6 +324,24 @@ static bool hc_binds(const Side& s, uint32_t low, int a, int b, int left) {
   return false;
 }
 
+// the most sub-moves of die d (up to n) from s by the plain walk: every
+// list through die_filter, no shortcut
+static int hc_depth_plain(const Side& s, uint32_t low, int d, int hl, int n) {
+  if (n == 0) return 0;
+  uint32_t L = die_filter(s.O, s.S1o, block_info_low(s.O, low), die_candidates(s.O, s.P, d), d);
+  if (hl <= 0) L &= ~HEAD;
+  int best = 0;
+  while (L) {
+    const int p = __builtin_ctz(L);
+    L &= L - 1u;
+    Side c = s;
+    apply_die(c, p, d);
+    const int v = 1 + hc_depth_plain(c, low, d, hl - (p == 23 ? 1 : 0), n - 1);
+    best = v > best ? v : best;
+  }
+  return best;
+}
+
 // n random block-prone positions (an own 6-window with 0-4 holes, the
 // opponent mostly past it so the rule applies), half doubles: a turn
 // turn_block_free calls block-free must never have the rule remove a
@@ -394,11 +412,97 @@ extern "C" int64_t hc_block_free_random(int64_t n, uint32_t seed, int64_t* freed
     const bool coarse = (runs6(U) & low & windows_few_holes(s.O, dh == dl ? 4 : 2)) == 0u;
     const bool binds = hc_binds(s, low, dh, dl, dh == dl ? 4 : 2);
     bad += bf && binds;
+    if (dh == dl) {
+      // fewer sub-moves left (a node inside a turn): dbl_block_free(k) is
+      // sound for each k, and the searches that stop at block-free nodes
+      // (f4_depth / f4_reach) agree with the plain walk
+      const int hl = 1 + (int)rnd(2);
+      for (int k = 1; k <= 4; ++k) {
+        bad += dbl_block_free(s.O, s.S1o, s.P, low, dh, k) && hc_binds(s, low, dh, dh, k);
+        const int ref = hc_depth_plain(s, low, dh, hl, k);
+        const int got = k == 1 ? f4_depth<1>(s, low, dh, hl, false)
+                               : (k == 2 ? f4_depth<2>(s, low, dh, hl, false)
+                                         : (k == 3 ? f4_depth<3>(s, low, dh, hl, false)
+                                                   : f4_depth<4>(s, low, dh, hl, false)));
+        const bool reach = k == 1 ? f4_reach<1>(s, low, dh, hl, false)
+                                  : (k == 2 ? f4_reach<2>(s, low, dh, hl, false)
+                                            : (k == 3 ? f4_reach<3>(s, low, dh, hl, false)
+                                                      : f4_reach<4>(s, low, dh, hl, false)));
+        bad += got != ref;
+        bad += reach != (ref >= k);
+      }
+    }
     bad += coarse && !bf;  // the refinement only ever frees turns
     fr += bf && !coarse;
     bd += binds;
   }
   *freed = fr;
   *bound = bd;
+  return bad;
+}
+
+// f4_sure_pair against f4_keep_pair on n random block-prone two-dice turns
+// (hc_block_free_random's generator, two dice only): every sure first move
+// keeps a move of the other die.  Returns violations; *sure = sure sources,
+// *total = first-move sources checked.
+extern "C" int64_t hc_sure_pair_random(int64_t n, uint32_t seed, int64_t* sure, int64_t* total) {
+  uint64_t x = 0xBF58476D1CE4E5B9ull ^ seed;
+  auto rnd = [&x](uint32_t m) {
+    x ^= x >> 12; x ^= x << 25; x ^= x >> 27;
+    return (uint32_t)(((x * 0x2545F4914F6CDD1Dull) >> 32) % m);
+  };
+  int64_t bad = 0, su = 0, tot = 0, done = 0;
+  while (done < n) {
+    Side s = side_start(0u);
+    for (int k = 0; k < 3; ++k) { s.own.w[k] = 0u; s.opp.w[k] = 0u; }
+    const int i0 = (int)rnd(19);
+    uint32_t Hm = 0u;
+    const int holes = (int)rnd(3);
+    while (__builtin_popcount(Hm) < holes) Hm |= 1u << (i0 + (int)rnd(6));
+    int left = 15;
+    for (int p = i0; p < i0 + 6; ++p)
+      if (!((Hm >> p) & 1u)) {
+        const int c = 1 + (rnd(3) == 0 ? 1 : 0);
+        for (int j = 0; j < c; ++j) nib_inc(s.own, p);
+        left -= c;
+      }
+    while (left > 0) {
+      const int p = (int)rnd(24);
+      if ((Hm >> p) & 1u) continue;
+      nib_inc(s.own, p);
+      --left;
+    }
+    uint32_t used = 0u;
+    for (int p = 0; p < 24; ++p) used |= nib_get(s.own, p) ? (1u << p) : 0u;
+    const int lo_min = rnd(4) == 0 ? 0 : i0 + 1;
+    bool any = false;
+    for (int q = lo_min; q < 24; ++q) any |= !((used >> q) & 1u);
+    if (!any) continue;
+    for (int lo = 15; lo > 0;) {
+      const int p = lo_min + (int)rnd((uint32_t)(24 - lo_min));
+      if ((used >> p) & 1u) continue;
+      nib_inc(s.opp, p);
+      --lo;
+    }
+    side_masks(s);
+    const int a = 1 + (int)rnd(6), b = 1 + (int)rnd(6);
+    if (a == b) continue;
+    const int dh = a > b ? a : b, dl = a > b ? b : a;
+    const uint32_t low = block_lowmask(s.P);
+    bool bound;
+    const uint32_t hs = two_block_holes(s.O, s.S1o, s.P, low, dh, dl, bound);
+    if (!bound) continue;
+    ++done;
+    for (int k = 0; k < 2; ++k) {
+      const int u = k ? dl : dh, v = k ? dh : dl;
+      const uint32_t L = legal1(s, low, u, false);
+      const uint32_t sr = f4_sure_pair(s.O, s.P, v, L, hs);
+      bad += (sr & ~f4_keep_pair(s, low, u, v, L, false)) != 0u;
+      su += __builtin_popcount(sr);
+      tot += __builtin_popcount(L);
+    }
+  }
+  *sure = su;
+  *total = tot;
   return bad;
 }

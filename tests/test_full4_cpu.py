@@ -237,9 +237,23 @@ def test_hostcheck_block_free_is_sound(hostcheck):
     """turn_block_free (narde_rules.h) on 200,000 random block-prone turns:
     a turn it calls block-free never has the block rule remove a candidate
     anywhere in its sub-move tree (exhaustive walk), and its per-window
-    test frees many turns the hole count alone calls block-bound."""
+    test frees many turns the hole count alone calls block-bound.  On the
+    doubles among them: dbl_block_free(k) is sound for every k = 1..4 and
+    the searches that stop at block-free nodes (f4_depth, f4_reach) equal
+    the plain walk."""
     f = hostcheck.hc_block_free_random
     f.restype = ctypes.c_int64
     fr, bd = ctypes.c_int64(0), ctypes.c_int64(0)
     assert f(ctypes.c_int64(200000), ctypes.c_uint32(11), ctypes.byref(fr), ctypes.byref(bd)) == 0
     assert fr.value > 5000 and bd.value > 5000
+
+
+def test_hostcheck_sure_pair_is_sound(hostcheck):
+    """Block-bound two-dice turns: every first move f4_sure_pair
+    (narde_rules.h) marks from the masks keeps a move of the other die
+    (the per-source f4_keep_pair) -- 100,000 random block-prone turns."""
+    f = hostcheck.hc_sure_pair_random
+    f.restype = ctypes.c_int64
+    su, tot = ctypes.c_int64(0), ctypes.c_int64(0)
+    assert f(ctypes.c_int64(100000), ctypes.c_uint32(3), ctypes.byref(su), ctypes.byref(tot)) == 0
+    assert su.value > tot.value // 4  # it settles a real share of the sources
