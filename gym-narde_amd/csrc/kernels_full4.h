@@ -243,7 +243,8 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
 #else
   bool bound = false;
   const uint32_t hs = dbl ? 0u : two_block_holes(s.O, s.S1o, s.P, low, dh, dl, bound);
-  const bool bf = dbl ? dbl_block_free(s.O, s.S1o, s.P, low, dh, 4) : !bound;
+  const uint32_t ws = dbl ? dbl_block_windows(s.O, s.S1o, s.P, low, dh, 4) : 0u;
+  const bool bf = dbl ? ws == 0u : !bound;
 #endif
   // first sub-move: the lists, the shortcuts, then every lane's checks at once
   const uint32_t Lh = legal1(s, low, dh, bf);
@@ -262,7 +263,12 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   const uint32_t sh = nbf2 ? f4_sure_pair(s.O, s.P, dl, Lh, hs) : 0u;
   const uint32_t sl = nbf2 ? f4_sure_pair(s.O, s.P, dh, Ll, hs) : 0u;
   const int hl0 = (dbl && s.ft_own && (dh == 3 || dh == 4 || dh == 6)) ? 2 : 1;
-  const bool fast = dbl && bf && f4_lower_bound(s.O, s.S1o, s.P, dh, hl0) >= 4;
+#if NARDE_DIAG_ABLATE & (4 | 1024 | 2048)
+  const uint32_t ws = 0u;  // DIAGNOSTIC builds
+#endif
+  // (block-bound: from the moves that can never be rejected, f4_safe_bound;
+  // ws = 0 makes it f4_lower_bound)
+  const bool fast = dbl && f4_safe_bound(s, dh, hl0, bf ? 0u : ws) >= 4;
   // not fast: a chain bound >= 7 still keeps every first sub-move (one
   // sub-move lowers it by <= 4) with M = 4
   const int cb0 = (dbl && bf && !fast) ? f4_chain_bound(s.O, s.S1o, s.P, dh, hl0) : 0;

@@ -583,23 +583,24 @@ NARDE_FN uint32_t windows_few_holes(uint32_t O, int k) {
 // (tools/diag/bf_stats.cpp, tests/hostcheck hc_block_free_random): it frees
 // ~2/3 of the two-dice and ~3/5 of the doubles turns the count alone calls
 // block-bound, and never a turn in which the rule removes a candidate.
-// doubles: block-free for the next k (1..4) sub-moves of die d -- the same
-// test with k landings and a step budget of k (a node inside a block-bound
-// turn is often block-free for the sub-moves it has left)
-NARDE_FN bool dbl_block_free(uint32_t O, uint32_t S1, uint32_t P, uint32_t low, int d, int k) {
+// doubles, the next k (1..4) sub-moves of die d: the points of the windows
+// that fail the per-window test (~0u if one is full already; 0: block-free)
+// -- the same test with k landings and a step budget of k (a node inside a
+// block-bound turn is often block-free for the sub-moves it has left)
+NARDE_FN uint32_t dbl_block_windows(uint32_t O, uint32_t S1, uint32_t P, uint32_t low, int d, int k) {
   uint32_t S = O, U = O;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     S = land_step(S, P, d);
     U |= j < k ? S : 0u;
   }
-  uint32_t win = runs6(U) & low & windows_few_holes(O, k > 2 ? 4 : 2);
+  uint32_t win = runs6(U) & low & windows_few_holes(O, k > 2 ? 4 : 2), ws = 0u;
   while (win) {
     const int i = __builtin_ctz(win);
     win &= win - 1u;
     const uint32_t W = 0x3Fu << i;
     const uint32_t H = W & ~O;
-    if (!H) return false;
+    if (!H) return ~0u;
     uint32_t T = O & ~(W & S1), seen = 0u;
     int cost = 0;
 #pragma unroll
@@ -609,9 +610,12 @@ NARDE_FN bool dbl_block_free(uint32_t O, uint32_t S1, uint32_t P, uint32_t low, 
       cost += j * __builtin_popcount(nw);
       seen |= nw;
     }
-    if (seen == H && cost <= k) return false;
+    ws |= (seen == H && cost <= k) ? W : 0u;
   }
-  return true;
+  return ws;
+}
+NARDE_FN bool dbl_block_free(uint32_t O, uint32_t S1, uint32_t P, uint32_t low, int d, int k) {
+  return dbl_block_windows(O, S1, P, low, d, k) == 0u;
 }
 
 // two dice: the per-window test; returns the holes (in O) of the windows
@@ -752,6 +756,28 @@ NARDE_FN bool f4_bearoff_fixed(const Side& s, int rem = 4) {
   x = (x & 0x0F0F0Fu) + ((x >> 4) & 0x0F0F0Fu);
   const uint32_t home = ((x * 0x010101u) >> 16) & 0xFFu;
   return (int)(15u - s.off_own - home) >= rem;
+}
+
+// f4_lower_bound for a block-bound doubles turn, from ws = dbl_block_windows
+// (its failing windows: no other window can ever fill this turn).  Only
+// sources whose landing cannot fill a failing window count: not a hole of
+// one, not a window point some sub-move may vacate (a source now, or a
+// bear-off source once bear-off opens, if it can this turn).  Such moves
+// are never rejected, in any order, and any sub-move lowers the count by at
+// most one (the window set stays that of the root) -- so, as for the
+// block-free bound, >= 4 at the root gives M = 4 and every C_k = L_k.
+// ws = 0 (block-free) gives f4_lower_bound itself.  Settles ~1/4 of the
+// block-bound doubles turns of random self-play.
+NARDE_FN int f4_safe_bound(const Side& s, int d, int hl, uint32_t ws) {
+  if (ws == ~0u) return 0;
+  const uint32_t C = die_candidates(s.O, s.P, d);
+  const uint32_t opens = f4_bearoff_fixed(s) ? 0u : ((1u << d) - 1u);
+  const uint32_t bad = ws & (~s.O | C | opens);
+  uint32_t L = C & ~(bad << d);
+  if (hl <= 0) L &= ~HEAD;
+  const uint32_t body = L & ~HEAD;
+  const int head = (L & HEAD) ? ((hl >= 2 && !(s.S1o & HEAD)) ? 2 : 1) : 0;
+  return __builtin_popcount(body) + __builtin_popcount(body & ~s.S1o) + head;
 }
 
 // Exact sub-move count of a block-free doubles turn whose bear-off status
@@ -1072,7 +1098,10 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, con
     uint32_t C = 0u;
     // block-free with a lower bound of >= 4 sub-moves: M = 4, and as each
     // sub-move lowers the bound by at most one, every C_k = L_k (no search)
-    const bool fast = bf && f4_lower_bound(s.O, s.S1o, s.P, d, hl) >= 4;
+    // (block-bound: the same from the moves that can never be rejected,
+    // f4_safe_bound)
+    const bool fast = bf ? f4_lower_bound(s.O, s.S1o, s.P, d, hl) >= 4
+                         : f4_safe_bound(s, d, hl, dbl_block_windows(s.O, s.S1o, s.P, low, d, 4)) >= 4;
     // block-free with bear-off fixed: M exactly from the chains, every C_k = L_k
     const bool exact = !fast && bf && f4_bearoff_fixed(s);
     // block-free, bear-off not open yet: M exactly from the chains and the

@@ -347,14 +347,15 @@ static int hc_depth_plain(const Side& s, uint32_t low, int d, int hl, int n) {
 // turn_block_free calls block-free must never have the rule remove a
 // candidate.  Returns such turns; *freed = turns the hole count alone calls
 // block-bound that the per-window test frees; *bound = turns where the rule
-// really binds.
-extern "C" int64_t hc_block_free_random(int64_t n, uint32_t seed, int64_t* freed, int64_t* bound) {
+// really binds; *safe4 = block-bound doubles turns f4_safe_bound settles.
+extern "C" int64_t hc_block_free_random(int64_t n, uint32_t seed, int64_t* freed, int64_t* bound,
+                                        int64_t* safe4) {
   uint64_t x = 0x94D049BB133111EBull ^ seed;
   auto rnd = [&x](uint32_t m) {
     x ^= x >> 12; x ^= x << 25; x ^= x >> 27;
     return (uint32_t)(((x * 0x2545F4914F6CDD1Dull) >> 32) % m);
   };
-  int64_t bad = 0, fr = 0, bd = 0;
+  int64_t bad = 0, fr = 0, bd = 0, fast = 0;
   for (int64_t done = 0; done < n; ++done) {
     Side s = side_start(0u);
     for (int k = 0; k < 3; ++k) { s.own.w[k] = 0u; s.opp.w[k] = 0u; }
@@ -431,6 +432,31 @@ extern "C" int64_t hc_block_free_random(int64_t n, uint32_t seed, int64_t* freed
         bad += got != ref;
         bad += reach != (ref >= k);
       }
+      // f4_safe_bound >= 4 (block-bound 'fast'): M = 4 and every first and
+      // second sub-move keeps the rest of the turn playable
+      if (!bf && f4_safe_bound(s, dh, hl, dbl_block_windows(s.O, s.S1o, s.P, low, dh, 4)) >= 4) {
+        ++fast;
+        bad += hc_depth_plain(s, low, dh, hl, 4) != 4;
+        uint32_t L = legal1(s, low, dh, false);
+        if (hl <= 0) L &= ~HEAD;
+        while (L) {
+          const int p = __builtin_ctz(L);
+          L &= L - 1u;
+          Side c = s;
+          apply_die(c, p, dh);
+          const int h2 = hl - (p == 23 ? 1 : 0);
+          bad += hc_depth_plain(c, low, dh, h2, 3) != 3;
+          uint32_t L2 = legal1(c, low, dh, false);
+          if (h2 <= 0) L2 &= ~HEAD;
+          while (L2) {
+            const int q = __builtin_ctz(L2);
+            L2 &= L2 - 1u;
+            Side c2 = c;
+            apply_die(c2, q, dh);
+            bad += hc_depth_plain(c2, low, dh, h2 - (q == 23 ? 1 : 0), 2) != 2;
+          }
+        }
+      }
     }
     bad += coarse && !bf;  // the refinement only ever frees turns
     fr += bf && !coarse;
@@ -438,6 +464,7 @@ extern "C" int64_t hc_block_free_random(int64_t n, uint32_t seed, int64_t* freed
   }
   *freed = fr;
   *bound = bd;
+  *safe4 = fast;
   return bad;
 }
 

@@ -234,18 +234,20 @@ def test_hostcheck_open_moves_matches_search(hostcheck):
 
 
 def test_hostcheck_block_free_is_sound(hostcheck):
-    """turn_block_free (narde_rules.h) on 200,000 random block-prone turns:
+    """turn_block_free (narde_rules.h) on 150,000 random block-prone turns:
     a turn it calls block-free never has the block rule remove a candidate
     anywhere in its sub-move tree (exhaustive walk), and its per-window
     test frees many turns the hole count alone calls block-bound.  On the
     doubles among them: dbl_block_free(k) is sound for every k = 1..4 and
     the searches that stop at block-free nodes (f4_depth, f4_reach) equal
-    the plain walk."""
+    the plain walk; where f4_safe_bound >= 4 (block-bound but settled from
+    the never-rejected moves) M = 4 and every first and second sub-move
+    keeps the rest playable."""
     f = hostcheck.hc_block_free_random
     f.restype = ctypes.c_int64
-    fr, bd = ctypes.c_int64(0), ctypes.c_int64(0)
-    assert f(ctypes.c_int64(200000), ctypes.c_uint32(11), ctypes.byref(fr), ctypes.byref(bd)) == 0
-    assert fr.value > 5000 and bd.value > 5000
+    fr, bd, s4 = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
+    assert f(ctypes.c_int64(150000), ctypes.c_uint32(11), ctypes.byref(fr), ctypes.byref(bd), ctypes.byref(s4)) == 0
+    assert fr.value > 5000 and bd.value > 5000 and s4.value > 500
 
 
 def test_hostcheck_sure_pair_is_sound(hostcheck):
