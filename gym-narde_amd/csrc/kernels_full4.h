@@ -57,8 +57,7 @@ __device__ __forceinline__ int wave_prefix(int x, int lane, int& total) {
 #define NARDE_F4_CUT 0
 #endif
 // later sub-moves of a block-bound doubles turn: 0 always search, 2 stop at
-// a node block-free for the sub-moves left (1: the old block-free bounds,
-// never true since every block-free doubles lane is direct)
+// a node block-free for the sub-moves left (measured slower: DESIGN §9)
 #ifndef NARDE_F4_LATE
 #define NARDE_F4_LATE 0
 #endif
@@ -266,22 +265,16 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
 #if NARDE_DIAG_ABLATE & (4 | 1024 | 2048)
   const uint32_t ws = 0u;  // DIAGNOSTIC builds
 #endif
-  // (block-bound: from the moves that can never be rejected, f4_safe_bound;
-  // ws = 0 makes it f4_lower_bound)
-  const bool fast = dbl && f4_safe_bound(s, dh, hl0, bf ? 0u : ws) >= 4;
-  // not fast: a chain bound >= 7 still keeps every first sub-move (one
-  // sub-move lowers it by <= 4) with M = 4
-  const int cb0 = (dbl && bf && !fast) ? f4_chain_bound(s.O, s.S1o, s.P, dh, hl0) : 0;
-  // block-free with bear-off fixed: M exactly from the chains and every
-  // C_k = L_k (f4_exact_moves) -- ~3/4 of the doubles turns the bounds miss
-  const bool cand = dbl && bf && !fast && cb0 < 7 && Lh != 0u;
-  const bool exact = cand && f4_bearoff_fixed(s);
-  const int T0 = cand ? f4_exact_moves(s, dh, hl0) : 0;
-  // block-free, bear-off not open yet: M exactly from the chains and the
-  // bear-offs they can open, every C_k = L_k (env_turn_full's ex4)
-  const bool ex4 = cand && !exact;
-  const int Mx = ex4 ? f4_open_moves(s, dh, hl0, T0) : T0;
-  const bool srch = dbl && !fast && Lh != 0u && cb0 < 7 && !exact && !ex4;
+  // block-free doubles: M exactly from the chains (f4_exact_moves, bear-off
+  // fixed) or from the chains and the bear-offs they can open
+  // (f4_open_moves), every C_k = L_k -- no bound, no search
+  const bool xbf = dbl && bf;
+  const int T0 = xbf ? f4_exact_moves(s, dh, hl0) : 0;
+  const int Mx = (xbf && !f4_bearoff_fixed(s)) ? f4_open_moves(s, dh, hl0, T0) : T0;
+  // block-bound doubles: M = 4 and every C_k = L_k when the moves that can
+  // never be rejected give >= 4 (f4_safe_bound); else the search
+  const bool fast = dbl && !bf && f4_safe_bound(s, dh, hl0, ws) >= 4;
+  const bool srch = dbl && !bf && !fast && Lh != 0u;
   // one cooperative pass for every lane's first-sub-move checks
   uint32_t r0[3];
   {
@@ -309,9 +302,9 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
     }
   } else {
     Cl = 0u;
-    if (fast || (cb0 >= 7 && Lh)) { Ch = Lh; M = 4; }
+    if (xbf) { Ch = Lh; M = Lh ? Mx : 0; }
+    else if (fast) { Ch = Lh; M = 4; }
     else if (!Lh) { Ch = 0u; M = 0; }
-    else if (exact || ex4) { Ch = Lh; M = Mx; }
     else if (r0[2]) { Ch = r0[2]; M = 4; }  // some source leaves 3 more
     else if (r0[1]) { Ch = r0[1]; M = 3; }
     else if (r0[0]) { Ch = r0[0]; M = 2; }
@@ -350,21 +343,15 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
     uint32_t Lk = act ? legal1(s, low, dk, bf) : 0u;
     if (hl <= 0) Lk &= ~HEAD;
     const int need = M - k - 1;
-    // cb0 >= 7: the exact chain count is >= 7 too (the bound counts fewer
-    // checkers per point), so as for ex4 / exact every C_k = L_k
-    bool direct = !dbl || fast || exact || ex4 || cb0 >= 7 || need <= 0;
+    // block-free doubles and 'fast' block-bound ones: every C_k = L_k
+    bool direct = !dbl || bf || fast || need <= 0;
 #if NARDE_F4_LATE == 2
-    // (block-free doubles lanes are all direct already.)  A block-bound lane
-    // stops searching once its node is block-free for the need + 1 sub-moves
-    // it has left (env_turn_full): the test only in waves that have one
+    // A block-bound lane stops searching once its node is block-free for the
+    // need + 1 sub-moves it has left (env_turn_full): the test only in waves
+    // that have one
     const bool maybe = act && !direct;
     if (__ballot(maybe) != 0ull)
       direct = direct || (maybe && dbl_block_free(s.O, s.S1o, s.P, low, dk, need + 1));
-#elif NARDE_F4_LATE == 1
-    const bool maybe = act && bf && !direct;
-    if (__ballot(maybe) != 0ull)
-      direct = direct || (maybe && (f4_bearoff_fixed(s, need + 1) ||
-                                    f4_chain_bound(s.O, s.S1o, s.P, dk, hl) >= need + 4));
 #endif
     uint32_t rk[3];
 #if NARDE_DIAG_ABLATE & 2

@@ -1096,26 +1096,18 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, con
     int hl = (s.ft_own && (d == 3 || d == 4 || d == 6)) ? 2 : 1;
     uint32_t L = legal1(s, low, d, bf);
     uint32_t C = 0u;
-    // block-free with a lower bound of >= 4 sub-moves: M = 4, and as each
-    // sub-move lowers the bound by at most one, every C_k = L_k (no search)
-    // (block-bound: the same from the moves that can never be rejected,
-    // f4_safe_bound)
-    const bool fast = bf ? f4_lower_bound(s.O, s.S1o, s.P, d, hl) >= 4
-                         : f4_safe_bound(s, d, hl, dbl_block_windows(s.O, s.S1o, s.P, low, d, 4)) >= 4;
-    // block-free with bear-off fixed: M exactly from the chains, every C_k = L_k
-    const bool exact = !fast && bf && f4_bearoff_fixed(s);
-    // block-free, bear-off not open yet: M exactly from the chains and the
-    // bear-offs they can open (f4_open_moves), every C_k = L_k
-    const bool ex4 = !fast && !exact && bf && L;
-    if (fast) {
+    // block-free: M exactly from the chains and the bear-offs they can open
+    // (f4_bf_moves), and as a sub-move lowers that count by at most one,
+    // every C_k = L_k (no search).  Block-bound: the same M = 4 and C_k = L_k
+    // when the moves that can never be rejected give >= 4 (f4_safe_bound);
+    // else the search.
+    const bool fast = !bf && f4_safe_bound(s, d, hl, dbl_block_windows(s.O, s.S1o, s.P, low, d, 4)) >= 4;
+    if (bf) {
+      C = L;
+      M = L ? f4_bf_moves(s, d, hl, 4) : 0;
+    } else if (fast) {
       C = L;
       M = 4;
-    } else if (exact) {
-      C = L;
-      M = L ? f4_exact_moves(s, d, hl) : 0;
-    } else if (ex4) {
-      C = L;
-      M = f4_open_moves(s, d, hl, f4_exact_moves(s, d, hl));
     } else if (L) {
       C = f4_keep<3>(s, low, d, hl, L, bf);
       M = 4;
@@ -1132,7 +1124,7 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, con
         // once the node is block-free for the M - k sub-moves it has left:
         // on an M-path its exact count (f4_bf_moves) is >= M - k and a
         // sub-move lowers it by at most one, so every C_k = L_k
-        const bool direct = fast || exact || ex4 || (!bf && dbl_block_free(s.O, s.S1o, s.P, low, d, M - k));
+        const bool direct = bf || fast || dbl_block_free(s.O, s.S1o, s.P, low, d, M - k);
         C = direct ? L : f4_keep_rt(s, low, d, hl, L, M - k - 1, bf);
       }
       int p;
