@@ -107,13 +107,7 @@ __device__ void coop_run_x(const Side& s, uint32_t low, int a, int b, int hl, ui
     } else {
       if (has) {
         const int hl2 = thl - (p == 23 ? 1 : 0);
-        int dep = 0;
-        if (tbf) {
-          uint32_t O2, S2;
-          child_masks(c, p, pa, O2, S2);
-          const int lb = f4_chain_bound(O2, S2, c.P, pa, hl2);
-          dep = lb >= tneed ? tneed : 0;
-        }
+        int dep = 0;  // (only block-bound lanes publish doubles tasks)
 #if NARDE_DIAG_ABLATE & 128
         dep = tneed;  // DIAGNOSTIC timing only: no doubles search in the passes
 #endif
@@ -139,7 +133,7 @@ __device__ void coop_run_x(const Side& s, uint32_t low, int a, int b, int hl, ui
 //     b, kept (res 1) iff a still does.
 //   mode 0 (depth, doubles a): m0 = sources; res j gets the sources after
 //     which at least j + 1 more sub-moves are playable (searched up to
-//     `need`; block-free lanes try the chain bound first).
+//     `need`; only block-bound lanes have such tasks).
 __device__ void coop_run(CoopLds& W, const Side& s, uint32_t low, int a, int b, int hl, uint32_t m0,
                          uint32_t m1, int need, bool bf, int mode, int lane, uint32_t out[3]) {
   out[0] = out[1] = out[2] = 0u;
@@ -202,13 +196,7 @@ __device__ void coop_run(CoopLds& W, const Side& s, uint32_t low, int a, int b, 
         if (L2) atomicOr(&W.res[ow][which], 1u << p);
       } else {
         const int hl2 = thl - (p == 23 ? 1 : 0);
-        int dep = 0;
-        if (tbf) {
-          uint32_t O2, S2;
-          child_masks(c, p, pa, O2, S2);
-          const int lb = f4_chain_bound(O2, S2, c.P, pa, hl2);
-          dep = lb >= tneed ? tneed : 0;
-        }
+        int dep = 0;  // (only block-bound lanes publish doubles tasks)
 #if NARDE_DIAG_ABLATE & 128
         dep = tneed;  // DIAGNOSTIC timing only: no doubles search in the passes
 #endif
