@@ -57,7 +57,9 @@ __device__ __forceinline__ int wave_prefix(int x, int lane, int& total) {
 #define NARDE_F4_CUT 0
 #endif
 // later sub-moves of a block-bound doubles turn: 0 always search, 2 stop at
-// a node block-free for the sub-moves left (measured slower: DESIGN §9)
+// a node block-free for the sub-moves left, 3 stop where the root's safe
+// bound (f4_safe_bound) covers the sub-moves left (2 and 3 measured slower,
+// code in this loop runs in every wave, the searches in few)
 #ifndef NARDE_F4_LATE
 #define NARDE_F4_LATE 0
 #endif
@@ -340,6 +342,14 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
     const bool maybe = act && !direct;
     if (__ballot(maybe) != 0ull)
       direct = direct || (maybe && dbl_block_free(s.O, s.S1o, s.P, low, dk, need + 1));
+#elif NARDE_F4_LATE == 3
+    // A block-bound lane stops searching once the moves that can never be
+    // rejected (the root's failing windows, f4_safe_bound) leave >= need + 1
+    // at its node: on an M-path a sub-move lowers that bound by at most one,
+    // so every source keeps need more
+    const bool maybe = act && !direct;
+    if (__ballot(maybe) != 0ull)
+      direct = direct || (maybe && f4_safe_bound(s, dk, hl, ws) >= need + 1);
 #endif
     uint32_t rk[3];
 #if NARDE_DIAG_ABLATE & 2
