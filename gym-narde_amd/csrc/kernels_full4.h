@@ -230,10 +230,10 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
 #elif NARDE_DIAG_ABLATE & 2048
   const bool bf = dbl ? true : turn_block_free(s.O, s.S1o, s.P, low, dh, dl);  // DIAGNOSTIC
 #else
-  bool bound = false;
-  const uint32_t hs = dbl ? 0u : two_block_holes(s.O, s.S1o, s.P, low, dh, dl, bound);
-  const uint32_t ws = dbl ? dbl_block_windows(s.O, s.S1o, s.P, low, dh, 4) : 0u;
-  const bool bf = dbl ? ws == 0u : !bound;
+  // one block test for both kinds of turn (turn_block_set)
+  const uint32_t bs = turn_block_set(s.O, s.S1o, s.P, low, dh, dl);
+  const bool bf = bs == 0u;
+  const uint32_t hs = dbl ? 0u : bs, ws = dbl ? bs : 0u;
 #endif
   // first sub-move: the lists, the shortcuts, then every lane's checks at once
   const uint32_t Lh = legal1(s, low, dh, bf);

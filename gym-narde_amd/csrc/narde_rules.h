@@ -643,11 +643,51 @@ NARDE_FN uint32_t two_block_holes(uint32_t O, uint32_t S1, uint32_t P, uint32_t 
   return hs;
 }
 
+// Both kinds of turn in one pass (a wave holds both: one reachable set, one
+// hole count, one window loop instead of two of each): 0 if the turn is
+// block-free; else two_block_holes' holes (two dice) or
+// dbl_block_windows' points (doubles, k = 4), ~0u if a failing window is
+// full already.  The doubles reachable set is a superset here (two more
+// steps of O..S2 cover S3, S4), which only lets more windows into the
+// exact per-window test.
+NARDE_FN uint32_t turn_block_set(uint32_t O, uint32_t S1, uint32_t P, uint32_t low, int dh, int dl) {
+  const bool dbl = dh == dl;
+  const uint32_t A = O | land_step(O, P, dh) | land_step(O, P, dl);
+  uint32_t U = A | land_step(A, P, dh) | land_step(A, P, dl);
+  const uint32_t V = land_step(U, P, dh);
+  U |= dbl ? (V | land_step(V, P, dh)) : 0u;
+  uint32_t win = runs6(U) & low & windows_few_holes(O, dbl ? 4 : 2), out = 0u;
+  while (win) {
+    const int i = __builtin_ctz(win);
+    win &= win - 1u;
+    const uint32_t W = 0x3Fu << i;
+    const uint32_t H = W & ~O;
+    if (!H) return ~0u;
+    const uint32_t src = O & ~(W & S1);
+    if (dbl) {
+      uint32_t T = src, seen = 0u;
+      int cost = 0;
+#pragma unroll
+      for (int j = 1; j <= 4; ++j) {
+        T = land_step(T, P, dh);
+        const uint32_t nw = H & T & ~seen;
+        cost += j * __builtin_popcount(nw);
+        seen |= nw;
+      }
+      out |= (seen == H && cost <= 4) ? W : 0u;
+    } else {
+      const uint32_t Lh = land_step(src, P, dh), Ll = land_step(src, P, dl);
+      const uint32_t h1 = H & (0u - H), h2 = H ^ h1;
+      const bool fail = !h2 ? (H & (Lh | Ll | land_step(Lh, P, dl) | land_step(Ll, P, dh))) != 0u
+                            : (((h1 & Lh) && (h2 & Ll)) || ((h1 & Ll) && (h2 & Lh)));
+      out |= fail ? H : 0u;
+    }
+  }
+  return out;
+}
+
 NARDE_FN bool turn_block_free(uint32_t O, uint32_t S1, uint32_t P, uint32_t low, int dh, int dl) {
-  if (dh == dl) return dbl_block_free(O, S1, P, low, dh, 4);
-  bool bound;
-  two_block_holes(O, S1, P, low, dh, dl, bound);
-  return !bound;
+  return turn_block_set(O, S1, P, low, dh, dl) == 0u;
 }
 
 // Block-bound two dice: the first moves p of die a (in La) sure to leave die
