@@ -236,8 +236,15 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   const uint32_t hs = dbl ? 0u : bs, ws = dbl ? bs : 0u;
 #endif
   // first sub-move: the lists, the shortcuts, then every lane's checks at once
-  const uint32_t Lh = legal1(s, low, dh, bf);
-  const uint32_t Ll = dbl ? 0u : legal1(s, low, dl, bf);
+  // (both dice's lists from one block-info of the root: legal1 twice would
+  // compute it twice in the block-bound lanes)
+  uint32_t Lh = die_candidates(s.O, s.P, dh);
+  uint32_t Ll = dbl ? 0u : die_candidates(s.O, s.P, dl);
+  if (!bf) {
+    const Blocks bl = block_info_low(s.O, low);
+    Lh = die_filter(s.O, s.S1o, bl, Lh, dh);
+    Ll = die_filter(s.O, s.S1o, bl, Ll, dl);
+  }
   // two dice, block-free: the pair checks of every source from the masks
   // (f4_keep_pair_bf) -- only non-block-free lanes publish pair tasks
   const bool pbf = !dbl && bf;
