@@ -63,8 +63,13 @@ __device__ __forceinline__ int wave_prefix(int x, int lane, int& total) {
 #ifndef NARDE_F4_LATE
 #define NARDE_F4_LATE 0
 #endif
+// owners up to which a pass is transposed (above: the packed LDS task list).
+// 2 was best while ~2.4 block-bound lanes per wave had checks; with the
+// block-bound lanes down to ~0.7 per wave the transposed walk wins for every
+// wave (64: the packed list is compiled out and the kernel needs no LDS):
+// 0.4218 against 0.4266 ms per 100 plies (1 / 3: 0.4238 / 0.4267)
 #ifndef NARDE_COOP_XPOSE
-#define NARDE_COOP_XPOSE 2
+#define NARDE_COOP_XPOSE 64
 #endif
 __device__ __forceinline__ uint32_t rl(uint32_t v, int l) {
   return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
