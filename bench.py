@@ -37,6 +37,11 @@ RECORD_BYTES = 64
 # FULL4: the same per-ply outputs with the 8-B played
 # sub-moves instead of the 4-B action codes = 118 B
 OUT_BYTES_PER_STEP_FULL = 118
+# speed of oracle/narde_port.py over the imported reference, same core
+# (tools/calibrate_port.py)
+PORT_OVER_REFERENCE = 1.015
+# plies per launch of the untimed device ramp
+RAMP_PLIES = 1000
 
 
 def launch_bytes(envs, plies, full=False):
@@ -51,7 +56,31 @@ def _port_worker(args):
     return steps, wall
 
 
-def cpu_baseline(seconds, cores):
+def available_cores():
+    """(cores, how): the CPUs this process may run on -- its affinity set,
+    capped by a cgroup CPU quota if one is set (on the GPU pool the affinity
+    set is the whole machine, the quota the box's share)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:  # cgroup v2
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:  # cgroup v1
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        return aff, f"{aff} CPUs in the affinity set, no cgroup CPU quota"
+    n = max(1, min(aff, int(quota)))
+    return n, f"{aff} CPUs in the affinity set, cgroup CPU quota {quota:g} CPUs"
+
+
+def cpu_baseline(seconds, cores, how):
     """Python restatement of the reference env (same per-env loop structure),
     one process per core, plus the C oracle on one core.  Runs BEFORE any GPU
     initialisation (fork is safe then)."""
@@ -86,7 +115,12 @@ def cpu_baseline(seconds, cores):
         "kind": "port",
         "sample": (f"oracle/narde_port.py (Python restatement of NardeEnv.step, reference loop "
                    f"structure) random-legal self-play, 64 envs x {seconds:.1f}s per process, "
-                   f"{cores} processes, {steps} env steps; CPU: {cpu_model}"),
+                   f"{cores} processes (one per available core: {how}), {steps} env steps; "
+                   f"CPU: {cpu_model}"),
+        "cpu_model": cpu_model,
+        # tools/calibrate_port.py in the build container: the port runs
+        # 12,293 steps/s/core against the imported reference's 12,116
+        "port_over_reference": PORT_OVER_REFERENCE,
         "c_oracle_1core": round(c_rate, 1),
     }
 
@@ -114,11 +148,17 @@ def main():
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--plies-per-launch", type=int, default=1000)
+    ap.add_argument("--ramp-launches", type=int, default=100,
+                    help="untimed 1,000-ply launches before --warmup (device clock ramp; 0 = none)")
+    ap.add_argument("--ramp-ms", type=float, default=150.0,
+                    help="... and at least this long")
     ap.add_argument("--api-steps", type=int, default=200)
     ap.add_argument("--fused-plies", type=int, default=1000)
     ap.add_argument("--fused-launches", type=int, default=20)
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
-    ap.add_argument("--cpu-cores", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--cpu-cores", type=int, default=0,
+                    help="processes of the CPU baseline (0 = every available core: the CPU "
+                         "affinity set, capped by the cgroup CPU quota)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--rules", choices=("ref2", "full4"), default="ref2",
                     help="rules of the timed path (value); the other mode is reported beside it")
@@ -135,7 +175,10 @@ def main():
     rank_env = int(os.environ.get("RANK", "0"))
     cpu = None
     if world_env == 1 and rank_env == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds, args.cpu_cores)
+        cores, how = available_cores()
+        if args.cpu_cores > 0:
+            cores, how = args.cpu_cores, f"--cpu-cores {args.cpu_cores}"
+        cpu = cpu_baseline(args.cpu_seconds, cores, how)
 
     import torch
     import torch.distributed as dist
@@ -157,18 +200,41 @@ def main():
 
     P = max(1, min(args.plies_per_launch, args.steps))
     bufs = env.rollout_buffers(P)
+    full_launch = env.rollout_launcher(P, bufs)
 
     def run_plies(k):
         launches = []
         done = 0
         while done < k:
             p = min(P, k - done)
-            env.rollout(p, bufs)
+            if p == P:
+                full_launch()  # pre-bound: one ctypes call per launch
+            else:
+                env.rollout(p, bufs)
             launches.append(p)
             done += p
         return launches
 
+    # untimed device ramp, whatever --warmup is: a cold MI355X runs its first
+    # ~100 back-to-back launches of this kernel at DVFS-reduced clocks
+    # (DESIGN.md section 6), so the ramp plays RAMP_PLIES-ply launches of the
+    # same kernel for at least --ramp-ms and --ramp-launches
+    ramp_n, ramp_t0 = 0, time.perf_counter()
+    if args.ramp_launches > 0:
+        rbufs = bufs if P == RAMP_PLIES else env.rollout_buffers(RAMP_PLIES)
+        ramp = env.rollout_launcher(RAMP_PLIES, rbufs)
+        while ramp_n < args.ramp_launches or (time.perf_counter() - ramp_t0) * 1e3 < args.ramp_ms:
+            for _ in range(10):
+                ramp()
+            ramp_n += 10
+            torch.cuda.synchronize()
+        del ramp, rbufs
+    ramp_ms = (time.perf_counter() - ramp_t0) * 1e3
+
     run_plies(args.warmup)
+    # per-env statistics land here; the timed region gathers them only when
+    # there is something to gather (N > 1: the one RCCL all-gather)
+    stats_buf = torch.empty((per, 3), dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -183,12 +249,15 @@ def main():
     ev0.record()
     launches = run_plies(K)
     ev1.record()
-    stats = D.gather_stats(env.stats())
+    if world > 1:
+        stats = D.gather_stats(env.stats(out=stats_buf))
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     span_ms = ev0.elapsed_time(ev1)
+    if world == 1:
+        stats = env.stats(out=stats_buf)
     # algorithmic bytes of every launch in the span (a last partial launch
     # included), and the mean duration of a full-length launch
     span_bytes = sum(launch_bytes(per, p, is_full4) for p in launches)
@@ -337,15 +406,38 @@ def main():
     if rank == 0:
         nbytes = launch_bytes(per, P, is_full4)
         achieved = nbytes / (kern_ms * 1e-3) / 1e9  # = span bytes / span time (max over ranks)
-        tj = args.traffic_json or os.path.join(
-            ROOT, "profiles", "pmc_k_rollout_full.json" if is_full4 else "pmc_k_rollout.json")
-        traffic = load_traffic(tj, per, P)
+        # the PMC summary measured at this launch shape (plies per launch):
+        # profiles/pmc_k_rollout[_full]_p<P>.json, else the 1,000-ply one
+        base = os.path.join(ROOT, "profiles", "pmc_k_rollout_full" if is_full4 else "pmc_k_rollout")
+        traffic = None
+        for tj in ([args.traffic_json] if args.traffic_json else [f"{base}_p{P}.json", f"{base}.json"]):
+            traffic = load_traffic(tj, per, P)
+            if traffic is not None:
+                break
         obytes = launch_bytes(per, P, not is_full4)
+        # what each rules mode is, and which BASELINE.json config it times
         rules_txt = {
-            "ref2": ("reference NardeEnv.step (REF2: <=2 checker moves per step, also on doubles; "
-                     "legal sets bit-exact vs the reference)"),
+            "ref2": ("REF2 = the reference's NardeEnv.step (narde_env.py:27-103: <=2 checker moves "
+                     "per step, also on doubles); legal sets bit-exact vs the reference"),
             "full4": ("FULL4 whole turns (4-move doubles, max dice used, higher-die rule; DESIGN.md "
-                      "section 10; every sub-move is the reference's single-die primitive)"),
+                      "section 10); every sub-move is the reference's single-die primitive, the "
+                      "whole-turn composition is the build's (parity unpinned: the reference never "
+                      "plays a whole turn)"),
+        }
+        config_txt = {
+            "ref2": ("configs[2]'s batch and dice (65536 envs/GPU, all 36 ordered pairs) under REF2, "
+                     "the rules the metric's 'legal-move bit-exact vs CPU' is defined on; "
+                     "configs[2] as written ('full rules incl. 4-move doubles') is the FULL4 leg, "
+                     "other_rules"),
+            "full4": ("configs[2] as written: 65536 envs/GPU, full rules incl. 4-move doubles "
+                      "(FULL4); the REF2 leg is other_rules"),
+        }
+        parity_txt = {
+            "ref2": ("bit-exact vs the reference's golden vectors and the CPU oracle; unpinned: "
+                     "TimeLimit truncation (gymnasium semantics, gymnasium absent) and the device "
+                     "RNG (the build's own synthetic workload)"),
+            "full4": ("sub-moves pinned to the reference (tests/golden/full4.npz); whole-turn "
+                      "composition unpinned (the build's rule, held to the build's oracle)"),
         }
         line = {
             "metric": METRIC,
@@ -355,17 +447,19 @@ def main():
             "steps": K,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / K * 1e3, 6),
+            "device_ramp_launches": ramp_n,
+            "device_ramp_ms": round(ramp_ms, 1),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (Philox dice, random legal policy, start position + auto-reset)",
             "config": {
-                "workload": (f"configs[2]: batch=65536 random-policy self-play per GPU; rules = "
-                             f"{rules_txt[args.rules]}; dice uniform over 36 ordered pairs; "
-                             f"TimeLimit 1000; every ply writes obs/reward/terminated/truncated/"
-                             f"legal set/actions for every env"),
+                "workload": (f"{config_txt[args.rules]}: random-policy self-play; rules = "
+                             f"{rules_txt[args.rules]}; TimeLimit 1000; every ply writes obs/"
+                             f"reward/terminated/truncated/legal set/actions for every env"),
                 "rules": args.rules,
+                "parity": parity_txt[args.rules],
                 "kernel": f"{'k_rollout<true, true> (FULL4)' if is_full4 else 'k_rollout_pc<true> (REF2)'}, {P} plies per launch",
                 "envs_per_gpu": per,
                 "global_envs": world * per,
@@ -395,7 +489,8 @@ def main():
             },
             "other_rules": {
                 "rules": other_rules,
-                "workload": rules_txt[other_rules],
+                "workload": f"{config_txt[other_rules]}; rules = {rules_txt[other_rules]}",
+                "parity": parity_txt[other_rules],
                 "kernel": f"{'k_rollout<true, true> (FULL4)' if other_rules == 'full4' else 'k_rollout_pc<true> (REF2)'}, {P} plies per launch, all outputs",
                 "value": round(other_rate, 1),
                 "unit": "env steps/s",

@@ -156,10 +156,11 @@ __global__ void __launch_bounds__(kSampleThreads) k_per_sample(const float* __re
 }
 
 // ------------------------------------------------------------- minibatch rows
+// row k's next observation is row (k + stride) % cap of the same ring (the
+// step after k's writes B = stride rows further on; DeviceReplay in dqn.py)
 __global__ void __launch_bounds__(256) k_gather_batch(const int64_t* __restrict__ idx, int batch, int ss,
-                                                      const float* __restrict__ obs,
-                                                      const float* __restrict__ next_obs,
-                                                      const int64_t* __restrict__ action,
+                                                      const float* __restrict__ obs, int64_t stride,
+                                                      int64_t cap, const int64_t* __restrict__ action,
                                                       const float* __restrict__ reward,
                                                       const float* __restrict__ done, float* __restrict__ s,
                                                       float* __restrict__ ns, int64_t* __restrict__ a,
@@ -169,8 +170,10 @@ __global__ void __launch_bounds__(256) k_gather_batch(const int64_t* __restrict_
   const int j = (int)(e / (uint32_t)ss);
   const int col = (int)(e - (uint32_t)j * (uint32_t)ss);
   const int64_t k = idx[j];
+  int64_t kn = k + stride;
+  if (kn >= cap) kn -= cap;
   s[e] = obs[k * ss + col];
-  ns[e] = next_obs[k * ss + col];
+  ns[e] = obs[kn * ss + col];
   if (col == 0) {
     a[2 * j] = action[2 * k];
     a[2 * j + 1] = action[2 * k + 1];
@@ -379,15 +382,16 @@ int narde_per_sample(int device, const float* p, const float* cdf, int64_t n, in
 }
 
 int narde_gather_batch(int device, const int64_t* idx, int64_t batch, int state_size, const float* obs,
-                       const float* next_obs, const int64_t* action, const float* reward, const float* done,
-                       float* s, float* ns, int64_t* a, float* r, float* d, void* stream) {
-  if (!idx || !obs || !next_obs || !action || !reward || !done || !s || !ns || !a || !r || !d)
+                       int64_t next_stride, int64_t capacity, const int64_t* action, const float* reward,
+                       const float* done, float* s, float* ns, int64_t* a, float* r, float* d, void* stream) {
+  if (!idx || !obs || !action || !reward || !done || !s || !ns || !a || !r || !d)
     return bad("NULL argument");
   if (batch <= 0 || state_size <= 0 || batch * state_size >= (int64_t(1) << 31)) return bad("bad sizes");
+  if (capacity <= 0 || next_stride < 0 || next_stride >= capacity) return bad("bad ring geometry");
   DeviceGuard dg(device);
   const int64_t total = batch * state_size;
   k_gather_batch<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(
-      idx, (int)batch, state_size, obs, next_obs, action, reward, done, s, ns, a, r, d);
+      idx, (int)batch, state_size, obs, next_stride, capacity, action, reward, done, s, ns, a, r, d);
   return check_launch("k_gather_batch");
 }
 

@@ -41,23 +41,31 @@ __global__ void __launch_bounds__(kBlock) k_observe(Planes pl, int n, int32_t* _
 // One DQN transition for every env, fused (config 4, gym_narde/dqn.py
 // BatchedDQNDriver): the 198-float observation of the post-step record
 // (k_observe's encoding), the reference trainer's reward shaping
-// (train_deepq_pytorch.py:885-908), the prioritized-replay write of
-// (s, a, r', s', done) at ring slot (pos + i) % capacity with the running max
-// priority, and s <- s'.  One thread per observation float (coalesced rows;
-// the 32 B record is an L1 hit for the row's 198 threads); column 0 also
-// writes the env's scalars.  HBM per env: 792 B read (s) + 3 x 792 B written.
+// (train_deepq_pytorch.py:885-912), the prioritized-replay write of
+// (a, r', done) with the running max priority, and s <- s'.
+//
+// Replay ring layout (DeviceReplay): row j holds transition j's s; its s'
+// is row (j + n) % capacity -- the s of the same env's next transition, so
+// each observation is stored once.  This step's rows are (pos + i) %
+// capacity (their s is already there: written as s' by the previous step,
+// or by DeviceReplay.seed); s' goes to row (pos + n + i) % capacity, whose
+// priority drops to 0 until the next step completes it (never sampled).
+// One thread per 4 observation floats (coalesced rows; the 32-B record is an
+// L1 hit for the row's threads); the thread holding column 0 of a row also
+// writes the env's scalars.  HBM per env: 2 x 792 B written (ring row, s').
 struct TransArgs {
   Planes pl;
   int n;
   int shaping;
-  float* state;                 // (n,198) in: s, out: s'
+  float* state;                 // (n,198) out: s'
   const int64_t* actions;       // (n,2)
   const int32_t* reward;        // (n,)
   const uint8_t* term;          // (n,)
   const uint8_t* trunc;         // (n,)
+  const uint64_t* legal;        // (n,) compact list #1 of the step; NULL = every env could move
+  int32_t* misc;                // (n,) off_w | off_b << 4 | black << 10: in before the step, out after
   float* off_seen;              // (n,2) borne-off trackers, white/black
-  float* r_obs;                 // replay (capacity,198)
-  float* r_next;                // replay (capacity,198)
+  float* r_obs;                 // replay ring (capacity,198)
   int64_t* r_action;            // replay (capacity,2)
   float* r_reward;              // replay (capacity,)
   float* r_done;                // replay (capacity,)
@@ -89,48 +97,64 @@ __device__ __forceinline__ float tes_value(uint4 a, uint4 b, int col) {
   return col >= 196 ? player : pv;
 }
 
-// the env scalars of one transition (the thread holding column 0 of row i)
-__device__ __forceinline__ void trans_scalars(const TransArgs& t, int i, int64_t slot, uint4 b) {
-  const float done = (t.term[i] | t.trunc[i]) ? 1.0f : 0.0f;
+// The reward shaping of train_deepq_pytorch.py:892-912 for one env: the
+// trainer reads env.unwrapped.current_player AFTER the step and that
+// player's borne-off count: +1 per checker newly borne off since its
+// tracker and +0.1 x the count.  With auto-reset the record already holds
+// the next game at a step that ends one, so the player and count come from
+// the pre-step misc word there: a terminal step names the mover (the winner,
+// 15 off, the player is not flipped), a truncated one the other player (the
+// mover's checkers cannot change its count).  No legal move (list #1
+// empty): no shaping, as the reference skips it (:869-873).  The trackers
+// restart at 0 with a new episode.  Same fp32 ops as the torch restatement
+// (BatchedDQNDriver._transition_torch).
+__device__ __forceinline__ void trans_scalars(const TransArgs& t, int i, int64_t slot, int64_t nslot,
+                                              uint4 b) {
+  const bool term = t.term[i] != 0, trunc = t.trunc[i] != 0;
+  const float done = (term || trunc) ? 1.0f : 0.0f;
+  const uint32_t post = b.z;
   float r = (float)t.reward[i];
   if (t.shaping) {
-    // +1 per checker newly borne off and +0.1 x total off, for the player
-    // to move AFTER the step (the reference reads the post-flip player);
-    // the trackers restart at 0 with a new episode.  Same fp32 ops as the
-    // torch restatement (BatchedDQNDriver._transition_torch).
-    const int black = (int)((b.z >> 10) & 1u);
-    const float now = (float)(black ? ((b.z >> 4) & 15u) : (b.z & 15u));
+    const uint32_t pre = (uint32_t)t.misc[i];
+    const bool moved = !t.legal || (t.legal[i] & 0xFFFFFFFFFFFFull) != 0ull;
+    const uint32_t pre_black = (pre >> 10) & 1u;
+    const int black = (int)(term ? pre_black : (trunc ? (pre_black ^ 1u) : ((post >> 10) & 1u)));
+    const uint32_t src = (term || trunc) ? pre : post;
+    const float now = term ? 15.0f : (float)(black ? ((src >> 4) & 15u) : (src & 15u));
     const float before = t.off_seen[2 * i + black];
-    {
+    if (moved) {
 #pragma clang fp contract(off)  // torch rounds the product and the sum separately: no FMA
       r = (r + fmaxf(now - before, 0.0f)) + 0.1f * now;
     }
     const float keep = 1.0f - done;
-    const float o0 = black ? t.off_seen[2 * i] : now;
-    const float o1 = black ? now : t.off_seen[2 * i + 1];
+    const float o0 = (moved && !black) ? now : t.off_seen[2 * i];
+    const float o1 = (moved && black) ? now : t.off_seen[2 * i + 1];
     t.off_seen[2 * i] = o0 * keep;
     t.off_seen[2 * i + 1] = o1 * keep;
   }
+  t.misc[i] = (int32_t)(post & 0x4FFu);  // off_w | off_b << 4 | black_to_move << 10
   t.r_action[2 * slot] = t.actions[2 * i];
   t.r_action[2 * slot + 1] = t.actions[2 * i + 1];
   t.r_reward[slot] = r;
   t.r_done[slot] = done;
   t.r_prio[slot] = *t.max_prio;
+  t.r_prio[nslot] = 0.0f;
 }
 
-// Each thread owns 4 consecutive floats of the flat (n, 198) arrays, so the
-// state load and the three row stores are 16 B per lane (1 KiB per wave
-// instruction; the two replay rows are written once and read only when
-// sampled: non-temporal).  That needs the ring rows pos .. pos + n - 1
-// contiguous and 16-B aligned (pos * 198 % 4 == 0, no wrap -- the steady
-// state when the capacity is a multiple of n); otherwise each float goes
-// on its own.
+// Each thread owns 4 consecutive floats of the flat (n, 198) arrays, so s'
+// goes out 16 B per lane (1 KiB per wave instruction; the ring row is
+// written once and read only when sampled: non-temporal) when this step's
+// s' rows (pos + n .. pos + 2n - 1) % capacity are contiguous and 16-B
+// aligned (the steady state when the capacity is a multiple of n);
+// otherwise each float goes on its own.
 __global__ void __launch_bounds__(kBlock) k_dqn_transition(TransArgs t) {
   const uint32_t total = (uint32_t)t.n * 198u;  // n * 198 < 2^31 (checked on the host)
   const uint32_t e0 = 4u * (blockIdx.x * kBlock + threadIdx.x);
   if (e0 >= total) return;
-  const int64_t pos = *t.pos;  // pos < capacity and i < n <= capacity: one wrap at most
-  const bool vec = (pos * 198) % 4 == 0 && pos + t.n <= t.capacity && e0 + 4u <= total;
+  const int64_t pos = *t.pos;  // pos < capacity, capacity >= 2n: one wrap at most
+  int64_t q0 = pos + t.n;
+  if (q0 >= t.capacity) q0 -= t.capacity;
+  const bool vec = (q0 * 198) % 4 == 0 && q0 + t.n <= t.capacity && e0 + 4u <= total;
   const int i0 = (int)(e0 / 198u);
   const int c0 = (int)(e0 - (uint32_t)i0 * 198u);
   const uint4 a0 = t.pl.p0[i0], b0 = t.pl.p1[i0];
@@ -145,15 +169,10 @@ __global__ void __launch_bounds__(kBlock) k_dqn_transition(TransArgs t) {
     nv[q] = c < 198 ? tes_value(a0, b0, c) : tes_value(a1, b1, c - 198);
   }
   if (vec) {
-    float4* st4 = reinterpret_cast<float4*>(t.state + e0);
-    const float4 ov = *st4;
-    const size_t d = (size_t)pos * 198 + e0;
     typedef float v4f __attribute__((ext_vector_type(4)));
-    const v4f o = {ov.x, ov.y, ov.z, ov.w};
     const v4f nn = {nv[0], nv[1], nv[2], nv[3]};
-    __builtin_nontemporal_store(o, reinterpret_cast<v4f*>(t.r_obs + d));
-    __builtin_nontemporal_store(nn, reinterpret_cast<v4f*>(t.r_next + d));
-    *st4 = make_float4(nv[0], nv[1], nv[2], nv[3]);
+    __builtin_nontemporal_store(nn, reinterpret_cast<v4f*>(t.r_obs + (size_t)q0 * 198 + e0));
+    *reinterpret_cast<float4*>(t.state + e0) = make_float4(nv[0], nv[1], nv[2], nv[3]);
   } else {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -161,10 +180,9 @@ __global__ void __launch_bounds__(kBlock) k_dqn_transition(TransArgs t) {
       if (e >= total) break;
       const int i = (int)(e / 198u);
       const int col = (int)(e - (uint32_t)i * 198u);
-      int64_t slot = pos + i;
-      if (slot >= t.capacity) slot -= t.capacity;
-      t.r_obs[slot * 198 + col] = t.state[e];
-      t.r_next[slot * 198 + col] = nv[q];
+      int64_t qs = q0 + i;
+      if (qs >= t.capacity) qs -= t.capacity;
+      t.r_obs[qs * 198 + col] = nv[q];
       t.state[e] = nv[q];
     }
   }
@@ -177,7 +195,9 @@ __global__ void __launch_bounds__(kBlock) k_dqn_transition(TransArgs t) {
     if (e - (uint32_t)i * 198u != 0u) continue;
     int64_t slot = pos + i;
     if (slot >= t.capacity) slot -= t.capacity;
-    trans_scalars(t, i, slot, i == i0 ? b0 : b1);
+    int64_t nslot = q0 + i;
+    if (nslot >= t.capacity) nslot -= t.capacity;
+    trans_scalars(t, i, slot, nslot, i == i0 ? b0 : b1);
   }
 }
 
@@ -229,12 +249,15 @@ __global__ void __launch_bounds__(kBlock) k_mask576_move2(Planes pl, int n, Rng 
     ply_draw(g, s.t, (uint32_t)i, r);
     dice_from(r[0], g.dice_mode, d0, d1);
   }
+  // a given die outside 1..6: no legal move, nothing is accepted
+  const bool bad = (uint32_t)(d0 - 1) > 5u || (uint32_t)(d1 - 1) > 5u;
+  if (bad) d0 = d1 = 1;
   Legal l;
   legal2(s, d0, d1, l);
   uint64_t m[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   int f1, t1;
   decode_action(move1[i], f1, t1);
-  if (l.count >= 2 && legal_contains(l, f1, t1)) {
+  if (!bad && l.count >= 2 && legal_contains(l, f1, t1)) {
     apply_move(s, f1, t1);
     const int dist = t1 == OFF ? f1 + 1 : (f1 > t1 ? f1 - t1 : t1 - f1);
     const int rem = (d0 == dist) ? d1 : ((d1 == dist) ? d0 : d1);

@@ -412,10 +412,13 @@ __global__ void __launch_bounds__(kBlock) k_legal_full(Planes pl, int n, Rng g,
   const bool valid = i < n;  // no early exit: the turn is wave-cooperative
   Side s = valid ? side_from_record(pl.p0[i], pl.p1[i]) : side_start(0u);
   int d0 = 1, d1 = 2;
+  bool bad = false;  // a given die outside 1..6: no legal move
   if (dice2) {
     if (valid) {
       d0 = dice2[2 * i];
       d1 = dice2[2 * i + 1];
+      bad = (uint32_t)(d0 - 1) > 5u || (uint32_t)(d1 - 1) > 5u;
+      if (bad) { d0 = 1; d1 = 2; }
     }
   } else {
     uint32_t r[4];
@@ -426,7 +429,7 @@ __global__ void __launch_bounds__(kBlock) k_legal_full(Planes pl, int n, Rng g,
   TurnOut o;
   // play word of -1s: nothing is applied
   coop_turn_full(s, d0, d1, true, ~0ull, w, o, wave_coop, (int)(threadIdx.x & 63));
-  if (valid) out[i] = o.legal;
+  if (valid) out[i] = bad ? 0ull : o.legal;
 }
 
 }  // namespace

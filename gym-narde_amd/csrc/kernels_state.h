@@ -6,15 +6,30 @@
 namespace {
 
 // ------------------------------------------------------------------ kernels
-// init_t >= 0: also set the RNG counter (create); < 0: keep each env's counter
+// init_t >= 0: also set the RNG counter (create); < 0: keep each env's counter.
+// opening (optional) u8[n][pairs][2]: each env's opening draws (white roll,
+// black roll) in draw order; as narde_env.py:111-117 the first pair of
+// different dice decides (higher roll moves first), pairs with a die outside
+// 1..6 are padding, and a row with no deciding pair takes the device draw.
 __global__ void __launch_bounds__(kBlock) k_reset(Planes pl, int n, Rng g, uint32_t epoch,
-                                                  const uint8_t* __restrict__ mask, int64_t init_t) {
+                                                  const uint8_t* __restrict__ mask, int64_t init_t,
+                                                  const uint8_t* __restrict__ opening, int pairs) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   if (mask && !mask[i]) return;
   uint32_t r[4];
   draw(g, epoch, (uint32_t)i, 1u, r);
   Side s = side_reset(r[0]);
+  if (opening) {
+    const uint8_t* row = opening + (size_t)i * (size_t)pairs * 2;
+    for (int k = 0; k < pairs; ++k) {
+      const int w = row[2 * k], b = row[2 * k + 1];
+      if ((uint32_t)(w - 1) <= 5u && (uint32_t)(b - 1) <= 5u && w != b) {
+        s = side_start(w > b ? 0u : 1u);
+        break;
+      }
+    }
+  }
   s.t = init_t >= 0 ? (uint32_t)init_t : pl.p1[i].w;
   uint4 a, b;
   side_to_record(s, a, b);
@@ -119,16 +134,29 @@ __global__ void __launch_bounds__(kBlock) k_get_stats(Planes pl, int n, int32_t*
   out[3 * i] = s.x; out[3 * i + 1] = s.y; out[3 * i + 2] = s.z;
 }
 
+// execute_rotated_move (narde.py:36-56,108-125) of one move per env.  The
+// reference executes any (from, to) it is handed; the moves this record can
+// hold are those whose source has one of the mover's checkers and whose
+// target is not an opponent point (every listed move is one).  Others -- an
+// empty source makes narde.py:123-125 conjure a checker of the other colour,
+// an opponent target cancels one checker of each -- leave the env unchanged
+// and set status[i] = 1 (status optional; from < 0 skips the env, status 0).
 __global__ void __launch_bounds__(kBlock) k_apply(Planes pl, int n, const int8_t* __restrict__ moves,
-                                                  const int8_t* __restrict__ player) {
+                                                  const int8_t* __restrict__ player,
+                                                  uint8_t* __restrict__ status) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const int f = moves[2 * i], t = moves[2 * i + 1];
+  if (status) status[i] = (f >= 0 && (f > 23 || t < 0 || t > OFF)) ? 1 : 0;
   if (f < 0 || f > 23 || t < 0 || t > OFF) return;
   Side s = side_from_record(pl.p0[i], pl.p1[i]);
   const uint32_t want_black = player ? (player[i] == -1 ? 1u : 0u) : s.black;
   const bool flip = want_black != s.black;
   if (flip) side_flip(s);
+  if (nib_get(s.own, f) == 0u || (t != OFF && nib_get(s.opp, t) != 0u)) {
+    if (status) status[i] = 1;
+    return;
+  }
   apply_move(s, f, t);
   if (flip) side_flip(s);
   uint4 a, b;

@@ -136,7 +136,7 @@ int set_error(int code, const char* what) { return fail(code, "%s", what); }
 
 extern "C" {
 
-int narde_version(void) { return 1; }
+int narde_version(void) { return 2; }
 const char* narde_last_error(void) { return g_err; }
 
 int narde_create(int device, int64_t num_envs, int64_t env_id_offset, uint64_t seed, int dice_mode,
@@ -182,7 +182,7 @@ int narde_create(int device, int64_t num_envs, int64_t env_id_offset, uint64_t s
                 hipGetErrorString(err));
   }
   k_reset<<<grid(num_envs), kBlock, 0, e->hstream>>>(e->pl, (int)num_envs, rng_of(e), 0u, nullptr,
-                                                     (int64_t)0);
+                                                     (int64_t)0, nullptr, 0);
   int rc = check_launch("k_reset");
   if (rc == NARDE_OK) {
     err = hipStreamSynchronize(e->hstream);
@@ -225,6 +225,9 @@ int narde_get_ply(const narde_env* e, uint32_t* t) {
 int narde_set_ply(narde_env* e, uint32_t t) {
   if (!e) return fail(NARDE_EINVAL, "NULL handle");
   DeviceGuard dg(e->device);
+  // every step / rollout still queued on any stream of the device first (they
+  // advance t): the private stream alone is not ordered with the caller's
+  HIP_TRY(hipDeviceSynchronize());
   k_set_ply<<<grid(e->n), kBlock, 0, e->hstream>>>(e->pl, (int)e->n, t);
   int rc = check_launch("k_set_ply");
   if (rc) return rc;
@@ -232,11 +235,12 @@ int narde_set_ply(narde_env* e, uint32_t t) {
   return NARDE_OK;
 }
 
-int narde_reset(narde_env* e, const uint8_t* mask, void* stream) {
+int narde_reset(narde_env* e, const uint8_t* mask, const uint8_t* opening, int pairs, void* stream) {
   if (!e) return fail(NARDE_EINVAL, "NULL handle");
+  if (opening && pairs <= 0) return fail(NARDE_EINVAL, "opening draws need pairs >= 1");
   DeviceGuard dg(e->device);
   k_reset<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), e->epoch, mask,
-                                                           (int64_t)-1);
+                                                           (int64_t)-1, opening, opening ? pairs : 0);
   e->epoch += 1;
   return check_launch("k_reset");
 }
@@ -382,7 +386,7 @@ int narde_get_stats(narde_env* e, int32_t* stats, void* stream) {
 int narde_apply_moves(narde_env* e, const int8_t* moves, const int8_t* player, void* stream) {
   if (!e || !moves) return fail(NARDE_EINVAL, "NULL argument");
   DeviceGuard dg(e->device);
-  k_apply<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, moves, player);
+  k_apply<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, moves, player, nullptr);
   return check_launch("k_apply");
 }
 
@@ -395,18 +399,18 @@ int narde_observe(narde_env* e, int32_t* obs, float* tes, void* stream) {
 }
 
 int narde_dqn_transition(narde_env* e, float* state, const int64_t* actions, const int32_t* reward,
-                         const uint8_t* terminated, const uint8_t* truncated, float* off_seen, int shaping,
-                         float* r_obs, float* r_next, int64_t* r_action, float* r_reward, float* r_done,
-                         float* r_prio, const float* max_prio, const int64_t* pos, int64_t capacity,
-                         void* stream) {
-  if (!e || !state || !actions || !reward || !terminated || !truncated || !r_obs || !r_next || !r_action ||
+                         const uint8_t* terminated, const uint8_t* truncated, const uint64_t* legal,
+                         int32_t* misc, float* off_seen, int shaping, float* r_obs, int64_t* r_action,
+                         float* r_reward, float* r_done, float* r_prio, const float* max_prio, const int64_t* pos,
+                         int64_t capacity, void* stream) {
+  if (!e || !state || !actions || !reward || !terminated || !truncated || !misc || !r_obs || !r_action ||
       !r_reward || !r_done || !r_prio || !max_prio || !pos || (shaping && !off_seen))
     return fail(NARDE_EINVAL, "NULL argument");
-  if (capacity < e->n) return fail(NARDE_EINVAL, "replay capacity below the env count");
+  if (capacity < 2 * e->n) return fail(NARDE_EINVAL, "replay capacity below twice the env count");
   if (e->n * 198 >= (int64_t(1) << 31)) return fail(NARDE_EINVAL, "too many envs for one transition launch");
   DeviceGuard dg(e->device);
-  TransArgs t{e->pl, (int)e->n, shaping, state, actions, reward, terminated, truncated, off_seen,
-              r_obs, r_next, r_action, r_reward, r_done, r_prio, max_prio, pos, capacity};
+  TransArgs t{e->pl, (int)e->n, shaping, state, actions, reward, terminated, truncated, legal, misc, off_seen,
+              r_obs, r_action, r_reward, r_done, r_prio, max_prio, pos, capacity};
   const int64_t quads = (e->n * 198 + 3) / 4;
   k_dqn_transition<<<(unsigned)((quads + kBlock - 1) / kBlock), kBlock, 0, (hipStream_t)stream>>>(t);
   return check_launch("k_dqn_transition");
@@ -605,13 +609,21 @@ int narde_host_apply_moves(narde_env* e, int64_t n, int8_t* board, uint8_t* off,
   int8_t* hb2 = ho.take<int8_t>(n * 24); int8_t* db2 = dq.take<int8_t>(n * 24);
   uint8_t* hoff2 = ho.take<uint8_t>(n * 2); uint8_t* doff2 = dq.take<uint8_t>(n * 2);
   uint8_t* hft2 = ho.take<uint8_t>(n * 2); uint8_t* dft2 = dq.take<uint8_t>(n * 2);
+  uint8_t* hst = ho.take<uint8_t>(n); uint8_t* dst = dq.take<uint8_t>(n);
   HIP_TRY(hipMemcpyAsync(e->d_in, e->h_in, hi.off, hipMemcpyHostToDevice, e->hstream));
   k_set_state<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, db, doff, dft, dp, nullptr, 0);
-  k_apply<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, dm, dp);
+  k_apply<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, dm, dp, dst);
   k_get_state<<<grid(n), kBlock, 0, e->hstream>>>(e->hpl, (int)n, db2, doff2, dft2, nullptr, nullptr);
   if ((rc = check_launch("host apply"))) return rc;
   HIP_TRY(hipMemcpyAsync(e->h_out, e->d_out, dq.off, hipMemcpyDeviceToHost, e->hstream));
   if ((rc = host_sync(e))) return rc;
+  // a move the record cannot hold (k_apply): nothing is written back
+  for (int64_t i = 0; i < n; ++i)
+    if (hst[i])
+      return fail(NARDE_EINVAL,
+                  "move (%d, %d) at index %lld is not executable: the source holds none of the "
+                  "mover's checkers or the target holds opponent checkers",
+                  (int)moves[2 * i], (int)moves[2 * i + 1], (long long)i);
   memcpy(board, hb2, n * 24); memcpy(off, hoff2, n * 2); memcpy(ft, hft2, n * 2);
   return NARDE_OK;
 }

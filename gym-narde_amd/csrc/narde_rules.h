@@ -454,12 +454,18 @@ struct StepOut {
 // flip_always: flip even after the game ended -- for callers that reset a
 // terminated env in the same ply anyway (auto-reset), where it saves the
 // divergent branch around the flip
+// nomove: the roll has no legal move whatever the board (a caller-given die
+// outside 1..6, see env_ply): list #1 is empty.
 NARDE_FN void env_step(Side& s, int d0, int d1, int code1, int code2, bool policy, uint32_t r1,
-                       uint32_t r2, StepOut& o, bool flip_always = false) {
+                       uint32_t r2, StepOut& o, bool flip_always = false, bool nomove = false) {
   // the mover's moves never change the opponent's points: one low mask
   // serves both lists
   const uint32_t low = block_lowmask(s.P);
   legal2_low(s, d0, d1, low, o.l1);
+  if (nomove) {
+    o.l1.L[0] = o.l1.L[1] = 0u;
+    o.l1.count = 0;
+  }
   o.L2 = 0u; o.d2 = 0; o.count2 = -1;
   const int n1 = o.l1.count;
   int f1 = -1, t1 = -1;
@@ -1270,8 +1276,12 @@ NARDE_FN void env_ply(Side& s, int4& st, const uint32_t r[4], bool have_dice, in
                       int dice_mode, bool policy, int c1, int c2, int max_steps, bool autoreset,
                       StepOut& o, int& term, int& trunc) {
   if (!have_dice) dice_from(r[0], dice_mode, d0, d1);
+  // a caller-given die outside 1..6 (no roll has one; the reference would
+  // scan with it, narde.py:64-77): a ply with no legal move
+  const bool bad = have_dice && ((uint32_t)(d0 - 1) > 5u || (uint32_t)(d1 - 1) > 5u);
+  if (bad) d0 = d1 = 1;
   const uint32_t mover_black = s.black;
-  env_step(s, d0, d1, c1, c2, policy, r[1], r[2], o, autoreset);
+  env_step(s, d0, d1, c1, c2, policy, r[1], r[2], o, autoreset, bad);
   s.elapsed += 1u;
   term = o.term;
   trunc = max_steps > 0 && s.elapsed >= (uint32_t)max_steps;
@@ -1302,6 +1312,11 @@ NARDE_FN void env_ply_full_with(Side& s, int4& st, const uint32_t r[4], uint32_t
                                 uint64_t pw, int max_steps, bool autoreset, TurnOut& o, int& term,
                                 int& trunc, Turn&& turn) {
   if (!have_dice) dice_from(r[0], dice_mode, d0, d1);
+  // a caller-given die outside 1..6: a turn with no legal move (the turn
+  // still runs on valid dice -- the device turn is wave-cooperative -- and
+  // its result is dropped)
+  const bool bad = have_dice && ((uint32_t)(d0 - 1) > 5u || (uint32_t)(d1 - 1) > 5u);
+  if (bad) { d0 = 1; d1 = 2; }
   uint32_t w[4] = {r[1], r[2], 0u, 0u};
   if (d0 == d1 && !play) {
     uint32_t q[4];
@@ -1310,7 +1325,17 @@ NARDE_FN void env_ply_full_with(Side& s, int4& st, const uint32_t r[4], uint32_t
     w[3] = q[1];
   }
   const uint32_t mover_black = s.black;
+  const Side before = s;
   turn(s, d0, d1, play, pw, w, o);
+  if (bad) {
+    s = before;
+    o.legal = 0ull;
+    o.played = ~0ull;
+    o.max_dice = 0;
+    o.term = s.off_own == 15u;
+    o.reward = o.term ? (s.off_opp > 0u ? 1 : 2) : 0;
+    if (!o.term) side_flip(s);
+  }
   s.elapsed += 1u;
   term = o.term;
   trunc = max_steps > 0 && s.elapsed >= (uint32_t)max_steps;

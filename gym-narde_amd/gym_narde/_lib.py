@@ -31,7 +31,7 @@ SIGNATURES = {
     "narde_num_envs": (_i64, [_vp]),
     "narde_get_ply": (_i32, [_vp, ctypes.POINTER(_u32)]),
     "narde_set_ply": (_i32, [_vp, _u32]),
-    "narde_reset": (_i32, [_vp, _vp, _vp]),
+    "narde_reset": (_i32, [_vp, _vp, _vp, _i32, _vp]),
     "narde_set_state": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "narde_get_state": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "narde_peek_dice": (_i32, [_vp, _vp, _vp]),
@@ -52,12 +52,12 @@ SIGNATURES = {
                                              _i32, _vp, _vp]),
     "narde_policy_masked_argmax576_dev": (_i32, [_i32, _vp, _i64, _vp, _i64, _vp, _u64, _vp, _i32, _vp,
                                                  _i64, _vp, _vp, _vp]),
-    "narde_dqn_transition": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp,
-                                    _vp, _vp, _i64, _vp]),
+    "narde_dqn_transition": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp,
+                                    _vp, _vp, _vp, _i64, _vp]),
     "narde_per_sample": (_i32, [_i32, _vp, _vp, _i64, _i64, _u64, _vp, _vp, ctypes.c_double, _vp, _vp, _vp,
                                 _vp, _vp]),
-    "narde_gather_batch": (_i32, [_i32, _vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                  _vp]),
+    "narde_gather_batch": (_i32, [_i32, _vp, _i64, _i32, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                  _vp, _vp]),
     "narde_rowmax_addend": (_i32, [_i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp]),
     "narde_dqn_loss": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, ctypes.c_float, _vp, _vp, _vp,
                               _vp, _vp, _vp]),

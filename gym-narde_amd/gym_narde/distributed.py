@@ -28,14 +28,16 @@ def rehearsal():
     return os.environ.get("NARDE_REHEARSAL", "0") == "1"
 
 
-def init_from_env(backend=None):
+def init_from_env(backend=None, force=False):
     """Initialise torch.distributed from torchrun's env (RANK/WORLD_SIZE/
     LOCAL_RANK/MASTER_*).  Returns (rank, world, local_rank); local_rank is the
-    GPU index to use (0 for every rank under rehearsal())."""
+    GPU index to use (0 for every rank under rehearsal()).  A world of one
+    process gets no process group unless `force` (then gather_stats runs the
+    real collective, e.g. to exercise the RCCL path on a one-GPU box)."""
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = 0 if rehearsal() else int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force) and not dist.is_initialized():
         if backend is None:
             backend = "gloo" if rehearsal() or not torch.cuda.is_available() else "nccl"
         if backend == "nccl":
@@ -48,8 +50,9 @@ def init_from_env(backend=None):
 
 def gather_stats(local_stats):
     """All-gather (B_local, 3) int32 statistics -> (B_global, 3) on every rank,
-    ordered by global env id."""
-    if not dist.is_initialized() or dist.get_world_size() == 1:
+    ordered by global env id (the local tensor itself when no process group
+    is initialised)."""
+    if not dist.is_initialized():
         return local_stats
     world = dist.get_world_size()
     src = local_stats.contiguous()

@@ -245,22 +245,34 @@ class DeviceReplay:
     proportional to priority**alpha, importance weights (N p)^-beta / max,
     beta anneals by beta_increment per sample, priorities = |td| + epsilon.
 
+    Layout (each observation stored once): the driver adds `stride` (= B,
+    its env count) transitions per step, env i at row (pos + i) % capacity,
+    so row j's next observation s' is the s of the same env's next
+    transition, row (j + stride) % capacity.  A step writes its transitions'
+    (a, r, done) and priority into rows whose s is already there (the
+    previous step's s', or seed()), and its s' into the next `stride` rows,
+    whose priority stays 0 -- never sampled -- until the next step completes
+    them.  So `capacity - stride` transitions are live at most
+    (capacity >= 2 * stride), `size` counts them, and sampling runs over the
+    first `rows` rows.
+
     The write cursor, beta and the max priority live in device scalars and
     are updated in place, so add/sample/update can be captured in a graph
-    (`pos` / `size` are host mirrors; sample() needs `size` fixed, i.e. a
+    (`pos` / `size` are host mirrors; sample() needs `rows` fixed, i.e. a
     full ring, to be replayed)."""
 
-    def __init__(self, capacity, state_size, device, alpha=0.6, beta=0.4, beta_increment=0.001,
+    def __init__(self, capacity, state_size, device, stride, alpha=0.6, beta=0.4, beta_increment=0.001,
                  epsilon=0.01):
-        self.capacity, self.device = int(capacity), device
+        self.capacity, self.stride, self.device = int(capacity), int(stride), device
+        if self.stride < 1 or self.capacity < 2 * self.stride:
+            raise ValueError("capacity must be at least twice the transitions per step (stride)")
         self.alpha, self.beta_increment, self.epsilon = alpha, beta_increment, epsilon
         z = dict(device=device)
         self.obs = torch.zeros((self.capacity, state_size), dtype=torch.float32, **z)
-        self.next_obs = torch.zeros((self.capacity, state_size), dtype=torch.float32, **z)
         self.action = torch.zeros((self.capacity, 2), dtype=torch.int64, **z)
         self.reward = torch.zeros(self.capacity, dtype=torch.float32, **z)
         self.done = torch.zeros(self.capacity, dtype=torch.float32, **z)
-        self.prio = torch.ones(self.capacity, dtype=torch.float32, **z)
+        self.prio = torch.zeros(self.capacity, dtype=torch.float32, **z)  # 0: empty / pending rows
         self.max_prio = torch.ones((), dtype=torch.float32, **z)
         self.beta_t = torch.full((), beta, dtype=torch.float64, **z)
         self.pos_t = torch.zeros((), dtype=torch.int64, **z)
@@ -273,35 +285,55 @@ class DeviceReplay:
     def beta(self):
         return float(self.beta_t)
 
-    def add(self, obs, action, reward, next_obs, done):
-        n = obs.shape[0]
-        if n > self.capacity:
-            raise ValueError("batch larger than the replay capacity")
-        idx = (torch.arange(n, device=self.device) + self.pos_t) % self.capacity
+    @property
+    def rows(self):
+        """Rows sampling runs over: the live transitions plus the pending s' rows."""
+        return min(self.size + self.stride, self.capacity) if self.size else 0
+
+    def next_index(self, idx):
+        """Row of each transition's next observation s'."""
+        return (idx + self.stride) % self.capacity
+
+    def seed(self, obs):
+        """Write the observations s of the transitions the next step adds
+        (rows pos .. pos + stride - 1, priority 0 until completed)."""
+        idx = (torch.arange(self.stride, device=self.device) + self.pos_t) % self.capacity
         self.obs.index_copy_(0, idx, obs)
-        self.next_obs.index_copy_(0, idx, next_obs)
+        self.prio.index_fill_(0, idx, 0.0)
+
+    def add(self, action, reward, next_obs, done):
+        """One step's `stride` transitions: k_dqn_transition's ring writes in
+        torch ops (the restatement it is tested against)."""
+        n = action.shape[0]
+        if n != self.stride:
+            raise ValueError("add() takes one step: stride transitions")
+        idx = (torch.arange(n, device=self.device) + self.pos_t) % self.capacity
         self.action.index_copy_(0, idx, action)
         self.reward.index_copy_(0, idx, reward)
         self.done.index_copy_(0, idx, done)
         self.prio.index_copy_(0, idx, self.max_prio.expand(n))
+        nidx = self.next_index(idx)
+        self.obs.index_copy_(0, nidx, next_obs)
+        self.prio.index_fill_(0, nidx, 0.0)
         self.pos_t.add_(n).remainder_(self.capacity)
         self.advance(n)
 
     def advance(self, n):
         """Host mirrors of one add() of n rows (also called per graph replay)."""
         self.pos = (self.pos + n) % self.capacity
-        self.size = min(self.size + n, self.capacity)
+        self.size = min(self.size + n, self.capacity - self.stride)
 
     def sample(self, batch, generator=None):
-        p = self.prio[: self.size] ** self.alpha
+        n = self.rows
+        p = self.prio[:n] ** self.alpha
         cdf = torch.cumsum(p, 0)
         total = cdf[-1]
         # inverse-CDF sampling (torch.multinomial over 1M categories spends
-        # ~0.5 ms renormalising one huge row)
+        # ~0.5 ms renormalising one huge row); pending rows have p = 0
         u = torch.rand(batch, device=p.device, generator=generator) * total
-        idx = torch.searchsorted(cdf, u, right=True).clamp_(max=self.size - 1)
+        idx = torch.searchsorted(cdf, u, right=True).clamp_(max=n - 1)
         probs_idx = p[idx] / total
-        w = (self.size * probs_idx) ** (-self.beta_t)
+        w = (n * probs_idx) ** (-self.beta_t)
         w = w / w.max()
         self.beta_t.add_(self.beta_increment).clamp_(max=1.0)
         return idx, w
@@ -316,19 +348,21 @@ class DeviceReplay:
         """sample() as k_per_sample: priority^alpha and its prefix sum in
         torch (rocPRIM scan), then the search, weights and beta step in one
         kernel with its own device Philox counter (`sample_ctr`)."""
-        p = self.prio[: self.size] ** self.alpha
+        n = self.rows
+        p = self.prio[:n] ** self.alpha
         cdf = torch.cumsum(p, 0)
         idx = torch.empty(batch, dtype=torch.int64, device=p.device)
         w = torch.empty(batch, dtype=torch.float32, device=p.device)
         _lib.check(_lib.load().narde_per_sample(
-            p.device.index, _lib.ptr(p), _lib.ptr(cdf), self.size, batch, int(seed) & (2 ** 64 - 1),
+            p.device.index, _lib.ptr(p), _lib.ptr(cdf), n, batch, int(seed) & (2 ** 64 - 1),
             _lib.ptr(self.sample_ctr), _lib.ptr(self.beta_t), float(self.beta_increment), _lib.ptr(idx),
             _lib.ptr(w), None if u_out is None else _f32(u_out), _lib.ptr(self._sample_scratch),
             _stream(p.device)), "narde_per_sample")
         return idx, w
 
     def gather(self, idx):
-        """(s, ns, a, r, d) rows of idx (k_gather_batch)."""
+        """(s, ns, a, r, d) rows of idx (k_gather_batch; ns from row
+        next_index(idx))."""
         B, ss = idx.shape[0], self.obs.shape[1]
         z = dict(device=self.obs.device)
         s = torch.empty((B, ss), dtype=torch.float32, **z)
@@ -337,7 +371,7 @@ class DeviceReplay:
         r = torch.empty(B, dtype=torch.float32, **z)
         d = torch.empty(B, dtype=torch.float32, **z)
         _lib.check(_lib.load().narde_gather_batch(
-            self.obs.device.index, _lib.ptr(idx), B, ss, _lib.ptr(self.obs), _lib.ptr(self.next_obs),
+            self.obs.device.index, _lib.ptr(idx), B, ss, _lib.ptr(self.obs), self.stride, self.capacity,
             _lib.ptr(self.action), _lib.ptr(self.reward), _lib.ptr(self.done), _lib.ptr(s), _lib.ptr(ns),
             _lib.ptr(a), _lib.ptr(r), _lib.ptr(d), _stream(self.obs.device)), "narde_gather_batch")
         return s, ns, a, r, d
@@ -383,7 +417,7 @@ class BatchedDQNDriver:
         self.opt = torch.optim.Adam(self.model.parameters(), lr=learning_rate, capturable=True, fused=True)
         # the fused learner's clip + Adam (two kernels instead of ~12 launches)
         self.fopt = FusedAdamClip(self.model.parameters(), lr=learning_rate, max_norm=10.0) if fused else None
-        self.replay = DeviceReplay(capacity, self.state_size, self.dev)
+        self.replay = DeviceReplay(capacity, self.state_size, self.dev, stride=env.num_envs)
         self.train_batch, self.gamma = int(train_batch), gamma
         z = dict(device=self.dev)
         self.eps_t = torch.full((), epsilon, dtype=torch.float32, **z)
@@ -402,6 +436,8 @@ class BatchedDQNDriver:
         self.off_seen = torch.zeros((B, 2), dtype=torch.float32, **z)
         self.state = self._observe()
         self._next = torch.empty_like(self.state)
+        self.misc = self._misc_now()
+        self.replay.seed(self.state)
         self.loss_t = torch.zeros((), dtype=torch.float32, **z)
         self.last_loss = None
         self.graph = None
@@ -420,15 +456,19 @@ class BatchedDQNDriver:
         x = self.env.observe().to(torch.float32)
         return x if out is None else out.copy_(x)
 
-    def _off_counts(self, obs):
-        """(B,2) borne-off counts (white, black) and the current player (+1/-1):
-        read off the 198-float obs (off/15 at 97 and 195, player one-hot at
-        196) when that is the observation, else from the env state."""
-        if self.obs_kind == "tesauro198":
-            off = torch.round(obs[:, 97:196:98] * 15.0)
-            return off, torch.where(obs[:, 196] > 0.5, 1.0, -1.0)
+    def _misc_now(self):
+        """(B,) int32 off_white | off_black << 4 | black_to_move << 10 of
+        every env's record now (k_dqn_transition's misc word)."""
         st = self.env.get_state()
-        return st["off"].to(torch.float32), st["player"].to(torch.float32)
+        off = st["off"].to(torch.int32)
+        return off[:, 0] | (off[:, 1] << 4) | ((st["player"] == -1).to(torch.int32) << 10)
+
+    def resync(self):
+        """After the env was stepped or reset outside the driver: observe
+        the current state again and make it the s of the next transitions."""
+        self.state.copy_(self._observe())
+        self.misc.copy_(self._misc_now())
+        self.replay.seed(self.state)
 
     @torch.no_grad()
     def act(self, x):
@@ -461,47 +501,58 @@ class BatchedDQNDriver:
         capture_graph() records).  Host-side counters: _host_after_step."""
         x = self.state
         actions = self.act(x)
-        _, reward, term, trunc, _ = self.env.step(actions.to(torch.int16))
+        _, reward, term, trunc, info = self.env.step(actions.to(torch.int16))
         if self.fused:
-            self._transition_fused(actions, reward, term, trunc)
+            self._transition_fused(actions, reward, term, trunc, info["legal"])
         else:
-            self._transition_torch(x, actions, reward, term, trunc)
+            self._transition_torch(actions, reward, term, trunc, info["legal"])
         self.tag_t.add_(1)
         loss = None
         for _ in range(self.updates_per_step):
             loss = self._update_body()
         return loss
 
-    def _transition_torch(self, x, actions, reward, term, trunc):
+    def _transition_torch(self, actions, reward, term, trunc, legal):
         """Shaping + replay write + s <- s' in torch ops (the restatement
         k_dqn_transition is tested against; the int24 observation path)."""
         r = reward.to(torch.float32)
-        done = (term | trunc).to(torch.float32)
+        t, u = term.bool(), trunc.bool()
+        done = (t | u).to(torch.float32)
         nxt = self._observe(out=self._next)
+        post = self._misc_now()
         if self.shaping:
-            # train_deepq_pytorch.py:885-908: +1 per checker newly borne off
-            # and +0.1 x total off, for env.unwrapped.current_player read AFTER
-            # the step (the reference reads the post-flip player)
-            off, player = self._off_counts(nxt)
-            col = (player < 0).long()
-            now = off.gather(1, col.unsqueeze(1)).squeeze(1)
-            before = self.off_seen.gather(1, col.unsqueeze(1)).squeeze(1)
-            r = r + (now - before).clamp(min=0) + 0.1 * now
-            self.off_seen.scatter_(1, col.unsqueeze(1), now.unsqueeze(1))
+            # train_deepq_pytorch.py:892-912: +1 per checker newly borne off
+            # and +0.1 x the count, for env.unwrapped.current_player read
+            # AFTER the step -- at a step that ends the game (auto-reset has
+            # already started the next one) the pre-step record's: the mover
+            # (the winner, 15 off) if it terminated, the other player if
+            # truncated; none without a legal move (:869-873)
+            pre = self.misc
+            moved = (legal & 0xFFFFFFFFFFFF) != 0
+            pre_black = (pre >> 10) & 1
+            black = torch.where(t, pre_black, torch.where(u, 1 - pre_black, (post >> 10) & 1)).long()
+            src = torch.where(t | u, pre, post)
+            cnt = torch.where(black == 1, (src >> 4) & 15, src & 15).to(torch.float32)
+            now = torch.where(t, torch.full_like(cnt, 15.0), cnt)
+            before = self.off_seen.gather(1, black.unsqueeze(1)).squeeze(1)
+            r = torch.where(moved, r + (now - before).clamp(min=0) + 0.1 * now, r)
+            seen = self.off_seen.scatter(1, black.unsqueeze(1), now.unsqueeze(1))
+            self.off_seen.copy_(torch.where(moved.unsqueeze(1), seen, self.off_seen))
             self.off_seen.mul_((1.0 - done).unsqueeze(1))  # new episode: trackers restart at 0
-        self.replay.add(x, actions, r, nxt, done)
+        self.misc.copy_(post)
+        self.replay.add(actions, r, nxt, done)
         self.state.copy_(nxt)
 
-    def _transition_fused(self, actions, reward, term, trunc):
+    def _transition_fused(self, actions, reward, term, trunc, legal):
         rp, n = self.replay, self.env.num_envs
         if not (self.state.is_contiguous() and actions.is_contiguous() and actions.dtype == torch.int64):
             raise ValueError("state / actions layout")
         self.env.handle.call(
             "narde_dqn_transition", _lib.ptr(self.state), _lib.ptr(actions), _lib.ptr(reward),
-            _lib.ptr(term), _lib.ptr(trunc), _lib.ptr(self.off_seen), int(self.shaping),
-            _lib.ptr(rp.obs), _lib.ptr(rp.next_obs), _lib.ptr(rp.action), _lib.ptr(rp.reward),
-            _lib.ptr(rp.done), _lib.ptr(rp.prio), _lib.ptr(rp.max_prio), _lib.ptr(rp.pos_t),
-            rp.capacity, ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream))
+            _lib.ptr(term), _lib.ptr(trunc), _lib.ptr(legal), _lib.ptr(self.misc), _lib.ptr(self.off_seen),
+            int(self.shaping), _lib.ptr(rp.obs), _lib.ptr(rp.action), _lib.ptr(rp.reward), _lib.ptr(rp.done),
+            _lib.ptr(rp.prio), _lib.ptr(rp.max_prio), _lib.ptr(rp.pos_t), rp.capacity,
+            ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream))
         rp.pos_t.add_(n).remainder_(rp.capacity)
         rp.advance(n)
 
@@ -518,15 +569,16 @@ class BatchedDQNDriver:
         eagerly on a side stream as torch's capture rules ask."""
         if self.updates_per_step != 1:
             raise ValueError("graph capture needs updates_per_step == 1")
-        cap = self.replay.capacity
-        need = max(0, -(-(cap - self.replay.size - warmup * self.env.num_envs) // self.env.num_envs))
+        cap, B = self.replay.capacity, self.env.num_envs
+        # steps until the ring is full (size = capacity - B live transitions)
+        need = max(0, -(-(cap - B - self.replay.size - warmup * B) // B))
         side = torch.cuda.Stream(self.dev)
         side.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.stream(side):
             for _ in range(need + warmup):
                 self.step()
         torch.cuda.current_stream(self.dev).wait_stream(side)
-        if self.replay.size != cap or self.replay.size < self.train_batch:
+        if self.replay.rows != cap or self.replay.size < self.train_batch:
             raise RuntimeError("replay ring not full before capture")
         g = torch.cuda.CUDAGraph()
         g.register_generator_state(self.gen)
@@ -596,7 +648,7 @@ class BatchedDQNDriver:
         branch, in torch ops (the restatement the fused path is tested
         against)."""
         idx, w = self.replay.sample(self.train_batch, generator=self.gen)
-        s, ns = self.replay.obs[idx], self.replay.next_obs[idx]
+        s, ns = self.replay.obs[idx], self.replay.obs[self.replay.next_index(idx)]
         a, r, d = self.replay.action[idx], self.replay.reward[idx], self.replay.done[idx]
         f = self.model.features(s)
         q1 = self.model.move1_head(f).gather(1, a[:, :1]).squeeze(1)

@@ -133,10 +133,25 @@ class VecNardeEnv:
         self.handle.ply = t
 
     # ------------------------------------------------------------ API
-    def reset(self, mask=None):
-        """NardeEnv.reset for all (or the masked) envs; returns obs (B,24) int32."""
-        m = None if mask is None else self._dev(mask, self.torch.uint8, (self.num_envs,))
-        self.handle.call("narde_reset", _lib.ptr(m), self._s())
+    def reset(self, mask=None, opening=None):
+        """NardeEnv.reset (narde_env.py:105-120) for all (or the masked) envs;
+        returns obs (B,24) int32.  opening: (B,K,2) uint8 opening draws
+        (white roll, black roll) per env in the reference's draw order -- the
+        first pair of different dice decides who moves first, pairs with a
+        die outside 1..6 are padding -- or None for the device draw (also
+        for an env whose row has no deciding pair)."""
+        B = self.num_envs
+        m = None if mask is None else self._dev(mask, self.torch.uint8, (B,))
+        o, pairs = None, 0
+        if opening is not None:
+            o = self.torch.as_tensor(opening, device=self.device).to(self.torch.uint8).contiguous()
+            if o.dim() == 2:
+                o = o.reshape(B, 1, 2)
+            if o.dim() != 3 or o.shape[0] != B or o.shape[2] != 2 or o.shape[1] < 1:
+                raise ValueError(f"opening must be (B, K, 2) with B = {B}, got {tuple(o.shape)}")
+            pairs = int(o.shape[1])
+        self.handle.call("narde_reset", _lib.ptr(m), _lib.ptr(o), pairs, self._s())
+        self._keep = (m, o)  # inputs alive until the kernel has read them
         return self.observe()
 
     def observe(self):
@@ -284,9 +299,36 @@ class VecNardeEnv:
                          _lib.ptr(bufs["legal"]), _lib.ptr(bufs["actions"]), self._s())
         return bufs
 
-    def stats(self):
-        """(B,3) int32 {episodes finished, white points, black points}."""
-        out = self.torch.empty((self.num_envs, 3), dtype=self.torch.int32, device=self.device)
+    def rollout_launcher(self, plies, bufs):
+        """rollout(plies, bufs) pre-bound: a zero-argument callable that makes
+        exactly one ctypes call (one kernel launch on the stream current
+        NOW), for hot loops where the per-call Python of rollout() would
+        show (the buffers must stay alive and unmoved while it is used)."""
+        for v in bufs.values():
+            if v is not None and v.shape[0] < plies:
+                raise ValueError("rollout buffer shorter than plies")
+        fn = self.handle.lib.narde_rollout_full if self.full else self.handle.lib.narde_rollout
+        name = "narde_rollout_full" if self.full else "narde_rollout"
+        args = (self.handle.h, int(plies), _lib.ptr(bufs["obs"]), _lib.ptr(bufs["reward"]),
+                _lib.ptr(bufs["terminated"]), _lib.ptr(bufs["truncated"]), _lib.ptr(bufs["legal"]),
+                _lib.ptr(bufs["actions"]), self._s())
+
+        def launch():
+            rc = fn(*args)
+            if rc:
+                _lib.check(rc, name)
+
+        launch.bufs = bufs  # keeps the buffers referenced as long as the launcher
+        return launch
+
+    def stats(self, out=None):
+        """(B,3) int32 {episodes finished, white points, black points} (into
+        `out` if given: a preallocated (B,3) int32 device tensor)."""
+        if out is None:
+            out = self.torch.empty((self.num_envs, 3), dtype=self.torch.int32, device=self.device)
+        elif (tuple(out.shape) != (self.num_envs, 3) or out.dtype != self.torch.int32
+              or out.device != self.device or not out.is_contiguous()):
+            raise ValueError("out must be a contiguous (B,3) int32 tensor on the env's device")
         self.handle.call("narde_get_stats", _lib.ptr(out), self._s())
         return out
 

@@ -35,7 +35,7 @@ def test_binding_matches_header():
 
 def test_version_and_error_string():
     lib = _lib.load()
-    assert lib.narde_version() == 1
+    assert lib.narde_version() == 2
     assert isinstance(lib.narde_last_error(), bytes)
 
 
@@ -63,15 +63,15 @@ def test_argument_errors_are_einval_before_any_device_call():
         ("narde_step", (N, N, N, N, N, N, N, N, N, 1, N)),
         ("narde_step_full", (N, N, N, N, N, N, N, N, N, 1, N)),
         ("narde_rollout", (N, 10, N, N, N, N, N, N, N)),
-        ("narde_reset", (N, N, N)),
+        ("narde_reset", (N, N, N, 0, N)),
         ("narde_legal_full", (N, N, N, N)),
         ("narde_legal_mask576_move2", (N, N, N, N, N)),
-        ("narde_dqn_transition", (N, N, N, N, N, N, N, 1, N, N, N, N, N, N, N, N, 16, N)),
+        ("narde_dqn_transition", (N, N, N, N, N, N, N, N, N, 1, N, N, N, N, N, N, N, 16, N)),
         ("narde_policy_masked_argmax576", (0, N, 576, N, 16, 0.1, 0, 0, 0, N, N)),
         ("narde_policy_masked_argmax576_dev", (0, N, 576, N, 16, N, 0, N, 0, N, 0, N, N, N)),
         ("narde_violates_block_rule", (0, N, 4, N, N)),
         ("narde_per_sample", (0, N, N, 100, 64, 0, N, N, 0.001, N, N, N, N, N)),
-        ("narde_gather_batch", (0, N, 64, 198, N, N, N, N, N, N, N, N, N, N, N)),
+        ("narde_gather_batch", (0, N, 64, 198, N, 64, 128, N, N, N, N, N, N, N, N, N)),
         ("narde_rowmax_addend", (0, N, 576, N, 576, N, 64, N, N)),
         ("narde_dqn_loss", (0, N, N, N, N, N, N, N, 64, 0.99, N, N, N, N, N, N)),
         ("narde_prio_update", (0, N, N, 64, 0.01, N, N, N, 0.01, 0.995, N)),

@@ -72,28 +72,45 @@ def test_expand_mask_and_masked_argmax():
 
 
 def test_replay_priority_rules():
-    r = DeviceReplay(10, 4, "cpu")
-    obs = torch.arange(24, dtype=torch.float32).view(6, 4)
-    r.add(obs, torch.zeros(6, 2, dtype=torch.int64), torch.ones(6), obs, torch.zeros(6))
-    assert r.size == 6 and r.pos == 6
-    r.add(obs, torch.zeros(6, 2, dtype=torch.int64), torch.ones(6), obs, torch.zeros(6))
-    assert r.size == 10 and r.pos == 2  # ring wrap
-    assert torch.equal(r.obs[0], obs[4]) and torch.equal(r.obs[2], obs[2])
-    r.update(torch.tensor([3]), torch.tensor([5.0]))
-    assert float(r.prio[3]) == pytest.approx(5.01) and float(r.max_prio) == pytest.approx(5.01)
+    """DeviceReplay's ring (each observation once, s' = row + stride) and the
+    reference's PER rules (train_deepq_pytorch.py:279-342)."""
+    r = DeviceReplay(10, 4, "cpu", stride=3)
+    obs = [torch.full((3, 4), float(k)) for k in range(6)]
+    r.seed(obs[0])
+    act = lambda k: torch.full((3, 2), k, dtype=torch.int64)  # noqa: E731
+    r.add(act(0), torch.ones(3), obs[1], torch.zeros(3))
+    assert r.size == 3 and r.pos == 3 and r.rows == 6
+    assert torch.equal(r.obs[0:3], obs[0]) and torch.equal(r.obs[3:6], obs[1])
+    assert r.prio[0:3].tolist() == [1.0] * 3 and r.prio[3:6].tolist() == [0.0] * 3  # s' rows pending
+    for k in range(1, 4):
+        r.add(act(k), torch.ones(3), obs[k + 1], torch.zeros(3))
+    # 12 rows written into 10: the ring wrapped; the live transitions are the
+    # 7 = capacity - stride rows that are not pending
+    assert r.pos == 2 and r.size == 7 and r.rows == 10
+    pend = r.next_index(torch.arange(9, 12) % 10)  # the last step's s' rows: 2, 3, 4
+    assert sorted(pend.tolist()) == [2, 3, 4] and float(r.prio[pend].sum()) == 0.0
+    for j in range(10):  # every live row's next observation is its env's next s
+        if float(r.prio[j]) > 0:
+            k = int(r.action[j, 0])
+            assert torch.equal(r.obs[j], obs[k][0]) and torch.equal(r.obs[(j + 3) % 10], obs[k + 1][0])
+    r.update(torch.tensor([6]), torch.tensor([5.0]))
+    assert float(r.prio[6]) == pytest.approx(5.01) and float(r.max_prio) == pytest.approx(5.01)
     g = torch.Generator().manual_seed(0)
     idx, w = r.sample(20000, generator=g)
     p = r.prio ** r.alpha
     p = p / p.sum()
     freq = torch.bincount(idx, minlength=10).float() / 20000
     assert torch.allclose(freq, p, atol=0.02)
+    assert float(freq[pend].sum()) == 0.0  # pending rows are never sampled
     # importance weights: (N p)^-beta normalised by the max
     beta = r.beta - r.beta_increment
     exp = (10 * p[idx]) ** (-beta)
     assert torch.allclose(w, exp / exp.max())
     # new transitions get the running max priority
-    r.add(obs[:1], torch.zeros(1, 2, dtype=torch.int64), torch.ones(1), obs[:1], torch.zeros(1))
-    assert float(r.prio[2]) == pytest.approx(5.01)
+    r.add(act(9), torch.ones(3), obs[0], torch.zeros(3))
+    assert float(r.prio[2]) == pytest.approx(5.01) and float(r.prio[5]) == 0.0
+    with pytest.raises(ValueError):
+        DeviceReplay(5, 4, "cpu", stride=3)  # capacity below twice the stride
 
 
 def test_features_nograd_matches_module():

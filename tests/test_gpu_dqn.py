@@ -77,7 +77,7 @@ def test_reference_step_accepts_driver_actions():
 
     env, drv = make(n=2048)
     env.selfplay(40)
-    drv.state = drv._observe()
+    drv.resync()
     has1 = expand_mask(env.legal_mask()).any(1).cpu().numpy()
     a = drv.act(drv.state).cpu().numpy().astype(np.int16)
     st = {k: v.cpu().numpy() for k, v in env.get_state().items()}
@@ -129,7 +129,7 @@ def test_graph_replay_matches_driver_semantics():
     env, drv = make(n=n)
     drv.capture_graph(warmup=2)
     cap = drv.replay.capacity
-    assert drv.replay.size == cap
+    assert drv.replay.rows == cap and drv.replay.size == cap - n
     steps0, train0 = drv.steps, drv.train_steps
     drv.eps_t.fill_(0.0)
     for k in range(12):
@@ -186,46 +186,55 @@ def test_policy_kernel_device_scalars_and_fused_addend():
 def test_fused_transition_matches_torch_restatement(shaping, pos):
     """k_dqn_transition (observation + reward shaping + replay write + s <- s')
     is bit-exact against the driver's torch restatement on the same step,
-    including a replay-ring wrap and games that end in the step."""
+    including a replay-ring wrap, games that end in the step (terminated and
+    truncated: the shaping reads the pre-step record there), and envs with
+    no legal move (no shaping)."""
     from gym_narde.dqn import BatchedDQNDriver
     from gym_narde.vector import VecNardeEnv
 
     n = 4096
-    env = VecNardeEnv(n, device="cuda:0", seed=23)
+    env = VecNardeEnv(n, device="cuda:0", seed=23, max_episode_steps=261)
     env.selfplay(260)
     drv = BatchedDQNDriver(env, capacity=3 * n, train_batch=1024, shaping=shaping)
-    drv.state = drv._observe()
+    drv.resync()
     g = torch.Generator(device="cuda:0").manual_seed(4)
     off0 = torch.randint(0, 16, (n, 2), device="cuda:0", generator=g).float()
-    state0 = drv.state.clone()
+    state0, misc0 = drv.state.clone(), drv.misc.clone()
     rp = drv.replay
-    p0 = 3 * n - 100 if pos == "wrap" else n  # ring wrap (per-float path) / 16-B rows (vector path)
-    rp.pos_t.fill_(p0)
+    # ring wrap of the s' rows (per-float path) / 16-B aligned contiguous rows (vector path)
+    p0 = 3 * n - 100 if pos == "wrap" else n
     rp.max_prio.fill_(2.5)
     a = drv.act(drv.state)
-    _, reward, term, trunc, _ = env.step(a.to(torch.int16))
-    reward, term, trunc = reward.clone(), term.clone(), trunc.clone()
-    assert int((term | trunc).sum()) > 0
+    _, reward, term, trunc, info = env.step(a.to(torch.int16))
+    reward, term, trunc, legal = reward.clone(), term.clone(), trunc.clone(), info["legal"].clone()
+    assert int(term.sum()) > 0 and int(trunc.sum()) > 0
+    assert int(((legal & 0xFFFFFFFFFFFF) == 0).sum()) > 0
 
     def run(fn):
         drv.state.copy_(state0)
         drv.off_seen.copy_(off0)
-        for t in (rp.obs, rp.next_obs, rp.action, rp.reward, rp.done, rp.prio):
+        drv.misc.copy_(misc0)
+        for t in (rp.obs, rp.action, rp.reward, rp.done, rp.prio):
             t.zero_()
         rp.pos_t.fill_(p0)
         fn()
-        return [t.clone() for t in (drv.state, drv.off_seen, rp.obs, rp.next_obs, rp.action, rp.reward,
+        return [t.clone() for t in (drv.state, drv.off_seen, drv.misc, rp.obs, rp.action, rp.reward,
                                     rp.done, rp.prio, rp.pos_t)]
 
-    fused = run(lambda: drv._transition_fused(a, reward, term, trunc))
-    ref = run(lambda: drv._transition_torch(drv.state, a, reward, term, trunc))
-    names = ["state", "off_seen", "obs", "next_obs", "action", "reward", "done", "prio", "pos"]
+    fused = run(lambda: drv._transition_fused(a, reward, term, trunc, legal))
+    ref = run(lambda: drv._transition_torch(a, reward, term, trunc, legal))
+    names = ["state", "off_seen", "misc", "obs", "action", "reward", "done", "prio", "pos"]
     for nm, x, y in zip(names, fused, ref):
         assert torch.equal(x, y), nm
-    if pos == "wrap":  # rows at both ends of the ring were written
-        assert float(ref[7][0]) == 2.5 and float(ref[7][3 * n - 1]) == 2.5
-    else:
-        assert float(ref[7][n]) == 2.5 and float(ref[7][2 * n - 1]) == 2.5 and float(ref[7][2 * n]) == 0.0
+    prio, obs = ref[7], ref[3]
+    rows = (torch.arange(n, device="cuda:0") + p0) % (3 * n)
+    nrows = (rows + n) % (3 * n)
+    assert bool((prio[rows] == 2.5).all()) and bool((prio[nrows] == 0).all())
+    assert torch.equal(obs[nrows], ref[0])  # s' stored once, in the next step's rows
+    if shaping:  # the winner of a terminal step is credited its 15 checkers off
+        r = ref[5][rows]
+        t = term.bool()
+        assert bool((r[t] >= reward[t].float() + 1.5).all())
 
 
 # ------------------------------------------------ fused learner kernels
@@ -236,7 +245,7 @@ def test_per_sample_kernel_vs_torch():
     from gym_narde.dqn import DeviceReplay
 
     n, B = 300000, 4096
-    rp = DeviceReplay(n, 4, "cuda:0")
+    rp = DeviceReplay(n, 4, "cuda:0", stride=1)
     g = torch.Generator(device="cuda:0").manual_seed(3)
     rp.prio.copy_(torch.rand(n, device="cuda:0", generator=g) * 3 + 0.01)
     rp.prio[:1000] = 50.0  # a heavy head
@@ -267,15 +276,17 @@ def test_per_sample_kernel_vs_torch():
 def test_gather_batch_and_rowmax_addend_exact():
     from gym_narde.dqn import DeviceReplay, rowmax_addend
 
-    rp = DeviceReplay(5000, 198, "cuda:0")
+    rp = DeviceReplay(5000, 198, "cuda:0", stride=1234)
     g = torch.Generator(device="cuda:0").manual_seed(5)
-    for t in (rp.obs, rp.next_obs, rp.reward, rp.done):
+    for t in (rp.obs, rp.reward, rp.done):
         t.copy_(torch.rand(t.shape, device="cuda:0", generator=g))
     rp.action.copy_(torch.randint(0, 576, rp.action.shape, device="cuda:0", generator=g))
     idx = torch.randint(0, 5000, (4096,), device="cuda:0", generator=g)
     s, ns, a, r, d = rp.gather(idx)
-    for got, src in ((s, rp.obs), (ns, rp.next_obs), (a, rp.action), (r, rp.reward), (d, rp.done)):
-        assert torch.equal(got, src[idx])
+    nxt = (idx + 1234) % 5000
+    for got, src in ((s, rp.obs[idx]), (ns, rp.obs[nxt]), (a, rp.action[idx]), (r, rp.reward[idx]),
+                     (d, rp.done[idx])):
+        assert torch.equal(got, src)
     base = torch.randn((4096, 576), device="cuda:0", generator=g)
     tab = torch.randn((576, 576), device="cuda:0", generator=g)
     rows = torch.randint(0, 576, (4096,), device="cuda:0", generator=g)
@@ -315,7 +326,7 @@ def test_dqn_loss_kernel_vs_torch_autograd():
 def test_prio_update_kernel_exact():
     from gym_narde.dqn import DeviceReplay
 
-    rp = DeviceReplay(10000, 4, "cuda:0")
+    rp = DeviceReplay(10000, 4, "cuda:0", stride=1)
     g = torch.Generator(device="cuda:0").manual_seed(2)
     idx = torch.randperm(10000, device="cuda:0", generator=g)[:4096]
     td = torch.rand(4096, device="cuda:0", generator=g) * 7
@@ -351,7 +362,7 @@ def test_fused_and_torch_learners_agree_on_one_update():
     # the fused minibatch, replayed through torch ops on a copy of the model
     rp.sample_ctr.copy_(sample_state[0]); rp.beta_t.copy_(sample_state[1]); rp.prio.copy_(sample_state[2])
     idx, w = rp.sample_fused(drv.train_batch, drv.seed)
-    s, ns, a, r, d = (rp.obs[idx], rp.next_obs[idx], rp.action[idx], rp.reward[idx], rp.done[idx])
+    s, ns, a, r, d = (rp.obs[idx], rp.obs[rp.next_index(idx)], rp.action[idx], rp.reward[idx], rp.done[idx])
     import copy as _copy
     model = _copy.deepcopy(drv.model)
     model.load_state_dict(state)
