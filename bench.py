@@ -18,6 +18,7 @@ statistics.
 Prints ONE JSON line on rank 0 (fields: DESIGN.md section 6).
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -231,6 +232,16 @@ def main():
         del ramp, rbufs
     ramp_ms = (time.perf_counter() - ramp_t0) * 1e3
 
+    # the timed region's own host path warmed up (untimed): its launcher, and
+    # its two timing events (a HIP event is created at its first record)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        ev0.record()
+        full_launch()
+        ev1.record()
+    torch.cuda.synchronize()
+    ramp_n += 3
+
     run_plies(args.warmup)
     # per-env statistics land here; the timed region gathers them only when
     # there is something to gather (N > 1: the one RCCL all-gather)
@@ -244,17 +255,22 @@ def main():
     # region (no per-launch event between them): kernel time per launch =
     # that span / launches, i.e. the launches' durations plus the gaps
     # between them (an upper bound on the dispatch duration rocprof shows)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    gc.disable()  # no collector pass inside a region this short
     t0 = time.perf_counter()
     ev0.record()
     launches = run_plies(K)
     ev1.record()
+    t_sub = time.perf_counter()
     if world > 1:
         stats = D.gather_stats(env.stats(out=stats_buf))
     torch.cuda.synchronize()
+    t_wait = time.perf_counter()
     barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    gc.enable()
+    host_us = {"submit": round((t_sub - t0) * 1e6, 1), "wait": round((t_wait - t_sub) * 1e6, 1),
+               "close": round((elapsed - (t_wait - t0)) * 1e6, 1)}
     span_ms = ev0.elapsed_time(ev1)
     if world == 1:
         stats = env.stats(out=stats_buf)
@@ -477,6 +493,9 @@ def main():
                 "bytes_per_launch": nbytes,
                 "kernel_ms": round(kern_ms, 5),
             },
+            # rank 0's wall split of the timed region: launches submitted,
+            # waiting for them (and the gather), the closing barrier + sync
+            "timed_region_host_us": host_us,
             "cpu_baseline": cpu,
             "api_step": {
                 "kernel": "k_step (one ply per launch, same outputs)",

@@ -28,33 +28,13 @@ struct StepArgs {
   Outs out;
 };
 
-// (DIAGNOSTIC bit 64: a store guarded by a condition the compiler cannot
-// fold but that never holds at run time)
-#if NARDE_DIAG_ABLATE & 64
-__device__ int g_diag_never;
-#define NARDE_DIAG_STORE_GUARD if (g_diag_never != 12345) return;
-#else
-#define NARDE_DIAG_STORE_GUARD
-#endif
-
+// Every per-ply output is a plain store.  Measured against non-temporal
+// stores on sustained 1,000-ply REF2 rollouts (one box): plain 0.1265 ms
+// per 100 plies, non-temporal obs rows 0.135 (the narrow outputs' policy
+// did not matter).
 template <class T>
 __device__ __forceinline__ void st_out(T* p, T v) {
-  NARDE_DIAG_STORE_GUARD
-#if NARDE_OBS_STORE == 2 || NARDE_OBS_STORE == 4
-  __builtin_nontemporal_store(v, p);
-#else
   *p = v;
-#endif
-}
-__device__ __forceinline__ void st_out(int4* p, int4 v) {
-  NARDE_DIAG_STORE_GUARD
-#if NARDE_OBS_STORE == 2 || NARDE_OBS_STORE == 3
-  typedef int v4i __attribute__((ext_vector_type(4)));
-  const v4i x = {v.x, v.y, v.z, v.w};
-  __builtin_nontemporal_store(x, reinterpret_cast<v4i*>(p));
-#else
-  *p = v;
-#endif
 }
 
 __device__ __forceinline__ int4 obs_quad(const Side& s, int q) {
@@ -88,9 +68,6 @@ __device__ __forceinline__ void store_obs_wave(int32_t* __restrict__ obs, size_t
 // LDS round trip costs more than the scattered stores (sustained 1,000-ply
 // rollouts, one box: 0.592 vs 0.614 ms per 100 plies); REF2's k_step keeps
 // the LDS path (6.1 vs 6.7 us per launch).
-#ifndef NARDE_FULL4_OBS_LDS
-#define NARDE_FULL4_OBS_LDS 0
-#endif
 __device__ __forceinline__ void store_common(const Outs& out, size_t ix, const Side& s, int reward,
                                              int term, int trunc, int4* lds, bool via_lds) {
   if (out.obs) {
@@ -105,7 +82,7 @@ __device__ __forceinline__ void store_common(const Outs& out, size_t ix, const S
 __device__ __forceinline__ void store_outs(const Outs& out, size_t ix, const Side& s,
                                            const StepOut& o, int term, int trunc, int4* lds,
                                            bool wave_full) {
-  store_common(out, ix, s, o.reward, term, trunc, lds, NARDE_OBS_STORE != 0 && wave_full);
+  store_common(out, ix, s, o.reward, term, trunc, lds, wave_full);
   if (out.legal) st_out(out.legal + ix, (uint64_t)compact_legal(o.l1));
   if (out.act_out)
     st_out(reinterpret_cast<uint32_t*>(out.act_out) + ix,
@@ -115,8 +92,8 @@ __device__ __forceinline__ void store_outs(const Outs& out, size_t ix, const Sid
 __device__ __forceinline__ void store_outs(const Outs& out, size_t ix, const Side& s,
                                            const TurnOut& o, int term, int trunc, int4* lds,
                                            bool wave_full) {
-  store_common(out, ix, s, o.reward, term, trunc, lds,
-               NARDE_FULL4_OBS_LDS && NARDE_OBS_STORE != 0 && wave_full);
+  (void)wave_full;
+  store_common(out, ix, s, o.reward, term, trunc, lds, false);
   if (out.legal) st_out(out.legal + ix, o.legal);
   if (out.played) st_out(out.played + ix, o.played);
 }
@@ -210,19 +187,11 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
 // record stays in VGPRs, each ply's outputs (if requested) are streamed to
 // [ply][n] rollout buffers.  kOut = false: statistics only (a separate
 // instantiation, so profiles tell the two apart).
-#ifndef NARDE_ROLLOUT_MINW
-#define NARDE_ROLLOUT_MINW 1
-#endif
 template <bool kOut, bool kFull>
-__global__ void __launch_bounds__(kBlock, NARDE_ROLLOUT_MINW) k_rollout(Planes pl, int n, Rng g, int plies, int max_steps,
-                                                    Outs out) {
+__global__ void __launch_bounds__(kBlock, 1) k_rollout(Planes pl, int n, Rng g, int plies, int max_steps,
+                                                       Outs out) {
   OBS_LDS_DECL
   COOP_LDS_DECL
-#ifdef NARDE_DIAG_LDS_PAD
-  // DIAGNOSTIC: LDS the kernel never uses, to cap its occupancy
-  __shared__ uint32_t diag_pad[NARDE_DIAG_LDS_PAD / 4];
-  if (n == -12345) ((volatile uint32_t*)diag_pad)[threadIdx.x] = (uint32_t)plies;
-#endif
   const int i = blockIdx.x * kBlock + threadIdx.x;
   const bool valid = i < n;
   if (!kFull && !valid) return;  // FULL4 lanes stay: its turn is wave-cooperative
@@ -263,45 +232,36 @@ __global__ void __launch_bounds__(kBlock, NARDE_ROLLOUT_MINW) k_rollout(Planes p
 //     in advance), and the per-ply outputs of the PREVIOUS block, expanded
 //     from the ply results the producers left in LDS and stored so that
 //     every wave-wide store is one contiguous 1 KiB.
-// Plies go in blocks of kPcR with one workgroup barrier per block; LDS holds
-// two slots of each ring (draws and results), 16 + 96 KiB.
+// Plies go in barrier blocks (pc_block) with one workgroup barrier per
+// block; LDS holds two slots of each ring (draws and results), 16 + 96 KiB.
 // Equivalent, bit for bit, to `plies` narde_step(NULL, NULL, autoreset=1).
-#ifndef NARDE_PC_SETS
-#define NARDE_PC_SETS 1
-#endif
-// rule (producer) waves per workgroup, each with its consumer wave(s)
-#ifndef NARDE_PC_GROUPS
-#define NARDE_PC_GROUPS 4
-#endif
-constexpr int kPcGroups = NARDE_PC_GROUPS;
-constexpr int kPcEnvs = 64 * kPcGroups;        // envs per workgroup
-constexpr int kPcSets = NARDE_PC_SETS;        // consumer waves per producer wave
-constexpr int kPcThreads = (1 + kPcSets) * kPcEnvs;  // producers + consumers
-// plies per barrier block (tuning knob: 3, 4 and 5 time the same)
-#ifndef NARDE_PC_R
-#define NARDE_PC_R 4
-#endif
-constexpr int kPcR = NARDE_PC_R;                       // plies per barrier block
+//
+// Shape measured on sustained 1,000-ply rollouts:
+// one consumer wave per rule wave (two or three timed the same), four rule
+// waves per workgroup (two or one: 0.173 / 0.179 against 0.132 ms per 100
+// plies -- the dispatcher then no longer pairs a rule wave with a consumer
+// wave on every SIMD), 4-ply blocks (3 / 5 / 6: 2-8 % slower), one
+// workgroup barrier per block (a pairwise hand-over through LDS counters
+// was bit-exact but 6 % slower), no wave priorities, no unrolled plies.
+constexpr int kPcGroups = 4;                    // rule (producer) waves per workgroup
+constexpr int kPcEnvs = 64 * kPcGroups;         // envs per workgroup
+constexpr int kPcThreads = 2 * kPcEnvs;         // producers + one consumer wave each
+constexpr int kPcR = 4;                         // plies per full barrier block
+constexpr int kPcSlots = 2;                     // ring slots (block b uses slot b & 1)
 
-// Ring slots and the synchronisation of the two roles:
-//   NARDE_PC_FLAGS 0: one workgroup barrier per block, 2 slots;
-//   NARDE_PC_FLAGS 1: each rule wave and its consumer wave (they share
-//     only their own 64 env columns) hand blocks over through three LDS
-//     counters -- drawn, produced, emitted -- with NARDE_PC_SLOTS slots, so
-//     neither role waits for the other pairs.  Bit-exact, but slower:
-//     sustained 1,000-ply rollouts 0.139 (3 slots) / 0.139-0.143 (2) against
-//     0.1315 ms per 100 plies with the barrier on the same box -- the
-//     workgroup-wide lockstep keeps the CU's output stream better formed.
-//     Kept as an A/B knob (default 0).
-#ifndef NARDE_PC_FLAGS
-#define NARDE_PC_FLAGS 0
-#endif
-#ifndef NARDE_PC_SLOTS
-#define NARDE_PC_SLOTS (NARDE_PC_FLAGS ? 3 : 2)
-#endif
-constexpr int kPcSlots = NARDE_PC_SLOTS;
-static_assert(!NARDE_PC_FLAGS || kPcSets == 1, "flag hand-over needs one consumer wave per rule wave");
-static_assert(NARDE_PC_FLAGS || kPcSlots == 2, "barrier hand-over uses two slots");
+// Barrier blocks of 1, 2, then kPcR plies: the output stream (the
+// consumers' stores of block b - 1 while the rule waves play block b) only
+// starts after the first block, and the kernel is store-bound, so a short
+// first block shortens the stretch with no stores -- worth ~3 us of a 20-ply
+// launch (~35 us), nothing at 1,000 plies.
+__device__ __forceinline__ int pc_nblocks(int plies) {
+  return plies <= 1 ? 1 : (plies <= 3 ? 2 : 2 + (plies - 3 + kPcR - 1) / kPcR);
+}
+__device__ __forceinline__ void pc_block(int b, int plies, int& p0, int& np) {
+  p0 = b == 0 ? 0 : (b == 1 ? 1 : 3 + (b - 2) * kPcR);
+  const int sz = b == 0 ? 1 : (b == 1 ? 2 : kPcR);
+  np = max(0, min(sz, plies - p0));
+}
 
 struct PcLds {
   uint2 draw[kPcSlots][kPcR][kPcEnvs];        // the ply's (wa, wb) per env and ply
@@ -326,11 +286,11 @@ __device__ __forceinline__ void pc_put(PcLds& L, int slot, int k, int le, const 
 
 // consumer: outputs of plies p0 .. p0+np-1 for the 64 envs of consumer wave cw
 __device__ __forceinline__ void pc_emit(const PcLds& L, int slot, int np, int p0, int n, int wg_env0,
-                                        int cw, int lane, const Outs& out, int k0, int kstep) {
+                                        int cw, int lane, const Outs& out) {
   const int e0 = cw * 64;          // first env of this wave, workgroup-local
   const int g0 = wg_env0 + e0;     // ... global (handle) index
   const bool mine = g0 + lane < n;
-  for (int k = k0; k < np; k += kstep) {
+  for (int k = 0; k < np; ++k) {
     const size_t row0 = (size_t)(p0 + k) * n + g0;
     if (out.obs) {
       // the wave's 64 obs rows are 384 contiguous int4 quads: lane takes
@@ -349,9 +309,6 @@ __device__ __forceinline__ void pc_emit(const PcLds& L, int slot, int np, int p0
         const uint32_t own = n0w[wi];
         const uint32_t opp = wi == 0 ? n0w[3] : n1w[wi - 1];
         int4 v;
-#if NARDE_DIAG_ABLATE & 8
-        st_out(dst + j, make_int4(own, opp, 0, 0)); continue;
-#endif
         v.x = (int)((own >> sh) & 15u) - (int)((opp >> sh) & 15u);
         v.y = (int)((own >> (sh + 4)) & 15u) - (int)((opp >> (sh + 4)) & 15u);
         v.z = (int)((own >> (sh + 8)) & 15u) - (int)((opp >> (sh + 8)) & 15u);
@@ -359,11 +316,7 @@ __device__ __forceinline__ void pc_emit(const PcLds& L, int slot, int np, int p0
         st_out(dst + j, v);
       }
     }
-#if NARDE_DIAG_ABLATE & 512
-    if (false) {  // DIAGNOSTIC timing only: obs rows only
-#else
     if (mine) {
-#endif
       const uint2 lg = L.legal[slot][k][e0 + lane];
       const uint2 c = L.cf[slot][k][e0 + lane];
       const size_t ix = row0 + lane;
@@ -376,55 +329,18 @@ __device__ __forceinline__ void pc_emit(const PcLds& L, int slot, int np, int p0
   }
 }
 
-// DIAGNOSTIC (-DNARDE_DIAG_CLOCK=1 builds only): per workgroup, wave 0's
-// (s_memtime, s_memrealtime) at entry and exit of the last k_rollout_pc
-// launch, for the in-kernel clock (MI355X_MICROARCH.md, DVFS give-back
-// item 6).  Read by narde_diag_clock; no output depends on it.
-#if NARDE_DIAG_CLOCK
-__device__ unsigned long long g_diag_clock[4096][4];
-#endif
-
-// flag hand-over (NARDE_PC_FLAGS): wait until *f >= target (wave-uniform
-// spin with s_sleep; bounded, so a logic error can never hang the device --
-// it would show as wrong results in the parity tests instead)
-__device__ __forceinline__ void pc_wait(volatile uint32_t* f, int target) {
-  if (target <= 0) return;
-  for (int guard = 0; guard < (1 << 21); ++guard) {
-    if (__builtin_amdgcn_readfirstlane((int)*f) >= target) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // no LDS access hoisted above the wait
-}
-// publish *f = v once this wave's LDS reads and writes have retired
-__device__ __forceinline__ void pc_signal(volatile uint32_t* f, int v) {
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only: stores to HBM stay in flight
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  *f = (uint32_t)v;
-}
-
 template <bool kOut>
 __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng g, int plies,
                                                            int max_steps, Outs out) {
   __shared__ PcLds L;
-#if NARDE_DIAG_CLOCK
-  const unsigned long long clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
-#endif
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const bool producer = wave < kPcGroups;
-#if NARDE_PC_PRIO == 1
-  if (!producer) __builtin_amdgcn_s_setprio(1);
-#elif NARDE_PC_PRIO == 2
-  if (producer) __builtin_amdgcn_s_setprio(1);
-#endif
-  const int le = (wave % kPcGroups) * 64 + lane;    // workgroup-local env
-  // consumer set: with kPcSets > 1 the consumer waves of one env group split
-  // the plies of each block (set c takes plies k = c, c + kPcSets, ...)
-  const int cset = producer ? 0 : (wave - kPcGroups) / kPcGroups;
+  const int cw = wave % kPcGroups;                  // the env group of this wave
+  const int le = cw * 64 + lane;                    // workgroup-local env
   const int wg_env0 = blockIdx.x * kPcEnvs;
   const int i = wg_env0 + le;
   const bool valid = i < n;
-  const int nb = (plies + kPcR - 1) / kPcR;
+  const int nb = pc_nblocks(plies);
 
   Side s;
   int4 st = make_int4(0, 0, 0, 0);
@@ -438,16 +354,12 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
   // {t >> 1, env, 0, 0}) per ply pair, its halves to plies 2j and 2j + 1
   // (narde_rules.h ply_words)
   auto draw_block = [&](int b) {
-    const int p0 = b * kPcR;
-    const int np = min(kPcR, plies - p0);
+    int p0, np;
+    pc_block(b, plies, p0, np);
     uint32_t R[4];
-    for (int k = cset; k < np; k += kPcSets) {
+    for (int k = 0; k < np; ++k) {
       const uint32_t t = t0 + (uint32_t)(p0 + k);
-#if NARDE_DIAG_ABLATE & 16
-      R[0] = t * 0x9E3779B9u ^ (uint32_t)i; R[1] = R[0] * 0x85EBCA6Bu; R[2] = R[1] ^ 0xC2B2AE35u; R[3] = R[0] + 7u;
-#else
-      if (k == cset || (t & 1u) == 0u || kPcSets > 1) ply_block(t, g.env0 + (uint32_t)i, g.k0, g.k1, R);
-#endif
+      if (k == 0 || (t & 1u) == 0u) ply_block(t, g.env0 + (uint32_t)i, g.k0, g.k1, R);
       const bool odd = (t & 1u) != 0u;
       L.draw[b % kPcSlots][k][le] = odd ? make_uint2(R[2], R[3]) : make_uint2(R[0], R[1]);
     }
@@ -459,77 +371,32 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
     ply_words(rv.x, rv.y, g.dice_mode, r);
     StepOut o;
     int term, trunc;
-#if NARDE_DIAG_ABLATE & 32
-    o.l1.L[0] = r[1] & MASK24; o.l1.L[1] = r[2] & MASK24; o.l1.d[0] = 6; o.l1.d[1] = 1; o.l1.n = 2;
-    o.code1 = (int)(r[1] >> 23); o.code2 = (int)(r[2] >> 23); o.reward = 0; o.term = 0;
-    term = 0; trunc = 0;
-    s.own.w[0] ^= r[1]; s.opp.w[1] ^= r[2]; s.t += 1u;
-#else
     env_ply(s, st, r, false, 0, 0, g.dice_mode, true, 0, 0, max_steps, true, o, term, trunc);
-#endif
     if (kOut) pc_put(L, b % kPcSlots, k, le, s, o, term, trunc);
   };
-#if NARDE_PC_FLAGS
-  __shared__ uint32_t flag_drawn[kPcGroups], flag_prod[kPcGroups], flag_emit[kPcGroups];
-  const int pr = wave % kPcGroups;  // this wave's pair
-  if (producer) flag_prod[pr] = 0u;
-  else { flag_drawn[pr] = 0u; flag_emit[pr] = 0u; }
-  __syncthreads();  // the one workgroup barrier: counters initialised
-  if (producer) {
-    for (int b = 0; b < nb; ++b) {
-      const int np = min(kPcR, plies - b * kPcR);
-      pc_wait(&flag_drawn[pr], b + 1);                     // block b's draws written
-      if (kOut) pc_wait(&flag_emit[pr], b + 1 - kPcSlots);  // the slot's last results read
-      if (valid)
-        for (int k = 0; k < np; ++k) one_ply(b, k);
-      pc_signal(&flag_prod[pr], b + 1);
-    }
-  } else {
-    for (int j = 0; j <= nb; ++j) {
-      if (j < nb) {
-        pc_wait(&flag_prod[pr], j + 1 - kPcSlots);  // the slot's last draws read
-        draw_block(j);
-        pc_signal(&flag_drawn[pr], j + 1);
-      }
-      if (kOut && j >= 1) {
-        const int p0 = (j - 1) * kPcR;
-        pc_wait(&flag_prod[pr], j);  // block j - 1's results written
-        pc_emit(L, (j - 1) % kPcSlots, min(kPcR, plies - p0), p0, n, wg_env0, pr, lane, out, 0, 1);
-        pc_signal(&flag_emit[pr], j);
-      }
-    }
-  }
-#else
   if (!producer) draw_block(0);
   __syncthreads();
   for (int b = 0; b < nb; ++b) {
-    const int p0 = b * kPcR;
-    const int np = min(kPcR, plies - p0);
+    int p0, np;
+    pc_block(b, plies, p0, np);
     if (producer) {
-      if (valid) {
-#if NARDE_PC_UNROLL
-        if (np == kPcR) {
-#pragma unroll
-          for (int k = 0; k < kPcR; ++k) one_ply(b, k);
-        } else {
-          for (int k = 0; k < np; ++k) one_ply(b, k);
-        }
-#else
+      if (valid)
         for (int k = 0; k < np; ++k) one_ply(b, k);
-#endif
-      }
     } else {
       if (b + 1 < nb) draw_block(b + 1);
-      if (kOut && b > 0)
-        pc_emit(L, (b - 1) & 1, kPcR, p0 - kPcR, n, wg_env0, wave % kPcGroups, lane, out, cset, kPcSets);
+      if (kOut && b > 0) {
+        int q0, nq;
+        pc_block(b - 1, plies, q0, nq);
+        pc_emit(L, (b - 1) % kPcSlots, nq, q0, n, wg_env0, cw, lane, out);
+      }
     }
     __syncthreads();
   }
   if (kOut && !producer && nb > 0) {
-    const int p0 = (nb - 1) * kPcR;
-    pc_emit(L, (nb - 1) & 1, plies - p0, p0, n, wg_env0, wave % kPcGroups, lane, out, cset, kPcSets);
+    int p0, np;
+    pc_block(nb - 1, plies, p0, np);
+    pc_emit(L, (nb - 1) % kPcSlots, np, p0, n, wg_env0, cw, lane, out);
   }
-#endif
   if (producer && valid) {
     uint4 ra, rb;
     side_to_record(s, ra, rb);
@@ -537,13 +404,6 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
     pl.p1[i] = rb;
     add_stats(pl.stats, i, st);
   }
-#if NARDE_DIAG_CLOCK
-  if (threadIdx.x == 0 && blockIdx.x < 4096) {
-    const unsigned long long clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
-    g_diag_clock[blockIdx.x][0] = clk0; g_diag_clock[blockIdx.x][1] = clk1;
-    g_diag_clock[blockIdx.x][2] = rt0; g_diag_clock[blockIdx.x][3] = rt1;
-  }
-#endif
 }
 
 }  // namespace

@@ -325,22 +325,12 @@ int narde_rollout(narde_env* e, int plies, int32_t* obs, int32_t* reward, uint8_
   const Outs out{obs, reward, terminated, truncated, legal_compact, actions_out, nullptr};
   const bool any = obs || reward || terminated || truncated || legal_compact || actions_out;
   const int pc_grid = (int)((e->n + kPcEnvs - 1) / kPcEnvs);
-#if NARDE_ROLLOUT_PC
   if (any)
     k_rollout_pc<true><<<pc_grid, kPcThreads, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), plies,
                                                                       e->max_steps, out);
   else
     k_rollout_pc<false><<<pc_grid, kPcThreads, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e),
                                                                        plies, e->max_steps, out);
-#else
-  (void)pc_grid;
-  if (any)
-    k_rollout<true, false><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e),
-                                                                          plies, e->max_steps, out);
-  else
-    k_rollout<false, false><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e),
-                                                                           plies, e->max_steps, out);
-#endif
   return check_launch("k_rollout");
 }
 
@@ -648,14 +638,3 @@ int narde_host_violates_block_rule(narde_env* e, int64_t n, const int8_t* boards
 }
 
 }  // extern "C"
-
-#if NARDE_DIAG_CLOCK
-// DIAGNOSTIC builds only (not in include/narde.h): copy the clock stamps of
-// the last k_rollout_pc launch, int64[4096][4] = {memtime0, memtime1,
-// realtime0, realtime1} per workgroup.
-extern "C" int narde_diag_clock(unsigned long long* host_out) {
-  HIP_TRY(hipDeviceSynchronize());
-  HIP_TRY(hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_diag_clock), sizeof(g_diag_clock)));
-  return NARDE_OK;
-}
-#endif

@@ -193,8 +193,10 @@ def test_fused_transition_matches_torch_restatement(shaping, pos):
     from gym_narde.vector import VecNardeEnv
 
     n = 4096
-    env = VecNardeEnv(n, device="cuda:0", seed=23, max_episode_steps=261)
-    env.selfplay(260)
+    # the step after 119 plies: random games end after 104-131 plies, so
+    # some end in this step and the TimeLimit (120) cuts others
+    env = VecNardeEnv(n, device="cuda:0", seed=23, max_episode_steps=120)
+    env.selfplay(119)
     drv = BatchedDQNDriver(env, capacity=3 * n, train_batch=1024, shaping=shaping)
     drv.resync()
     g = torch.Generator(device="cuda:0").manual_seed(4)
