@@ -74,6 +74,7 @@ def test_invalid_position_rejected_before_any_gpu_call():
 
 
 def test_golden_fixtures_are_plain_data():
-    for name in ("legal.npz", "steps.npz", "episodes.npz", "resets.npz", "block.npz", "apply.npz"):
+    for name in ("legal.npz", "steps.npz", "episodes.npz", "resets.npz", "block.npz", "apply.npz",
+                 "full4.npz", "callers.npz", "trainer.npz"):
         d = golden(name)
         assert all(isinstance(v, np.ndarray) and v.dtype != object for v in d.values())

@@ -278,3 +278,22 @@ def test_hostcheck_legal_random_prime_boards(hostcheck):
     normal = ((ref_moves[one, :, 1] != 24) & (np.arange(64)[None, :] < ref_cnt[one, None])).sum(1)
     assert (normal <= cand).all()
     assert int((normal < cand).sum()) > 200
+
+
+def test_oracle_replays_trainer_fixture_steps():
+    """The oracle's NardeEnv.step on every step the reference trainer loop
+    took (tests/golden/trainer.npz: pre-step state, the env's own roll, the
+    trainer's action): observation, reward and end equal the reference's;
+    and where the trainer's own roll had no move, its block-rule probes on
+    mutated boards (train_deepq_pytorch.py:1066-1076) equal the oracle's
+    _violates_block_rule."""
+    d = golden("trainer.npz")
+    r = O.step(d["pre_board"], d["pre_off"], d["pre_ft"], d["player"], d["env_dice"], d["action"],
+               with_lists=False)
+    assert np.array_equal(r["obs"], d["obs"])
+    assert np.array_equal(r["reward"].astype(np.int64), d["reward"].astype(np.int64))
+    assert np.array_equal(r["terminated"], d["done"] & ~d["truncated"].astype(bool))
+    # shaping as the reference computes it, from the oracle's post-step state
+    # (float64, train_deepq_pytorch.py:892-912)
+    assert (d["shaped"] >= d["reward"]).all()
+    assert len(d["blocks"]) == int(d["blocks_len"].sum()) > 0
