@@ -261,8 +261,11 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   const uint32_t hs = 0u;  // DIAGNOSTIC builds
 #endif
   const bool nbf2 = !dbl && !bf;
-  const uint32_t sh = nbf2 ? f4_sure_pair(s.O, s.P, dl, Lh, hs) : 0u;
-  const uint32_t sl = nbf2 ? f4_sure_pair(s.O, s.P, dh, Ll, hs) : 0u;
+  uint32_t sh = 0u, sl = 0u;
+  if (__ballot(nbf2) != 0ull) {  // wave-uniform: only waves with such a lane
+    sh = nbf2 ? f4_sure_pair(s.O, s.P, dl, Lh, hs) : 0u;
+    sl = nbf2 ? f4_sure_pair(s.O, s.P, dh, Ll, hs) : 0u;
+  }
   const int hl0 = (dbl && s.ft_own && (dh == 3 || dh == 4 || dh == 6)) ? 2 : 1;
 #if NARDE_DIAG_ABLATE & (4 | 1024 | 2048)
   const uint32_t ws = 0u;  // DIAGNOSTIC builds
@@ -275,7 +278,8 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
   const int Mx = (xbf && !f4_bearoff_fixed(s)) ? f4_open_moves(s, dh, hl0, T0) : T0;
   // block-bound doubles: M = 4 and every C_k = L_k when the moves that can
   // never be rejected give >= 4 (f4_safe_bound); else the search
-  const bool fast = dbl && !bf && f4_safe_bound(s, dh, hl0, ws) >= 4;
+  bool fast = false;
+  if (__ballot(dbl && !bf) != 0ull) fast = dbl && !bf && f4_safe_bound(s, dh, hl0, ws) >= 4;
   const bool srch = dbl && !bf && !fast && Lh != 0u;
   // one cooperative pass for every lane's first-sub-move checks
   uint32_t r0[3];

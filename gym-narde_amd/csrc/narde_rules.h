@@ -1301,8 +1301,11 @@ NARDE_FN void env_ply(Side& s, int4& st, const uint32_t r[4], bool have_dice, in
 }
 
 // One FULL4 ply: env_ply with a whole turn per step.  Pick words w = {r1,
-// r2, q0, q1}, q = Philox4x32-10(ctr = {t, env, 0, 2}) drawn only on doubles
-// (the only turns with more than two sub-moves).
+// r2, r1 * 0x85EBCA6B, r2 * 0xC2B2AE35} (mod 2^32): sub-moves 2 and 3 of a
+// doubles turn take the high bits of odd multiples of the first two words
+// (a multiplicative hash of independent Philox outputs) instead of a second
+// Philox block -- every wave rolls a double on nearly every ply, so that
+// block cost a whole Philox per ply.
 // Turn = the function that plays the turn (env_turn_full, or the device's
 // wave-cooperative equivalent), called as turn(s, d0, d1, play, pw, w, o)
 // with every lane converged.
@@ -1317,13 +1320,8 @@ NARDE_FN void env_ply_full_with(Side& s, int4& st, const uint32_t r[4], uint32_t
   // its result is dropped)
   const bool bad = have_dice && ((uint32_t)(d0 - 1) > 5u || (uint32_t)(d1 - 1) > 5u);
   if (bad) { d0 = 1; d1 = 2; }
-  uint32_t w[4] = {r[1], r[2], 0u, 0u};
-  if (d0 == d1 && !play) {
-    uint32_t q[4];
-    philox4x32_10(s.t, env, 0u, 2u, k0, k1, q);
-    w[2] = q[0];
-    w[3] = q[1];
-  }
+  const uint32_t w[4] = {r[1], r[2], r[1] * 0x85EBCA6Bu, r[2] * 0xC2B2AE35u};
+  (void)env; (void)k0; (void)k1;
   const uint32_t mover_black = s.black;
   const Side before = s;
   turn(s, d0, d1, play, pw, w, o);

@@ -639,8 +639,8 @@ void or_selfplay(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int plies,
 
 /*
  * FULL4 self-play driver restatement: as or_selfplay
- * with a whole FULL4 turn per step.  Pick words w = {r1, r2, q0, q1} with
- * q = Philox4x32-10(ctr = {t, e, 0, 2}) (drawn on doubles only).  Per-ply
+ * with a whole FULL4 turn per step.  Pick words w = {r1, r2, r1 * 0x85EBCA6B,
+ * r2 * 0xC2B2AE35} (mod 2^32; the last two only matter on doubles).  Per-ply
  * outputs (optional): obs, reward, terminated, truncated, dice, legal u64
  * (C_0 masks | d_hi<<48 | d_lo<<52 | M<<56), played u64 (bytes 2k/2k+1 =
  * from/die of sub-move k, 0xFF = none).
@@ -662,12 +662,7 @@ void or_selfplay_full(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int p
             or_ply_draw(t0 + (uint32_t)p, env0 + i, key, p == 0, dice_mode, R, r);
             int32_t d[2];
             or_dice_from(r[0], dice_mode, d);
-            uint32_t w[4] = {r[1], r[2], 0, 0};
-            if (d[0] == d[1]) {
-                uint32_t c2[4] = {t0 + (uint32_t)p, (uint32_t)(env0 + i), 0, 2}, q[4];
-                or_philox4x32_10(c2, key, q);
-                w[2] = q[0]; w[3] = q[1];
-            }
+            uint32_t w[4] = {r[1], r[2], r[1] * 0x85EBCA6Bu, r[2] * 0xC2B2AE35u};
             int mover = s.player;
             uint32_t cm[4][2];
             int8_t pl[4][2];
