@@ -3,16 +3,6 @@
 // not a standalone header.
 #pragma once
 
-// ---- diagnostic knob (-D...; 0 is the product build) ----------------------
-// DIAGNOSTIC ablations of the FULL4 turn (timing only; results are wrong):
-// 1 no first-sub-move pass, 2 no later doubles passes, 4 all turns treated
-// as block-free, 128 pass tasks skip the doubles search, 256 skip the pair
-// check, 1024 two-dice turns treated as block-free, 2048 doubles turns
-// treated as block-free (tools/diag builds)
-#ifndef NARDE_DIAG_ABLATE
-#define NARDE_DIAG_ABLATE 0
-#endif
-
 namespace {
 
 constexpr int kBlock = 256;

@@ -131,8 +131,8 @@ __device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t i,
 // the last env pass valid = false and a dummy state)
 __device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t i, bool valid,
                                     const int8_t* play, const uint8_t* dice, int max_steps,
-                                    bool autoreset, TurnOut& o, int& term, int& trunc, CoopLds& W,
-                                    uint32_t R[4], bool first) {
+                                    bool autoreset, TurnOut& o, int& term, int& trunc, uint32_t R[4],
+                                    bool first) {
   uint32_t r[4];
   ply_draw_cached(g, s.t, i, R, first, r);
   int d0 = 1, d1 = 2;
@@ -143,7 +143,7 @@ __device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t i,
   env_ply_full_with(s, st, r, g.env0 + i, g.k0, g.k1, dice != nullptr, d0, d1, g.dice_mode,
                     play != nullptr, pw, max_steps, autoreset, o, term, trunc,
                     [&](Side& s2, int a, int b, bool pl, uint64_t pw2, const uint32_t* w2, TurnOut& o2) {
-                      coop_turn_full(s2, a, b, pl, pw2, w2, o2, W, lane);
+                      coop_turn_full(s2, a, b, pl, pw2, w2, o2, lane);
                     });
 }
 
@@ -160,7 +160,6 @@ __device__ __forceinline__ void add_stats(int4* __restrict__ stats, int i, const
 template <bool kFull>
 __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
   OBS_LDS_DECL
-  COOP_LDS_DECL
   const int i = blockIdx.x * kBlock + threadIdx.x;
   const bool valid = i < a.n;
   if (!kFull && !valid) return;  // FULL4 lanes stay: its turn is wave-cooperative
@@ -170,8 +169,8 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
   int term, trunc;
   uint32_t R[4];
   if constexpr (kFull)
-    ply(s, st, a.g, (uint32_t)i, valid, a.play, a.dice, a.max_steps, a.autoreset != 0, o, term, trunc,
-        wave_coop, R, true);
+    ply(s, st, a.g, (uint32_t)i, valid, a.play, a.dice, a.max_steps, a.autoreset != 0, o, term, trunc, R,
+        true);
   else
     ply(s, st, a.g, (uint32_t)i, a.actions, a.dice, a.max_steps, a.autoreset != 0, o, term, trunc, R, true);
   if (!valid) return;
@@ -183,39 +182,241 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
   store_outs(a.out, (size_t)i, s, o, term, trunc, wave_lds, i - (int)(threadIdx.x & 63) + 64 <= a.n);
 }
 
-// `plies` plies of random-legal self-play with auto-reset in one launch; the
-// record stays in VGPRs, each ply's outputs (if requested) are streamed to
-// [ply][n] rollout buffers.  kOut = false: statistics only (a separate
-// instantiation, so profiles tell the two apart).
-template <bool kOut, bool kFull>
-__global__ void __launch_bounds__(kBlock, 1) k_rollout(Planes pl, int n, Rng g, int plies, int max_steps,
-                                                       Outs out) {
-  OBS_LDS_DECL
-  COOP_LDS_DECL
-  const int i = blockIdx.x * kBlock + threadIdx.x;
+// ---------------------------------------------------------------------------
+// k_rollout_full: the FULL4 rollout (`plies` whole turns of random-legal
+// self-play per env, auto-reset) as rule waves and helper waves.
+//
+// A FULL4 turn is cheap when it is block-free (turn_block_set == 0: no block
+// filter can bite anywhere in the turn) -- ~99 % of turns -- and costly when
+// it is not: block filters, sure-move tests and the cooperative searches of
+// coop_turn_full, ~3x the instructions of a free turn.  Run in one wave,
+// that general code is paid by every wave holding such a lane: ~37 % of
+// wave-plies for ~0.7 % of lanes (the one-wave kernel spent 0.409 ms per 100
+// plies against 0.289 with every turn forced free).  And one wave per SIMD
+// (B = 65,536 envs = 1,024 waves) issues only every other VALU slot of its
+// SIMD.  So each workgroup holds 256 envs on 4 rule waves and 4 helper
+// waves, one of each per SIMD:
+//   * a rule wave plays the block-free turns of its 64 envs (turn_free: no
+//     cooperative pass, no block filter) and stores their outputs.  A lane
+//     whose turn is block-bound parks its env in its LDS mailbox and posts it
+//     to the helper; the lane sits out until the env comes back, then goes
+//     on from its own ply.  So lanes drift apart; a lane more than
+//     kFxDrift - 1 plies ahead of the wave's slowest lane waits;
+//   * the helper wave sleeps until a park wakes it (s_wakeup), then plays
+//     the posted turns with the general turn, block-free code compiled out
+//     (helper lane l serves rule lane l's mailbox; the wave is converged, as
+//     coop_turn_full needs), stores their outputs and hands the envs back --
+//     in the issue slots its rule wave leaves free.
+// (The helper plays what is posted at once: waiting for 2 or 3 parked envs
+// per pass -- its pass costs about the same for one env as for several --
+// was slower, 0.490 / 0.542 against 0.444 ms per 100 plies at that stage:
+// the parked lanes' latency, not the helper's issue, bounds the wave.)
+// Drift bound, measured (sustained 1,000-ply launches, one box): every ply
+// waiting for the parked envs 0.513 ms per 100 plies (the general turn's
+// latency stalls the wave); 2 / 4 / 8 / 12 / 16 / unbounded: 0.412 / 0.395 /
+// 0.374 / 0.372 / 0.409 / 0.465 -- past ~12 plies the lanes' rows scatter
+// over more lines than the caches merge.  Staging the rows in an LDS ring
+// and storing whole rows (as k_rollout_pc does) kept the stores coalesced
+// at any drift but cost ~120 VALU + 20 LDS instructions per ply more than
+// storing from registers: 0.404.
+// The two waves of a pair meet only through per-lane LDS words: rule lane l
+// counts its parks and stores the count to post[l] after filling its
+// mailbox; helper lane l plays the turn when post[l] moves past the count it
+// has answered, and stores that count to back[l] after writing the env back;
+// the rule lane takes the env back when back[l] reaches its count.
+// `fin`: the rule wave has finished.  Every
+// branch around a cross-lane operation is wave-uniform (a ballot or a
+// readfirstlane): a handshake run by one lane inside these loops lets the
+// compiler split the loop per lane, which breaks the cooperative turn.  No
+// workgroup barrier after the start.
+// Every env plays exactly the plies it would in k_step<true> (same draws,
+// same turn), so the outputs equal `plies` launches of narde_step_full.
+constexpr int kFxGroups = 4;                 // rule waves per workgroup (one per SIMD)
+constexpr int kFxEnvs = 64 * kFxGroups;      // envs per workgroup
+constexpr int kFxThreads = 2 * kFxEnvs;      // + one helper wave per rule wave
+constexpr int kFxDrift = 10;                 // lanes stay within kFxDrift plies of the slowest
+
+struct FxLds {  // the mailboxes of one rule/helper pair
+  uint4 m0[64], m1[64], m2[64];  // the parked env's side (mover's view): mail_put
+  uint4 r[64];                   // its ply words (rule -> helper)
+  uint32_t ply[64];              // the rollout ply of the parked turn (its output row)
+  uint32_t bs[64];               // its turn_block_set (rule -> helper)
+  uint32_t ret[64];              // statistics of the turn (helper -> rule): episodes | white << 4 | black << 8
+  uint32_t post[64], back[64];   // park counts: posted by the rule lane, answered by the helper lane
+  uint32_t fin;                  // the rule wave has finished
+};
+
+__device__ __forceinline__ void mail_put(FxLds& M, int l, const Side& s) {
+  const uint32_t misc = s.off_own | (s.off_opp << 4) | (s.ft_own << 8) | (s.ft_opp << 9) | (s.black << 10) |
+                        (s.elapsed << 16);
+  M.m0[l] = make_uint4(s.own.w[0], s.own.w[1], s.own.w[2], s.opp.w[0]);
+  M.m1[l] = make_uint4(s.opp.w[1], s.opp.w[2], misc, s.t);
+  M.m2[l] = make_uint4(s.O, s.P, s.S1o, s.S1p);
+}
+
+__device__ __forceinline__ Side mail_get(const FxLds& M, int l) {
+  const uint4 a = M.m0[l], b = M.m1[l], c = M.m2[l];
+  Side s;
+  s.own.w[0] = a.x; s.own.w[1] = a.y; s.own.w[2] = a.z;
+  s.opp.w[0] = a.w; s.opp.w[1] = b.x; s.opp.w[2] = b.y;
+  s.off_own = b.z & 15u; s.off_opp = (b.z >> 4) & 15u;
+  s.ft_own = (b.z >> 8) & 1u; s.ft_opp = (b.z >> 9) & 1u;
+  s.black = (b.z >> 10) & 1u; s.elapsed = b.z >> 16;
+  s.t = b.w;
+  s.O = c.x; s.P = c.y; s.S1o = c.z; s.S1p = c.w;
+  return s;
+}
+
+// LDS hand-over words.  The data a word publishes is written by the same
+// lane with plain LDS stores just before it (and LDS executes one wave's
+// operations in order): a compiler-only release fence keeps the stores
+// ahead of the word, without waiting for them.
+__device__ __forceinline__ uint32_t lds_acquire(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_publish(uint32_t* p, uint32_t v) {
+  __atomic_signal_fence(__ATOMIC_RELEASE);
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// s_wakeup: ends the s_sleep of every wave of the workgroup (no builtin)
+__device__ __forceinline__ void wake_workgroup() { asm volatile("s_wakeup" ::: "memory"); }
+
+template <bool kOut>
+__global__ void __launch_bounds__(kFxThreads) k_rollout_full(Planes pl, int n, Rng g, int plies,
+                                                             int max_steps, Outs out) {
+  __shared__ FxLds fx[kFxGroups];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int grp = wave % kFxGroups;
+  FxLds& M = fx[grp];
+  const int i = blockIdx.x * kFxEnvs + grp * 64 + lane;
   const bool valid = i < n;
-  if (!kFull && !valid) return;  // FULL4 lanes stay: its turn is wave-cooperative
-  const bool wave_full = i - (int)(threadIdx.x & 63) + 64 <= n;
-  Side s = valid ? side_from_record(pl.p0[i], pl.p1[i]) : side_start(0u);
-  int4 st = make_int4(0, 0, 0, 0);
-  uint32_t R[4];  // the Philox block of the current ply pair
-  for (int p = 0; p < plies; ++p) {
-    typename std::conditional<kFull, TurnOut, StepOut>::type o;
-    int term, trunc;
-    if constexpr (kFull)
-      ply(s, st, g, (uint32_t)i, valid, (const int8_t*)nullptr, nullptr, max_steps, true, o, term, trunc,
-          wave_coop, R, p == 0);
-    else
-      ply(s, st, g, (uint32_t)i, (const int16_t*)nullptr, nullptr, max_steps, true, o, term, trunc, R,
-          p == 0);
-    if (kOut && valid) store_outs(out, (size_t)p * n + i, s, o, term, trunc, wave_lds, wave_full);
+  if (wave < kFxGroups) {
+    M.post[lane] = 0u;
+    M.back[lane] = 0u;
+    M.fin = 0u;  // (every lane of the rule wave stores the same word)
   }
-  if (!valid) return;
-  uint4 ra, rb;
-  side_to_record(s, ra, rb);
-  pl.p0[i] = ra;
-  pl.p1[i] = rb;
-  add_stats(pl.stats, i, st);
+  __syncthreads();
+
+  if (wave < kFxGroups) {
+    // ---- rule wave: block-free turns; block-bound ones go to the helper
+    Side s = valid ? side_from_record(pl.p0[i], pl.p1[i]) : side_start(0u);
+    int4 st = make_int4(0, 0, 0, 0);
+    uint32_t R[4];       // the Philox block of the current ply pair
+    bool fresh = true;   // R not drawn yet
+    bool parked = false;
+    uint32_t seq = 0u;   // parks of this lane
+    int p = 0;           // this env's next ply of the launch
+    int lo = 0;          // the slowest lane's next ply (wave-uniform)
+    for (;;) {
+      if (__ballot(parked) != 0ull) {  // wave-uniform: take the envs handed back
+        if (parked && lds_acquire(&M.back[lane]) == seq) {
+          // the state after ply p; R still holds the Philox block of ply p's
+          // pair, which also serves ply p + 1 if that one is odd
+          s = mail_get(M, lane);
+          const uint32_t rt = M.ret[lane];
+          st.x += (int)(rt & 15u); st.y += (int)((rt >> 4) & 15u); st.z += (int)((rt >> 8) & 15u);
+          parked = false;
+          ++p;
+        }
+      }
+      while (lo < plies && __ballot(valid && p <= lo) == 0ull) ++lo;
+      const bool act = valid && !parked && p < plies && p < lo + kFxDrift;
+      if (__ballot(act) == 0ull) {
+        if (__ballot(parked) == 0ull) break;  // every ply played
+        // parked lanes hold the wave: wait for the helper
+        wake_workgroup();
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      uint32_t r[4] = {0u, 0u, 0u, 0u};
+      int dh = 1, dl = 1;
+      uint32_t bs = 0u;
+      if (act) {
+        ply_draw_cached(g, s.t, (uint32_t)i, R, fresh, r);
+        fresh = false;
+        int d0, d1;
+        dice_from(r[0], g.dice_mode, d0, d1);
+        dh = d0 > d1 ? d0 : d1;
+        dl = d0 > d1 ? d1 : d0;
+        bs = turn_block_set(s.O, s.S1o, s.P, block_lowmask(s.P), dh, dl);
+      }
+      const bool pk = act && bs != 0u;
+      if (pk) {  // block-bound: park the env with the helper
+        mail_put(M, lane, s);
+        M.r[lane] = make_uint4(r[0], r[1], r[2], r[3]);
+        M.ply[lane] = (uint32_t)p;
+        M.bs[lane] = bs;
+        lds_publish(&M.post[lane], ++seq);
+        parked = true;
+      }
+      if (__ballot(pk) != 0ull) wake_workgroup();  // the helper sleeps
+      if (act && !pk) {
+        uint32_t w[4];
+        turn_words(r, w);
+        const uint32_t mover_black = s.black;
+        TurnOut o;
+        turn_free(s, dh, dl, w, o);
+        int term, trunc;
+        ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, true, term, trunc);
+        if (kOut) store_outs(out, (size_t)p * n + i, s, o, term, trunc, nullptr, false);
+        ++p;
+      }
+    }
+    lds_publish(&M.fin, 1u);
+    if (!valid) return;
+    uint4 ra, rb;
+    side_to_record(s, ra, rb);
+    pl.p0[i] = ra;
+    pl.p1[i] = rb;
+    add_stats(pl.stats, i, st);
+  } else {
+    // ---- helper wave: the posted (block-bound) turns
+    uint32_t done = 0u;  // parks of rule lane `lane` answered
+    for (;;) {
+      const uint32_t want = lds_acquire(&M.post[lane]);
+      const bool mine = want != done;
+      if (__ballot(mine) != 0ull) {  // wave-uniform
+        Side s;
+        uint32_t r[4] = {0u, 0u, 0u, 0u};
+        int p = 0;
+        uint32_t bs = 0u;
+        if (mine) {
+          s = mail_get(M, lane);
+          const uint4 rr = M.r[lane];
+          r[0] = rr.x; r[1] = rr.y; r[2] = rr.z; r[3] = rr.w;
+          p = (int)M.ply[lane];
+          bs = M.bs[lane];
+        } else {  // an empty board: no candidate, no check, no pass task
+          s.own.w[0] = s.own.w[1] = s.own.w[2] = 0u;
+          s.opp.w[0] = s.opp.w[1] = s.opp.w[2] = 0u;
+          s.O = s.P = s.S1o = s.S1p = 0u;
+          s.off_own = s.off_opp = s.ft_own = s.ft_opp = s.black = s.elapsed = s.t = 0u;
+        }
+        int d0, d1;
+        dice_from(r[0], g.dice_mode, d0, d1);
+        uint32_t w[4];
+        turn_words(r, w);
+        const uint32_t mover_black = s.black;
+        TurnOut o;
+        coop_turn_full<true>(s, d0, d1, false, ~0ull, w, o, lane, bs);  // the whole wave: cooperative passes
+        int4 st = make_int4(0, 0, 0, 0);
+        int term, trunc;
+        ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, true, term, trunc);
+        if (mine) {
+          if (kOut) store_outs(out, (size_t)p * n + i, s, o, term, trunc, nullptr, false);
+          mail_put(M, lane, s);
+          M.ret[lane] = (uint32_t)st.x | ((uint32_t)st.y << 4) | ((uint32_t)st.z << 8);
+          done = want;
+          lds_publish(&M.back[lane], want);
+        }
+        continue;
+      }
+      if (__builtin_amdgcn_readfirstlane((int)lds_acquire(&M.fin)) != 0) break;
+      // idle: a long sleep (a poll costs ~30 instructions of its SIMD's issue,
+      // which the rule wave needs); a park's s_wakeup ends it early
+      __builtin_amdgcn_s_sleep(24);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------

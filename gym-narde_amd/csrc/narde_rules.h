@@ -1266,6 +1266,38 @@ NARDE_FN void ply_words_of(const uint32_t R[4], uint32_t t, int dice_mode, uint3
   ply_words(odd ? R[2] : R[0], odd ? R[3] : R[1], dice_mode, r);
 }
 
+// The end of every ply after its turn (narde_env.py:95-103 done, then the
+// gymnasium TimeLimit and the auto-reset): elapsed, terminated/truncated,
+// the statistics at an episode end, the next episode's opening roll from
+// r3, and t += 1.
+NARDE_FN void ply_close(Side& s, int4& st, int o_term, int o_reward, uint32_t mover_black, uint32_t r3,
+                        int max_steps, bool autoreset, int& term, int& trunc) {
+  s.elapsed += 1u;
+  term = o_term;
+  trunc = max_steps > 0 && s.elapsed >= (uint32_t)max_steps;
+  if (term | trunc) {
+    st.x += 1;
+    if (term) {
+      if (mover_black) st.z += o_reward;
+      else st.y += o_reward;
+    }
+    if (autoreset) {
+      const uint32_t t = s.t;
+      s = side_reset(r3);
+      s.t = t;
+    }
+  }
+  s.t += 1u;
+}
+
+// the four pick words of a FULL4 turn (see env_ply_full_with)
+NARDE_FN void turn_words(const uint32_t r[4], uint32_t w[4]) {
+  w[0] = r[1];
+  w[1] = r[2];
+  w[2] = r[1] * 0x85EBCA6Bu;
+  w[3] = r[2] * 0xC2B2AE35u;
+}
+
 // One ply for one env: NardeEnv.step + gymnasium TimeLimit
 // (max_episode_steps, gym_narde/__init__.py:3-7) + optional auto-reset,
 // then t += 1.
@@ -1282,22 +1314,7 @@ NARDE_FN void env_ply(Side& s, int4& st, const uint32_t r[4], bool have_dice, in
   if (bad) d0 = d1 = 1;
   const uint32_t mover_black = s.black;
   env_step(s, d0, d1, c1, c2, policy, r[1], r[2], o, autoreset, bad);
-  s.elapsed += 1u;
-  term = o.term;
-  trunc = max_steps > 0 && s.elapsed >= (uint32_t)max_steps;
-  if (term | trunc) {
-    st.x += 1;
-    if (term) {
-      if (mover_black) st.z += o.reward;
-      else st.y += o.reward;
-    }
-    if (autoreset) {
-      const uint32_t t = s.t;
-      s = side_reset(r[3]);
-      s.t = t;
-    }
-  }
-  s.t += 1u;
+  ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, autoreset, term, trunc);
 }
 
 // One FULL4 ply: env_ply with a whole turn per step.  Pick words w = {r1,
@@ -1320,7 +1337,8 @@ NARDE_FN void env_ply_full_with(Side& s, int4& st, const uint32_t r[4], uint32_t
   // its result is dropped)
   const bool bad = have_dice && ((uint32_t)(d0 - 1) > 5u || (uint32_t)(d1 - 1) > 5u);
   if (bad) { d0 = 1; d1 = 2; }
-  const uint32_t w[4] = {r[1], r[2], r[1] * 0x85EBCA6Bu, r[2] * 0xC2B2AE35u};
+  uint32_t w[4];
+  turn_words(r, w);
   (void)env; (void)k0; (void)k1;
   const uint32_t mover_black = s.black;
   const Side before = s;
@@ -1334,22 +1352,7 @@ NARDE_FN void env_ply_full_with(Side& s, int4& st, const uint32_t r[4], uint32_t
     o.reward = o.term ? (s.off_opp > 0u ? 1 : 2) : 0;
     if (!o.term) side_flip(s);
   }
-  s.elapsed += 1u;
-  term = o.term;
-  trunc = max_steps > 0 && s.elapsed >= (uint32_t)max_steps;
-  if (term | trunc) {
-    st.x += 1;
-    if (term) {
-      if (mover_black) st.z += o.reward;
-      else st.y += o.reward;
-    }
-    if (autoreset) {
-      const uint32_t t = s.t;
-      s = side_reset(r[3]);
-      s.t = t;
-    }
-  }
-  s.t += 1u;
+  ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, autoreset, term, trunc);
 }
 
 NARDE_FN void env_ply_full(Side& s, int4& st, const uint32_t r[4], uint32_t env, uint32_t k0,
