@@ -126,6 +126,15 @@ def cpu_baseline(seconds, cores, how):
     }
 
 
+def kernel_name(full4, plies):
+    """The kernel narde_rollout[_full] launches for this shape (narde.hip):
+    FULL4 takes k_rollout_full (rule + helper waves) from 48 plies per launch,
+    k_rollout_wave (one wave per 64 envs) below."""
+    if not full4:
+        return "k_rollout_pc<true>"
+    return "k_rollout_full<true>" if plies >= 48 else "k_rollout_wave<true>"
+
+
 def load_traffic(path, envs, plies):
     """HBM bytes per k_rollout launch from the committed rocprofv3 PMC
     summary (tools/pmc_summary.py), if it was measured at this shape."""
@@ -476,7 +485,7 @@ def main():
                              f"reward/terminated/truncated/legal set/actions for every env"),
                 "rules": args.rules,
                 "parity": parity_txt[args.rules],
-                "kernel": f"{'k_rollout<true, true> (FULL4)' if is_full4 else 'k_rollout_pc<true> (REF2)'}, {P} plies per launch",
+                "kernel": f"{kernel_name(is_full4, P)} ({'FULL4' if is_full4 else 'REF2'}), {P} plies per launch",
                 "envs_per_gpu": per,
                 "global_envs": world * per,
                 "parallelism": f"dp{world} (env-id shards, 1 RCCL all-gather of stats)",
@@ -484,7 +493,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_rollout<true, true>" if is_full4 else "k_rollout_pc<true>",
+                "kernel": kernel_name(is_full4, P),
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -510,7 +519,7 @@ def main():
                 "rules": other_rules,
                 "workload": f"{config_txt[other_rules]}; rules = {rules_txt[other_rules]}",
                 "parity": parity_txt[other_rules],
-                "kernel": f"{'k_rollout<true, true> (FULL4)' if other_rules == 'full4' else 'k_rollout_pc<true> (REF2)'}, {P} plies per launch, all outputs",
+                "kernel": f"{kernel_name(other_rules == 'full4', P)} ({other_rules.upper()}), {P} plies per launch, all outputs",
                 "value": round(other_rate, 1),
                 "unit": "env steps/s",
                 "kernel_ms": round(other_ms, 5),

@@ -183,6 +183,37 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// k_rollout_wave: the FULL4 rollout for short launches (plies < kFxMinPlies),
+// one wave per 64 envs, every lane's turn played wave-cooperatively
+// (coop_turn_full): `plies` whole turns of random-legal self-play with
+// auto-reset, the record in VGPRs, every ply's outputs stored straight from
+// registers.  k_rollout_full below is faster per ply but its launch lasts
+// until the most-delayed env has played its plies, which a short launch does
+// not amortise.
+template <bool kOut>
+__global__ void __launch_bounds__(kBlock, 1) k_rollout_wave(Planes pl, int n, Rng g, int plies, int max_steps,
+                                                            Outs out) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = i < n;  // lanes past n stay: the turn is wave-cooperative
+  Side s = valid ? side_from_record(pl.p0[i], pl.p1[i]) : side_start(0u);
+  int4 st = make_int4(0, 0, 0, 0);
+  uint32_t R[4];  // the Philox block of the current ply pair
+  for (int p = 0; p < plies; ++p) {
+    TurnOut o;
+    int term, trunc;
+    ply(s, st, g, (uint32_t)i, valid, (const int8_t*)nullptr, nullptr, max_steps, true, o, term, trunc, R,
+        p == 0);
+    if (kOut && valid) store_outs(out, (size_t)p * n + i, s, o, term, trunc, nullptr, false);
+  }
+  if (!valid) return;
+  uint4 ra, rb;
+  side_to_record(s, ra, rb);
+  pl.p0[i] = ra;
+  pl.p1[i] = rb;
+  add_stats(pl.stats, i, st);
+}
+
+// ---------------------------------------------------------------------------
 // k_rollout_full: the FULL4 rollout (`plies` whole turns of random-legal
 // self-play per env, auto-reset) as rule waves and helper waves.
 //
@@ -235,6 +266,10 @@ constexpr int kFxGroups = 4;                 // rule waves per workgroup (one pe
 constexpr int kFxEnvs = 64 * kFxGroups;      // envs per workgroup
 constexpr int kFxThreads = 2 * kFxEnvs;      // + one helper wave per rule wave
 constexpr int kFxDrift = 10;                 // lanes stay within kFxDrift plies of the slowest
+// launches shorter than this take k_rollout_wave (sustained, ms per 100
+// plies, k_rollout_wave / k_rollout_full: 20 plies 0.540 / 0.602, 50 plies
+// 0.477 / 0.471, 100 plies 0.447 / 0.420, 200 plies 0.429 / 0.397)
+constexpr int kFxMinPlies = 48;
 
 struct FxLds {  // the mailboxes of one rule/helper pair
   uint4 m0[64], m1[64], m2[64];  // the parked env's side (mover's view): mail_put

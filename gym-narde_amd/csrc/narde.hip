@@ -346,12 +346,20 @@ int narde_rollout_full(narde_env* e, int plies, int32_t* obs, int32_t* reward, u
   const Outs out{obs, reward, terminated, truncated, legal_first, nullptr, played};
   const bool any = obs || reward || terminated || truncated || legal_first || played;
   const int fx_grid = (int)((e->n + kFxEnvs - 1) / kFxEnvs);
-  if (any)
+  if (plies < kFxMinPlies) {  // short launches: one wave per 64 envs
+    if (any)
+      k_rollout_wave<true><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), plies,
+                                                                         e->max_steps, out);
+    else
+      k_rollout_wave<false><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), plies,
+                                                                          e->max_steps, out);
+  } else if (any) {
     k_rollout_full<true><<<fx_grid, kFxThreads, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), plies,
                                                                         e->max_steps, out);
-  else
+  } else {
     k_rollout_full<false><<<fx_grid, kFxThreads, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), plies,
                                                                          e->max_steps, out);
+  }
   return check_launch("k_rollout<full>");
 }
 

@@ -125,18 +125,21 @@ def test_full4_selfplay_trajectory_vs_oracle(dice_mode, max_steps):
 
 
 def test_full4_rollout_equals_steps():
-    """k_rollout<full> over launch boundaries == per-ply k_step<full>."""
-    n, seed = 2048, 31337
+    """narde_rollout_full over launch boundaries == per-ply k_step<full>: 1 and
+    29 plies take k_rollout_wave, 70 and 100 k_rollout_full (rule + helper
+    waves, lanes drifting up to 10 plies), ragged n (the last workgroup
+    partly empty)."""
+    n, seed = 2048 + 77, 31337
     a = vec(n, seed=seed)
     b = vec(n, seed=seed)
-    bufs = a.rollout_buffers(70)
+    bufs = a.rollout_buffers(100)
     got = {k: [] for k in bufs}
-    for plies in (1, 29, 70):
+    for plies in (1, 29, 70, 100):
         a.rollout(plies, bufs)
         for k, v in bufs.items():
             got[k].append(np_(v[:plies]).copy())
     got = {k: np.concatenate(v) for k, v in got.items()}
-    for p in range(100):
+    for p in range(200):
         obs, rew, term, trunc, info = b.step()
         assert np.array_equal(got["obs"][p], np_(obs)), p
         assert np.array_equal(got["reward"][p], np_(rew)), p
@@ -147,11 +150,13 @@ def test_full4_rollout_equals_steps():
     assert np.array_equal(np_(a.stats()), np_(b.stats()))
 
 
-def test_full4_full_batch_window_and_invariants():
-    """B = 65,536 (the bench shape): a 2,048-env window equals the oracle run
-    on those global ids; checker conservation and played == max dice
-    everywhere."""
-    n, plies, seed = 65536, 120, 7
+@pytest.mark.parametrize("plies", [120, 20])
+def test_full4_full_batch_window_and_invariants(plies):
+    """B = 65,536 (the bench shape; 120 plies: k_rollout_full, 20:
+    k_rollout_wave, the driver's launch): a 2,048-env window equals the
+    oracle run on those global ids; checker conservation and played == max
+    dice everywhere."""
+    n, seed = 65536, 7
     env = vec(n, seed=seed)
     bufs = env.rollout_buffers(plies)
     env.rollout(plies, bufs)
@@ -174,4 +179,4 @@ def test_full4_full_batch_window_and_invariants():
     nplayed = sum((((played >> np.uint64(16 * k)) & np.uint64(0xFF)) != np.uint64(0xFF)).astype(np.int64)
                   for k in range(4))
     assert np.array_equal(nplayed, M)
-    assert (M == 4).mean() > 0.1
+    assert (M == 4).mean() > 0.08
