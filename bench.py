@@ -241,15 +241,27 @@ def main():
         del ramp, rbufs
     ramp_ms = (time.perf_counter() - ramp_t0) * 1e3
 
-    # the timed region's own host path warmed up (untimed): its launcher, and
-    # its two timing events (a HIP event is created at its first record)
+    # the timed region's launches, pre-bound: K plies as launches of P (the
+    # last one shorter if P does not divide K), the two timing events recorded
+    # inside the first and the last launch's own call (narde_rollout_timed:
+    # no separate event-record calls on the host path).  Warmed up untimed,
+    # with the events (a HIP event is created at its first record).
+    K = args.steps
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for _ in range(3):
+    for _ in range(2):
         ev0.record()
-        full_launch()
         ev1.record()
+    sizes = [P] * (K // P) + ([K % P] if K % P else [])
+    calls = []
+    for j, p in enumerate(sizes):
+        evs = (ev0 if j == 0 else None, ev1 if j == len(sizes) - 1 else None)
+        calls.append(full_launch if evs == (None, None) else env.rollout_launcher(p, bufs, events=evs))
+    for _ in range(3):
+        calls[0]()
+        if len(calls) > 1:
+            calls[-1]()
     torch.cuda.synchronize()
-    ramp_n += 3
+    ramp_n += 3 if len(calls) == 1 else 6
 
     run_plies(args.warmup)
     # per-env statistics land here; the timed region gathers them only when
@@ -259,16 +271,15 @@ def main():
     barrier()
     torch.cuda.synchronize()
 
-    K = args.steps
     # HIP events on the launching stream around the launches of the timed
     # region (no per-launch event between them): kernel time per launch =
     # that span / launches, i.e. the launches' durations plus the gaps
     # between them (an upper bound on the dispatch duration rocprof shows)
     gc.disable()  # no collector pass inside a region this short
     t0 = time.perf_counter()
-    ev0.record()
-    launches = run_plies(K)
-    ev1.record()
+    for call in calls:
+        call()
+    launches = sizes
     t_sub = time.perf_counter()
     if world > 1:
         stats = D.gather_stats(env.stats(out=stats_buf))

@@ -367,6 +367,23 @@ int narde_selfplay_full(narde_env* e, int plies, void* stream) {
   return narde_rollout_full(e, plies, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, stream);
 }
 
+int narde_rollout_timed(narde_env* e, int full, int plies, int32_t* obs, int32_t* reward, uint8_t* terminated,
+                        uint8_t* truncated, uint64_t* legal, void* last, void* ev_start, void* ev_stop,
+                        void* stream) {
+  if (!e || plies < 0) return fail(NARDE_EINVAL, "bad argument");
+  DeviceGuard dg(e->device);
+  if (ev_start && hipEventRecord((hipEvent_t)ev_start, (hipStream_t)stream) != hipSuccess)
+    return fail(NARDE_EHIP, "hipEventRecord(ev_start) failed");
+  const int rc = full ? narde_rollout_full(e, plies, obs, reward, terminated, truncated, legal,
+                                           (uint64_t*)last, stream)
+                      : narde_rollout(e, plies, obs, reward, terminated, truncated, legal, (int16_t*)last,
+                                      stream);
+  if (rc) return rc;
+  if (ev_stop && hipEventRecord((hipEvent_t)ev_stop, (hipStream_t)stream) != hipSuccess)
+    return fail(NARDE_EHIP, "hipEventRecord(ev_stop) failed");
+  return NARDE_OK;
+}
+
 int narde_legal_full(narde_env* e, const uint8_t* dice, uint64_t* legal_first, void* stream) {
   if (!e || !legal_first) return fail(NARDE_EINVAL, "NULL argument");
   DeviceGuard dg(e->device);

@@ -42,6 +42,7 @@ SIGNATURES = {
     "narde_step_full": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
     "narde_rollout_full": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "narde_selfplay_full": (_i32, [_vp, _i32, _vp]),
+    "narde_rollout_timed": (_i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "narde_legal_full": (_i32, [_vp, _vp, _vp, _vp]),
     "narde_get_stats": (_i32, [_vp, _vp, _vp]),
     "narde_apply_moves": (_i32, [_vp, _vp, _vp, _vp]),

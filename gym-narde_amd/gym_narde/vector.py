@@ -299,19 +299,32 @@ class VecNardeEnv:
                          _lib.ptr(bufs["legal"]), _lib.ptr(bufs["actions"]), self._s())
         return bufs
 
-    def rollout_launcher(self, plies, bufs):
+    def rollout_launcher(self, plies, bufs, events=None):
         """rollout(plies, bufs) pre-bound: a zero-argument callable that makes
         exactly one ctypes call (one kernel launch on the stream current
         NOW), for hot loops where the per-call Python of rollout() would
-        show (the buffers must stay alive and unmoved while it is used)."""
+        show (the buffers must stay alive and unmoved while it is used).
+        events = (start, stop) torch.cuda.Event (either None): recorded on
+        that stream right before / after the launch, inside the same call
+        (narde_rollout_timed); they must have been recorded once already
+        (a torch event creates its HIP event at its first record)."""
         for v in bufs.values():
             if v is not None and v.shape[0] < plies:
                 raise ValueError("rollout buffer shorter than plies")
-        fn = self.handle.lib.narde_rollout_full if self.full else self.handle.lib.narde_rollout
-        name = "narde_rollout_full" if self.full else "narde_rollout"
-        args = (self.handle.h, int(plies), _lib.ptr(bufs["obs"]), _lib.ptr(bufs["reward"]),
-                _lib.ptr(bufs["terminated"]), _lib.ptr(bufs["truncated"]), _lib.ptr(bufs["legal"]),
-                _lib.ptr(bufs["actions"]), self._s())
+        bufargs = (_lib.ptr(bufs["obs"]), _lib.ptr(bufs["reward"]), _lib.ptr(bufs["terminated"]),
+                   _lib.ptr(bufs["truncated"]), _lib.ptr(bufs["legal"]), _lib.ptr(bufs["actions"]))
+        if events is None:
+            fn = self.handle.lib.narde_rollout_full if self.full else self.handle.lib.narde_rollout
+            name = "narde_rollout_full" if self.full else "narde_rollout"
+            args = (self.handle.h, int(plies)) + bufargs + (self._s(),)
+        else:
+            evs = []
+            for ev in events:
+                if ev is not None and not ev.cuda_event:
+                    raise ValueError("record each event once before binding it (its HIP event is created then)")
+                evs.append(ctypes.c_void_p(ev.cuda_event) if ev is not None else None)
+            fn, name = self.handle.lib.narde_rollout_timed, "narde_rollout_timed"
+            args = (self.handle.h, int(self.full), int(plies)) + bufargs + (evs[0], evs[1], self._s())
 
         def launch():
             rc = fn(*args)
@@ -319,6 +332,7 @@ class VecNardeEnv:
                 _lib.check(rc, name)
 
         launch.bufs = bufs  # keeps the buffers referenced as long as the launcher
+        launch.events = events
         return launch
 
     def stats(self, out=None):

@@ -173,6 +173,14 @@ int narde_rollout_full(narde_env *env, int plies, int32_t *obs, int32_t *reward,
                        uint8_t *terminated, uint8_t *truncated, uint64_t *legal_first,
                        uint64_t *played, void *stream);
 int narde_selfplay_full(narde_env *env, int plies, void *stream);
+/* narde_rollout (full = 0; `last` = actions i16[plies][B][2]) or
+ * narde_rollout_full (full = 1; `last` = played u64[plies][B]) with HIP
+ * events recorded on `stream` just before the launch (ev_start) and just
+ * after it (ev_stop), each optional (NULL): a timed launch is one call
+ * instead of three (bench.py's timed region). */
+int narde_rollout_timed(narde_env *env, int full, int plies, int32_t *obs, int32_t *reward,
+                        uint8_t *terminated, uint8_t *truncated, uint64_t *legal, void *last,
+                        void *ev_start, void *ev_stop, void *stream);
 /* C_0 and M for dice u8[B][2] (NULL = the next step's device dice). */
 int narde_legal_full(narde_env *env, const uint8_t *dice, uint64_t *legal_first, void *stream);
 

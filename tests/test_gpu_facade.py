@@ -149,3 +149,35 @@ def test_example_play_random_agent_runs():
     assert len(lengths) == 3 and sum(wins.values()) + sum(1 for x in lengths if x >= 1000) >= 3
     wins, lengths = mod.make_plays(games=1, seed=1, legal=False)
     assert len(lengths) == 1
+
+
+@pytest.mark.parametrize("rules", ["ref2", "full4"])
+def test_timed_rollout_launcher(rules):
+    """VecNardeEnv.rollout_launcher(events=...) -> narde_rollout_timed (the
+    bench's timed launch): the same outputs and state as plain launches, the
+    events bracket the launch on its stream; an event never recorded is
+    refused."""
+    from gym_narde.vector import VecNardeEnv
+
+    n, plies = 4096, 24
+    a = VecNardeEnv(n, device="cuda:0", seed=5, rules=rules)
+    b = VecNardeEnv(n, device="cuda:0", seed=5, rules=rules)
+    ba, bb = a.rollout_buffers(plies), b.rollout_buffers(plies)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with pytest.raises(ValueError):
+        a.rollout_launcher(plies, ba, events=(e0, e1))
+    e0.record()
+    e1.record()
+    timed = a.rollout_launcher(plies, ba, events=(e0, e1))
+    plain = b.rollout_launcher(plies, bb)
+    for _ in range(2):
+        timed()
+        plain()
+    torch.cuda.synchronize()
+    assert e0.elapsed_time(e1) > 0.0
+    for k in ba:
+        assert torch.equal(ba[k], bb[k]), k
+    assert torch.equal(a.stats(), b.stats())
+    sa, sb = a.get_state(), b.get_state()
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
