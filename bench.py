@@ -128,10 +128,11 @@ def cpu_baseline(seconds, cores, how):
 
 def kernel_name(full4, plies):
     """The kernel narde_rollout[_full] launches for this shape (narde.hip):
+    REF2 stores non-temporally up to 32 plies per launch (kPcNtMaxPlies);
     FULL4 takes k_rollout_full (rule + helper waves) from 48 plies per launch,
     k_rollout_wave (one wave per 64 envs) below."""
     if not full4:
-        return "k_rollout_pc<true>"
+        return "k_rollout_pc<true, true>" if plies <= 32 else "k_rollout_pc<true, false>"
     return "k_rollout_full<true>" if plies >= 48 else "k_rollout_wave<true>"
 
 
@@ -244,8 +245,10 @@ def main():
     # the timed region's launches, pre-bound: K plies as launches of P (the
     # last one shorter if P does not divide K), the two timing events recorded
     # inside the first and the last launch's own call (narde_rollout_timed:
-    # no separate event-record calls on the host path).  Warmed up untimed,
-    # with the events (a HIP event is created at its first record).
+    # no separate event-record calls on the host path; hipExtLaunchKernel's
+    # packet events cost ~12 us more per round trip than these markers).
+    # Warmed up untimed, with the events (a HIP event is created at its
+    # first record).
     K = args.steps
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for _ in range(2):

@@ -37,6 +37,22 @@ __device__ __forceinline__ void st_out(T* p, T v) {
   *p = v;
 }
 
+// non-temporal form (global_store ... nt) for the plies at the end of a
+// rollout launch (k_rollout_pc, kPcNtTail)
+template <bool kNt, class T>
+__device__ __forceinline__ void st_out_p(T* p, T v) {
+  if constexpr (!kNt) {
+    *p = v;
+  } else if constexpr (sizeof(T) == 16) {
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    v4i x;
+    __builtin_memcpy(&x, &v, 16);
+    __builtin_nontemporal_store(x, reinterpret_cast<v4i*>(p));
+  } else {
+    __builtin_nontemporal_store(v, p);
+  }
+}
+
 __device__ __forceinline__ int4 obs_quad(const Side& s, int q) {
   return make_int4(obs_point(s, 4 * q), obs_point(s, 4 * q + 1), obs_point(s, 4 * q + 2),
                    obs_point(s, 4 * q + 3));
@@ -520,52 +536,67 @@ __device__ __forceinline__ void pc_put(PcLds& L, int slot, int k, int le, const 
                                  (uint32_t)o.reward | ((uint32_t)term << 8) | ((uint32_t)trunc << 16));
 }
 
-// consumer: outputs of plies p0 .. p0+np-1 for the 64 envs of consumer wave cw
-__device__ __forceinline__ void pc_emit(const PcLds& L, int slot, int np, int p0, int n, int wg_env0,
-                                        int cw, int lane, const Outs& out) {
+// consumer: outputs of ply p (block slot `slot`, index k) for the 64 envs of
+// consumer wave cw
+template <bool kNt>
+__device__ __forceinline__ void pc_emit_ply(const PcLds& L, int slot, int k, int p, int n, int wg_env0, int cw,
+                                            int lane, const Outs& out) {
   const int e0 = cw * 64;          // first env of this wave, workgroup-local
   const int g0 = wg_env0 + e0;     // ... global (handle) index
-  const bool mine = g0 + lane < n;
-  for (int k = 0; k < np; ++k) {
-    const size_t row0 = (size_t)(p0 + k) * n + g0;
-    if (out.obs) {
-      // the wave's 64 obs rows are 384 contiguous int4 quads: lane takes
-      // quads lane + 64 q, so every store instruction covers 1 KiB
-      int4* dst = reinterpret_cast<int4*>(out.obs + row0 * 24);
+  const size_t row0 = (size_t)p * n + g0;
+  if (out.obs) {
+    // the wave's 64 obs rows are 384 contiguous int4 quads: lane takes
+    // quads lane + 64 q, so every store instruction covers 1 KiB
+    int4* dst = reinterpret_cast<int4*>(out.obs + row0 * 24);
 #pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        const int j = lane + 64 * q;
-        const int el = j / 6, qq = j - 6 * el;
-        if (g0 + el >= n) continue;
-        const int wi = qq >> 1, sh = (qq & 1) * 16;
-        // read only the two words this quad needs: own word wi is dword wi
-        // of nib0, opponent word wi is dword 3 of nib0 or wi - 1 of nib1
-        const uint32_t* n0w = reinterpret_cast<const uint32_t*>(&L.nib0[slot][k][e0 + el]);
-        const uint32_t* n1w = reinterpret_cast<const uint32_t*>(&L.nib1[slot][k][e0 + el]);
-        const uint32_t own = n0w[wi];
-        const uint32_t opp = wi == 0 ? n0w[3] : n1w[wi - 1];
-        int4 v;
-        v.x = (int)((own >> sh) & 15u) - (int)((opp >> sh) & 15u);
-        v.y = (int)((own >> (sh + 4)) & 15u) - (int)((opp >> (sh + 4)) & 15u);
-        v.z = (int)((own >> (sh + 8)) & 15u) - (int)((opp >> (sh + 8)) & 15u);
-        v.w = (int)((own >> (sh + 12)) & 15u) - (int)((opp >> (sh + 12)) & 15u);
-        st_out(dst + j, v);
-      }
+    for (int q = 0; q < 6; ++q) {
+      const int j = lane + 64 * q;
+      const int el = j / 6, qq = j - 6 * el;
+      if (g0 + el >= n) continue;
+      const int wi = qq >> 1, sh = (qq & 1) * 16;
+      // read only the two words this quad needs: own word wi is dword wi
+      // of nib0, opponent word wi is dword 3 of nib0 or wi - 1 of nib1
+      const uint32_t* n0w = reinterpret_cast<const uint32_t*>(&L.nib0[slot][k][e0 + el]);
+      const uint32_t* n1w = reinterpret_cast<const uint32_t*>(&L.nib1[slot][k][e0 + el]);
+      const uint32_t own = n0w[wi];
+      const uint32_t opp = wi == 0 ? n0w[3] : n1w[wi - 1];
+      int4 v;
+      v.x = (int)((own >> sh) & 15u) - (int)((opp >> sh) & 15u);
+      v.y = (int)((own >> (sh + 4)) & 15u) - (int)((opp >> (sh + 4)) & 15u);
+      v.z = (int)((own >> (sh + 8)) & 15u) - (int)((opp >> (sh + 8)) & 15u);
+      v.w = (int)((own >> (sh + 12)) & 15u) - (int)((opp >> (sh + 12)) & 15u);
+      st_out_p<kNt>(dst + j, v);
     }
-    if (mine) {
-      const uint2 lg = L.legal[slot][k][e0 + lane];
-      const uint2 c = L.cf[slot][k][e0 + lane];
-      const size_t ix = row0 + lane;
-      if (out.reward) st_out(out.reward + ix, (int32_t)(c.y & 0xFFu));
-      if (out.term) st_out(out.term + ix, (uint8_t)((c.y >> 8) & 1u));
-      if (out.trunc) st_out(out.trunc + ix, (uint8_t)((c.y >> 16) & 1u));
-      if (out.legal) st_out(out.legal + ix, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
-      if (out.act_out) st_out(reinterpret_cast<uint32_t*>(out.act_out) + ix, c.x);
-    }
+  }
+  if (g0 + lane < n) {
+    const uint2 lg = L.legal[slot][k][e0 + lane];
+    const uint2 c = L.cf[slot][k][e0 + lane];
+    const size_t ix = row0 + lane;
+    if (out.reward) st_out_p<kNt>(out.reward + ix, (int32_t)(c.y & 0xFFu));
+    if (out.term) st_out_p<kNt>(out.term + ix, (uint8_t)((c.y >> 8) & 1u));
+    if (out.trunc) st_out_p<kNt>(out.trunc + ix, (uint8_t)((c.y >> 16) & 1u));
+    if (out.legal) st_out_p<kNt>(out.legal + ix, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
+    if (out.act_out) st_out_p<kNt>(reinterpret_cast<uint32_t*>(out.act_out) + ix, c.x);
   }
 }
 
-template <bool kOut>
+// consumer: outputs of plies p0 .. p0+np-1, stored non-temporally in short
+// launches (kNt: plies <= kPcNtMaxPlies, chosen at launch).  Plain stores
+// leave their lines dirty in the XCD L2s, and the write-back of what is still
+// dirty when the kernel ends sits on a short launch's critical path: one
+// 20-ply launch after an idle GPU takes 36.4 us with non-temporal stores
+// against 38.7 us with plain ones, while sustained 1,000-ply launches are
+// faster with plain stores (0.127 against 0.135 ms per 100 plies).  Only the
+// last 2-8 plies non-temporal gained nothing at 20 plies and cost 2 % at
+// 1,000 (tools/diag/gpu_ab_nt.sh, one box).
+constexpr int kPcNtMaxPlies = 32;
+template <bool kNt>
+__device__ __forceinline__ void pc_emit(const PcLds& L, int slot, int np, int p0, int n, int wg_env0, int cw,
+                                        int lane, const Outs& out) {
+  for (int k = 0; k < np; ++k) pc_emit_ply<kNt>(L, slot, k, p0 + k, n, wg_env0, cw, lane, out);
+}
+
+template <bool kOut, bool kNt>
 __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng g, int plies,
                                                            int max_steps, Outs out) {
   __shared__ PcLds L;
@@ -623,7 +654,7 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
       if (kOut && b > 0) {
         int q0, nq;
         pc_block(b - 1, plies, q0, nq);
-        pc_emit(L, (b - 1) % kPcSlots, nq, q0, n, wg_env0, cw, lane, out);
+        pc_emit<kNt>(L, (b - 1) % kPcSlots, nq, q0, n, wg_env0, cw, lane, out);
       }
     }
     __syncthreads();
@@ -631,7 +662,7 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
   if (kOut && !producer && nb > 0) {
     int p0, np;
     pc_block(nb - 1, plies, p0, np);
-    pc_emit(L, (nb - 1) % kPcSlots, np, p0, n, wg_env0, cw, lane, out);
+    pc_emit<kNt>(L, (nb - 1) % kPcSlots, np, p0, n, wg_env0, cw, lane, out);
   }
   if (producer && valid) {
     uint4 ra, rb;

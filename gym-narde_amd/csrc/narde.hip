@@ -317,6 +317,42 @@ int narde_step_full(narde_env* e, const int8_t* play, const uint8_t* dice, int32
   return check_launch("k_step<full>");
 }
 
+// The rollout launches.  narde_rollout_timed brackets them with two
+// hipEventRecord markers: hipExtLaunchKernel's packet-level start / stop
+// events were measured too and cost ~12 us more per host round trip of one
+// launch than the markers' ~4 us (tools/diag/single_launch.py, one box).
+namespace {
+
+int launch_rollout_ref2(narde_env* e, int plies, const Outs& out, bool any, hipStream_t stream) {
+  const dim3 g((unsigned)((e->n + kPcEnvs - 1) / kPcEnvs)), b(kPcThreads);
+  if (any && plies <= kPcNtMaxPlies)
+    k_rollout_pc<true, true><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
+  else if (any)
+    k_rollout_pc<true, false><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
+  else
+    k_rollout_pc<false, false><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
+  return check_launch("k_rollout");
+}
+
+int launch_rollout_full(narde_env* e, int plies, const Outs& out, bool any, hipStream_t stream) {
+  if (plies < kFxMinPlies) {  // short launches: one wave per 64 envs
+    const dim3 g((unsigned)grid(e->n)), b(kBlock);
+    if (any)
+      k_rollout_wave<true><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
+    else
+      k_rollout_wave<false><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
+  } else {
+    const dim3 g((unsigned)((e->n + kFxEnvs - 1) / kFxEnvs)), b(kFxThreads);
+    if (any)
+      k_rollout_full<true><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
+    else
+      k_rollout_full<false><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
+  }
+  return check_launch("k_rollout<full>");
+}
+
+}  // namespace
+
 int narde_rollout(narde_env* e, int plies, int32_t* obs, int32_t* reward, uint8_t* terminated,
                   uint8_t* truncated, uint64_t* legal_compact, int16_t* actions_out, void* stream) {
   if (!e || plies < 0) return fail(NARDE_EINVAL, "bad argument");
@@ -324,14 +360,7 @@ int narde_rollout(narde_env* e, int plies, int32_t* obs, int32_t* reward, uint8_
   DeviceGuard dg(e->device);
   const Outs out{obs, reward, terminated, truncated, legal_compact, actions_out, nullptr};
   const bool any = obs || reward || terminated || truncated || legal_compact || actions_out;
-  const int pc_grid = (int)((e->n + kPcEnvs - 1) / kPcEnvs);
-  if (any)
-    k_rollout_pc<true><<<pc_grid, kPcThreads, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), plies,
-                                                                      e->max_steps, out);
-  else
-    k_rollout_pc<false><<<pc_grid, kPcThreads, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e),
-                                                                       plies, e->max_steps, out);
-  return check_launch("k_rollout");
+  return launch_rollout_ref2(e, plies, out, any, (hipStream_t)stream);
 }
 
 int narde_selfplay(narde_env* e, int plies, void* stream) {
@@ -345,22 +374,7 @@ int narde_rollout_full(narde_env* e, int plies, int32_t* obs, int32_t* reward, u
   DeviceGuard dg(e->device);
   const Outs out{obs, reward, terminated, truncated, legal_first, nullptr, played};
   const bool any = obs || reward || terminated || truncated || legal_first || played;
-  const int fx_grid = (int)((e->n + kFxEnvs - 1) / kFxEnvs);
-  if (plies < kFxMinPlies) {  // short launches: one wave per 64 envs
-    if (any)
-      k_rollout_wave<true><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), plies,
-                                                                         e->max_steps, out);
-    else
-      k_rollout_wave<false><<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), plies,
-                                                                          e->max_steps, out);
-  } else if (any) {
-    k_rollout_full<true><<<fx_grid, kFxThreads, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), plies,
-                                                                        e->max_steps, out);
-  } else {
-    k_rollout_full<false><<<fx_grid, kFxThreads, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), plies,
-                                                                         e->max_steps, out);
-  }
-  return check_launch("k_rollout<full>");
+  return launch_rollout_full(e, plies, out, any, (hipStream_t)stream);
 }
 
 int narde_selfplay_full(narde_env* e, int plies, void* stream) {
@@ -372,12 +386,17 @@ int narde_rollout_timed(narde_env* e, int full, int plies, int32_t* obs, int32_t
                         void* stream) {
   if (!e || plies < 0) return fail(NARDE_EINVAL, "bad argument");
   DeviceGuard dg(e->device);
+  const bool any = obs || reward || terminated || truncated || legal || last;
   if (ev_start && hipEventRecord((hipEvent_t)ev_start, (hipStream_t)stream) != hipSuccess)
     return fail(NARDE_EHIP, "hipEventRecord(ev_start) failed");
-  const int rc = full ? narde_rollout_full(e, plies, obs, reward, terminated, truncated, legal,
-                                           (uint64_t*)last, stream)
-                      : narde_rollout(e, plies, obs, reward, terminated, truncated, legal, (int16_t*)last,
-                                      stream);
+  int rc = NARDE_OK;
+  if (plies > 0 && full) {
+    const Outs out{obs, reward, terminated, truncated, legal, nullptr, (uint64_t*)last};
+    rc = launch_rollout_full(e, plies, out, any, (hipStream_t)stream);
+  } else if (plies > 0) {
+    const Outs out{obs, reward, terminated, truncated, legal, (int16_t*)last, nullptr};
+    rc = launch_rollout_ref2(e, plies, out, any, (hipStream_t)stream);
+  }
   if (rc) return rc;
   if (ev_stop && hipEventRecord((hipEvent_t)ev_stop, (hipStream_t)stream) != hipSuccess)
     return fail(NARDE_EHIP, "hipEventRecord(ev_stop) failed");

@@ -177,7 +177,7 @@ int narde_selfplay_full(narde_env *env, int plies, void *stream);
  * narde_rollout_full (full = 1; `last` = played u64[plies][B]) with HIP
  * events recorded on `stream` just before the launch (ev_start) and just
  * after it (ev_stop), each optional (NULL): a timed launch is one call
- * instead of three (bench.py's timed region). */
+ * instead of three (bench.py's timed region).  plies = 0 launches nothing. */
 int narde_rollout_timed(narde_env *env, int full, int plies, int32_t *obs, int32_t *reward,
                         uint8_t *terminated, uint8_t *truncated, uint64_t *legal, void *last,
                         void *ev_start, void *ev_stop, void *stream);

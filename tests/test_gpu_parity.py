@@ -163,7 +163,7 @@ def test_rollout_vs_oracle_and_step(n):
     stepper = vec(n, seed=seed, env_id_offset=env0, max_episode_steps=150)
     ref = O.SelfPlay(n, seed=seed, env0=env0, max_steps=150)
     ref.reset(0)
-    for plies in (1, 64, 235):
+    for plies in (1, 20, 64, 235):  # <= 32 plies: the non-temporal-store kernel
         rec = ref.run(plies)
         bufs = env.rollout(plies)
         # the compact legal sets and codes, bit for bit, against the per-ply
@@ -181,7 +181,7 @@ def test_rollout_vs_oracle_and_step(n):
         cnt = (np.vectorize(lambda x: bin(int(x) & 0xFFFFFFFFFFFF).count("1"))(lg)).astype(np.int16)
         assert np.array_equal(cnt, rec["count1"])
     assert np.array_equal(np_(env.stats()), ref.stats)
-    assert env.ply == 300
+    assert env.ply == 320
 
 
 def test_step_graph_replay_vs_oracle():
@@ -237,8 +237,9 @@ def test_full_batch_subset_and_invariants():
 
 
 def test_bench_launch_window_and_invariants():
-    """The exact launch bench.py times (k_rollout_pc<true>: B = 65,536, 1,000
-    plies, every output), then a 100-ply one: a 2,048-env window of every
+    """The launches bench.py times (k_rollout_pc<true, *>: B = 65,536, 1,000
+    plies, every output), then a 100-ply one and the driver's 20-ply one
+    (non-temporal stores): a 2,048-env window of every
     output equals the oracle on those global ids; over the whole batch the
     outputs obey the rules' invariants (at most 15 checkers a side, reward
     only on a finished game (1 or 2), no truncation: no random game lasts
@@ -248,7 +249,7 @@ def test_bench_launch_window_and_invariants():
     ref = O.SelfPlay(m, seed=seed, env0=lo)
     ref.reset(0)
     sl = slice(lo, lo + m)
-    for P in (1000, 100):
+    for P in (1000, 100, 20):
         bufs = env.rollout_buffers(P)
         env.rollout(P, bufs)
         rec = ref.run(P)
@@ -267,7 +268,7 @@ def test_bench_launch_window_and_invariants():
         assert not bool(trunc.any())
         del bufs, obs, rew, term, trunc
     assert np.array_equal(np_(env.stats())[sl], ref.stats)
-    assert env.ply == 1100
+    assert env.ply == 1120
 
 
 def test_sharded_handles_equal_single():
