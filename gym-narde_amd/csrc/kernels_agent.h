@@ -141,19 +141,34 @@ __device__ __forceinline__ void trans_scalars(const TransArgs& t, int i, int64_t
   t.r_prio[nslot] = 0.0f;
 }
 
-// Each thread owns 4 consecutive floats of the flat (n, 198) arrays, so s'
-// goes out 16 B per lane (1 KiB per wave instruction; the ring row is
-// written once and read only when sampled: non-temporal) when this step's
-// s' rows (pos + n .. pos + 2n - 1) % capacity are contiguous and 16-B
-// aligned (the steady state when the capacity is a multiple of n);
-// otherwise each float goes on its own.
-__global__ void __launch_bounds__(kBlock) k_dqn_transition(TransArgs t) {
-  const uint32_t total = (uint32_t)t.n * 198u;  // n * 198 < 2^31 (checked on the host)
-  const uint32_t e0 = 4u * (blockIdx.x * kBlock + threadIdx.x);
-  if (e0 >= total) return;
+// Two kinds of block in one launch.  Blocks below obs_blocks: each thread
+// owns 4 consecutive floats of the flat (n, 198) arrays, so s' goes out 16 B
+// per lane (1 KiB per wave instruction; the ring row is written once and
+// read only when sampled: non-temporal) when this step's s' rows
+// (pos + n .. pos + 2n - 1) % capacity are contiguous and 16-B aligned (the
+// steady state when the capacity is a multiple of n); otherwise each float
+// goes on its own.  The blocks after them: one thread per env for the
+// replay row's scalars and the shaping trackers, so those narrow arrays are
+// written coalesced (a thread per env, not the one thread of each 198-float
+// row that owns its column 0: those writes were scattered over partial
+// lines).
+__global__ void __launch_bounds__(kBlock) k_dqn_transition(TransArgs t, int obs_blocks) {
   const int64_t pos = *t.pos;  // pos < capacity, capacity >= 2n: one wrap at most
   int64_t q0 = pos + t.n;
   if (q0 >= t.capacity) q0 -= t.capacity;
+  if ((int)blockIdx.x >= obs_blocks) {
+    const int i = ((int)blockIdx.x - obs_blocks) * kBlock + (int)threadIdx.x;
+    if (i >= t.n) return;
+    int64_t slot = pos + i;
+    if (slot >= t.capacity) slot -= t.capacity;
+    int64_t nslot = q0 + i;
+    if (nslot >= t.capacity) nslot -= t.capacity;
+    trans_scalars(t, i, slot, nslot, t.pl.p1[i]);
+    return;
+  }
+  const uint32_t total = (uint32_t)t.n * 198u;  // n * 198 < 2^31 (checked on the host)
+  const uint32_t e0 = 4u * (blockIdx.x * kBlock + threadIdx.x);
+  if (e0 >= total) return;
   const bool vec = (q0 * 198) % 4 == 0 && q0 + t.n <= t.capacity && e0 + 4u <= total;
   const int i0 = (int)(e0 / 198u);
   const int c0 = (int)(e0 - (uint32_t)i0 * 198u);
@@ -185,19 +200,6 @@ __global__ void __launch_bounds__(kBlock) k_dqn_transition(TransArgs t) {
       t.r_obs[qs * 198 + col] = nv[q];
       t.state[e] = nv[q];
     }
-  }
-  // column 0 of a row lies in at most one thread's 4 floats
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t e = e0 + (uint32_t)q;
-    if (e >= total) break;
-    const int i = (int)(e / 198u);
-    if (e - (uint32_t)i * 198u != 0u) continue;
-    int64_t slot = pos + i;
-    if (slot >= t.capacity) slot -= t.capacity;
-    int64_t nslot = q0 + i;
-    if (nslot >= t.capacity) nslot -= t.capacity;
-    trans_scalars(t, i, slot, nslot, i == i0 ? b0 : b1);
   }
 }
 

@@ -21,5 +21,9 @@ PY
 mkdir -p tools/diag/build
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -shared \
   -o tools/diag/build/libnarde_$tag.so "$tmp/gym-narde_amd/csrc/narde.hip" "$tmp/gym-narde_amd/csrc/dqn_learner.hip"
+if [ "${ASM:-0}" = 1 ]; then  # the device assembly too (tools/diag/build/libnarde_<tag>.s)
+  /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -S --cuda-device-only \
+    -o tools/diag/build/libnarde_$tag.s "$tmp/gym-narde_amd/csrc/narde.hip" 2>/dev/null
+fi
 rm -rf "$tmp"
 echo "built tools/diag/build/libnarde_$tag.so"
