@@ -1,11 +1,14 @@
-"""World-size-2 rehearsal of the multi-GPU path on CPU (gloo).
+"""World-size-2 and -4 rehearsals of the multi-GPU path on CPU (gloo).
 
 Each rank owns a contiguous shard of global env ids (gym_narde.distributed.
-env_shard), runs its shard -- here with the CPU oracle standing in for the
-GPU kernels, which this container lacks -- and the statistics are combined
-with the same gather_stats the GPU run uses (RCCL there, gloo here).  The
-gathered result must equal one process running all envs: device dice are
-keyed by the global env id, so sharding cannot change any env's game."""
+env_shard) and plays it with the product's own rules engine -- narde_rules.h,
+the source the HIP kernels are built from, compiled for the host
+(tests/hostcheck: hc_reset_batch + hc_selfplay, the same per-env Philox
+draws keyed by the global env id) because this container has no GPU -- and
+the statistics are combined with the same gather_stats the GPU run uses
+(RCCL there, gloo here).  The gathered result must equal the CPU oracle
+playing all envs in one process: sharding cannot change any env's game."""
+import ctypes
 import os
 import socket
 
@@ -25,14 +28,30 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, out_path):
+def _shard_selfplay(lib, first, per):
+    """The rank's shard through the host build of the device rules engine."""
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    b = np.zeros((per, 24), np.int8)
+    off = np.zeros((per, 2), np.uint8)
+    ft = np.zeros((per, 2), np.uint8)
+    pl = np.zeros(per, np.int8)
+    el = np.zeros(per, np.uint16)
+    st = np.zeros((per, 3), np.int32)
+    lib.hc_reset_batch(ctypes.c_int64(per), ctypes.c_int64(first), ctypes.c_uint64(SEED), ctypes.c_uint32(0),
+                       P(b), P(off), P(ft), P(pl), P(el))
+    lib.hc_selfplay(ctypes.c_int64(per), ctypes.c_int64(first), ctypes.c_uint64(SEED), ctypes.c_uint32(0),
+                    ctypes.c_int(PLIES), ctypes.c_int(0), ctypes.c_int(1000), P(b), P(off), P(ft), P(pl), P(el),
+                    P(st), None, None, None, None, None, None, None)
+    return st
+
+
+def _rank_main(rank, world, port, lib_path, out_path):
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path[:0] = [os.path.join(root, "gym-narde_amd"), os.path.join(root, "oracle")]
+    sys.path[:0] = [os.path.join(root, "gym-narde_amd")]
     import torch.distributed as dist
 
-    import oracle as Orc
     from gym_narde import distributed as D
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
@@ -40,10 +59,8 @@ def _rank_main(rank, world, port, out_path):
     r, w, _ = D.init_from_env(backend="gloo")
     assert (r, w) == (rank, world)
     first, per = D.env_shard(B, r, w)
-    sp = Orc.SelfPlay(per, seed=SEED, env0=first)
-    sp.reset(0)
-    sp.run(PLIES, record=False)
-    gathered = D.gather_stats(torch.from_numpy(sp.stats.copy()))
+    st = _shard_selfplay(ctypes.CDLL(lib_path), first, per)
+    gathered = D.gather_stats(torch.from_numpy(st))
     if r == 0:
         np.save(out_path, gathered.numpy())
     dist.barrier()
@@ -61,9 +78,10 @@ def test_env_shard_partition():
         env_shard(10, 0, 3)
 
 
-def test_gloo_world2_equals_single_process(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_shards_equal_single_process(tmp_path, hostcheck, world):
     out = str(tmp_path / "gathered.npy")
-    mp.spawn(_rank_main, args=(2, _free_port(), out), nprocs=2, join=True)
+    mp.spawn(_rank_main, args=(world, _free_port(), hostcheck._name, out), nprocs=world, join=True)
     gathered = np.load(out)
     sp = O.SelfPlay(B, seed=SEED, env0=0)
     sp.reset(0)
