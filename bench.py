@@ -12,8 +12,8 @@ the env record in VGPRs, each ply's outputs streamed to [P][B] rollout
 buffers (K steps = ceil(K/P) launches).  The per-ply API kernel k_step is
 measured beside it (eager and hipGraph-replayed).  N GPUs = N processes
 (torchrun), each owning a contiguous shard of global env ids (weak
-scaling); the timed region ends with the RCCL all-gather of per-env episode
-statistics.
+scaling); at N > 1 the timed region ends with the RCCL all-gather of every
+rank's episode totals.
 
 Prints ONE JSON line on rank 0 (fields: DESIGN.md section 6).
 """
@@ -267,8 +267,8 @@ def main():
     ramp_n += 3 if len(calls) == 1 else 6
 
     run_plies(args.warmup)
-    # per-env statistics land here; the timed region gathers them only when
-    # there is something to gather (N > 1: the one RCCL all-gather)
+    # per-env statistics land here; at N > 1 the timed region ends with the
+    # one RCCL all-gather of every rank's episode totals (24 B per rank)
     stats_buf = torch.empty((per, 3), dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
     barrier()
@@ -285,7 +285,7 @@ def main():
     launches = sizes
     t_sub = time.perf_counter()
     if world > 1:
-        stats = D.gather_stats(env.stats(out=stats_buf))
+        totals = D.gather_totals(env.stats(out=stats_buf))
     torch.cuda.synchronize()
     t_wait = time.perf_counter()
     barrier()
@@ -296,7 +296,7 @@ def main():
                "close": round((elapsed - (t_wait - t0)) * 1e6, 1)}
     span_ms = ev0.elapsed_time(ev1)
     if world == 1:
-        stats = env.stats(out=stats_buf)
+        totals = D.gather_totals(env.stats(out=stats_buf))
     # algorithmic bytes of every launch in the span (a last partial launch
     # included), and the mean duration of a full-length launch
     span_bytes = sum(launch_bytes(per, p, is_full4) for p in launches)
@@ -310,7 +310,7 @@ def main():
     elapsed, kern_ms = float(t[0]), float(t[1])
     total_steps = world * per * K
     value = total_steps / elapsed
-    summary = D.summarize(stats)
+    summary = D.summarize(totals)
 
     # secondary 1: per-ply API kernel k_step (eager, then hipGraph replay)
     S = args.api_steps
@@ -502,7 +502,7 @@ def main():
                 "kernel": f"{kernel_name(is_full4, P)} ({'FULL4' if is_full4 else 'REF2'}), {P} plies per launch",
                 "envs_per_gpu": per,
                 "global_envs": world * per,
-                "parallelism": f"dp{world} (env-id shards, 1 RCCL all-gather of stats)",
+                "parallelism": f"dp{world} (env-id shards, 1 RCCL all-gather of episode totals)",
                 "episodes_finished": summary["episodes"],
             },
             "roofline": {

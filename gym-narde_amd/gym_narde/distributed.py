@@ -63,6 +63,22 @@ def gather_stats(local_stats):
     return out.to(local_stats.device)
 
 
+def gather_totals(local_stats):
+    """Per-rank totals {episodes, white points, black points} of (B_local, 3)
+    statistics, all-gathered: (world, 3) int64 on every rank, rank order (the
+    local totals as (1, 3) when no process group is initialised).  One 24-B
+    RCCL all-gather per rank -- what the self-play driver reports per run --
+    instead of gather_stats' 12 B per env."""
+    tot = local_stats.to(torch.int64).sum(0, keepdim=True)
+    if not dist.is_initialized():
+        return tot
+    if dist.get_backend() == "gloo" and tot.is_cuda:  # gloo gathers host tensors
+        tot = tot.cpu()
+    out = torch.empty((dist.get_world_size(), 3), dtype=torch.int64, device=tot.device)
+    dist.all_gather_into_tensor(out, tot)
+    return out
+
+
 def summarize(stats):
     """{episodes, white_points, black_points} of a (B, 3) statistics tensor."""
     s = stats.to(torch.int64).sum(0).tolist()

@@ -61,8 +61,10 @@ def _rank_main(rank, world, port, lib_path, out_path):
     first, per = D.env_shard(B, r, w)
     st = _shard_selfplay(ctypes.CDLL(lib_path), first, per)
     gathered = D.gather_stats(torch.from_numpy(st))
+    totals = D.gather_totals(torch.from_numpy(st))  # what bench.py's timed region gathers
     if r == 0:
         np.save(out_path, gathered.numpy())
+        np.save(out_path + ".totals.npy", totals.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -88,6 +90,9 @@ def test_gloo_shards_equal_single_process(tmp_path, hostcheck, world):
     sp.run(PLIES, record=False)
     assert gathered.shape == (B, 3)
     assert np.array_equal(gathered, sp.stats)
+    totals = np.load(out + ".totals.npy")  # (world, 3): each rank's shard summed
+    per = B // world
+    assert np.array_equal(totals, sp.stats.astype(np.int64).reshape(world, per, 3).sum(1))
     from gym_narde.distributed import summarize
 
     s = summarize(torch.from_numpy(gathered))

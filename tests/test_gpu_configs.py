@@ -303,6 +303,9 @@ st = env.stats()
 g = D.gather_stats(st)  # all_gather_into_tensor over RCCL on device tensors
 torch.cuda.synchronize()
 assert g.is_cuda and g.shape == st.shape and torch.equal(g, st)
+tot = D.gather_totals(st)  # the bench's timed-region gather: per-rank totals
+torch.cuda.synchronize()
+assert tot.is_cuda and tot.shape == (1, 3) and torch.equal(tot[0], st.to(torch.int64).sum(0))
 t = torch.tensor([1.5, 2.5], dtype=torch.float64, device="cuda:0")
 dist.all_reduce(t, op=dist.ReduceOp.MAX)  # the bench's max-over-ranks timing
 dist.barrier()
