@@ -97,3 +97,12 @@ def test_gloo_shards_equal_single_process(tmp_path, hostcheck, world):
 
     s = summarize(torch.from_numpy(gathered))
     assert s["episodes"] > 0 and s["white_points"] + s["black_points"] > 0
+
+
+def test_gather_totals_without_process_group():
+    from gym_narde.distributed import gather_totals, summarize
+
+    st = torch.tensor([[1, 2, 0], [3, 0, 6]], dtype=torch.int32)
+    tot = gather_totals(st)
+    assert tot.dtype == torch.int64 and tot.tolist() == [[4, 2, 6]]
+    assert summarize(tot) == {"episodes": 4, "white_points": 2, "black_points": 6}

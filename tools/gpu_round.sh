@@ -12,7 +12,7 @@ OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 echo "[gpu_round] $(date +%T) pytest -m gpu"
-timeout -k 10 420 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu.log" 2>&1 \
+timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 \
   && echo "pytest rc=0" >> "$OUT/pytest_gpu.log" \
   && echo "[gpu_round] $(date +%T) smoke" \
   && timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 \
