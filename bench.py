@@ -195,7 +195,7 @@ def main():
     import torch.distributed as dist
 
     from gym_narde import distributed as D
-    from gym_narde.vector import VecNardeEnv
+    from gym_narde.vector import TimingEvent, VecNardeEnv
 
     rank, world, local = D.init_from_env()
     torch.cuda.set_device(local)
@@ -247,13 +247,12 @@ def main():
     # inside the first and the last launch's own call (narde_rollout_timed:
     # no separate event-record calls on the host path; hipExtLaunchKernel's
     # packet events cost ~12 us more per round trip than these markers).
-    # Warmed up untimed, with the events (a HIP event is created at its
-    # first record).
+    # The events are timing-only markers (TimingEvent: HIP events with
+    # hipEventDisableSystemFence -- a default event's record writes back and
+    # invalidates the caches, which lengthens the span it measures by ~1 us
+    # at the driver's shape).  The launch path is warmed up untimed.
     K = args.steps
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for _ in range(2):
-        ev0.record()
-        ev1.record()
+    ev0, ev1 = TimingEvent(dev), TimingEvent(dev)
     sizes = [P] * (K // P) + ([K % P] if K % P else [])
     calls = []
     for j, p in enumerate(sizes):
@@ -289,12 +288,13 @@ def main():
     torch.cuda.synchronize()
     t_wait = time.perf_counter()
     barrier()
-    torch.cuda.synchronize()
+    if world > 1:  # (one process: no barrier, and the device is idle already)
+        torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     gc.enable()
     host_us = {"submit": round((t_sub - t0) * 1e6, 1), "wait": round((t_wait - t_sub) * 1e6, 1),
                "close": round((elapsed - (t_wait - t0)) * 1e6, 1)}
-    span_ms = ev0.elapsed_time(ev1)
+    span_ms = ev0.elapsed_ms(ev1)
     if world == 1:
         totals = D.gather_totals(env.stats(out=stats_buf))
     # algorithmic bytes of every launch in the span (a last partial launch

@@ -403,6 +403,27 @@ int narde_rollout_timed(narde_env* e, int full, int plies, int32_t* obs, int32_t
   return NARDE_OK;
 }
 
+int narde_timing_event_create(int device, unsigned flags, void** event) {
+  if (!event) return fail(NARDE_EINVAL, "NULL argument");
+  DeviceGuard dg(device);
+  hipEvent_t ev = nullptr;
+  if (hipEventCreateWithFlags(&ev, flags) != hipSuccess) return fail(NARDE_EHIP, "hipEventCreateWithFlags failed");
+  *event = ev;
+  return NARDE_OK;
+}
+
+int narde_timing_event_destroy(void* event) {
+  if (event && hipEventDestroy((hipEvent_t)event) != hipSuccess) return fail(NARDE_EHIP, "hipEventDestroy failed");
+  return NARDE_OK;
+}
+
+int narde_timing_event_elapsed_ms(void* start, void* stop, float* ms) {
+  if (!start || !stop || !ms) return fail(NARDE_EINVAL, "NULL argument");
+  if (hipEventElapsedTime(ms, (hipEvent_t)start, (hipEvent_t)stop) != hipSuccess)
+    return fail(NARDE_EHIP, "hipEventElapsedTime failed");
+  return NARDE_OK;
+}
+
 int narde_legal_full(narde_env* e, const uint8_t* dice, uint64_t* legal_first, void* stream) {
   if (!e || !legal_first) return fail(NARDE_EINVAL, "NULL argument");
   DeviceGuard dg(e->device);

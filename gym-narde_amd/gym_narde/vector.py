@@ -304,10 +304,10 @@ class VecNardeEnv:
         exactly one ctypes call (one kernel launch on the stream current
         NOW), for hot loops where the per-call Python of rollout() would
         show (the buffers must stay alive and unmoved while it is used).
-        events = (start, stop) torch.cuda.Event (either None): recorded on
+        events = (start, stop) torch.cuda.Event or TimingEvent (either None): recorded on
         that stream right before / after the launch, inside the same call
-        (narde_rollout_timed); they must have been recorded once already
-        (a torch event creates its HIP event at its first record)."""
+        (narde_rollout_timed); a torch event must have been recorded once
+        already (it creates its HIP event at its first record)."""
         for v in bufs.values():
             if v is not None and v.shape[0] < plies:
                 raise ValueError("rollout buffer shorter than plies")
@@ -320,6 +320,9 @@ class VecNardeEnv:
         else:
             evs = []
             for ev in events:
+                if isinstance(ev, TimingEvent):
+                    evs.append(ctypes.c_void_p(ev.handle))
+                    continue
                 if ev is not None and not ev.cuda_event:
                     raise ValueError("record each event once before binding it (its HIP event is created then)")
                 evs.append(ctypes.c_void_p(ev.cuda_event) if ev is not None else None)
@@ -379,3 +382,43 @@ class VecNardeEnv:
 
     def close(self):
         self.handle.close()
+
+
+class TimingEvent:
+    """A HIP event made by the library (narde_timing_event_create) for
+    rollout_launcher(..., events=...).  flags: DISABLE_SYSTEM_FENCE (default)
+    makes the record a timing-only marker -- no system-scope cache write-back
+    and invalidate when it completes, so the marker after a launch does not
+    lengthen the span it measures; 0 = HIP's default event (what a
+    torch.cuda.Event is)."""
+
+    DISABLE_SYSTEM_FENCE = 0x20000000
+
+    def __init__(self, device=None, flags=DISABLE_SYSTEM_FENCE):
+        import torch
+
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self._lib = _lib.load()
+        h = ctypes.c_void_p()
+        _lib.check(self._lib.narde_timing_event_create(dev.index or 0, int(flags), ctypes.byref(h)),
+                   "narde_timing_event_create")
+        self.handle = h.value
+
+    def elapsed_ms(self, stop):
+        """Milliseconds from this event to `stop` (both recorded and complete)."""
+        ms = ctypes.c_float()
+        _lib.check(self._lib.narde_timing_event_elapsed_ms(ctypes.c_void_p(self.handle),
+                                                            ctypes.c_void_p(stop.handle), ctypes.byref(ms)),
+                   "narde_timing_event_elapsed_ms")
+        return float(ms.value)
+
+    def close(self):
+        if self.handle:
+            self._lib.narde_timing_event_destroy(ctypes.c_void_p(self.handle))
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

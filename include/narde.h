@@ -181,6 +181,15 @@ int narde_selfplay_full(narde_env *env, int plies, void *stream);
 int narde_rollout_timed(narde_env *env, int full, int plies, int32_t *obs, int32_t *reward,
                         uint8_t *terminated, uint8_t *truncated, uint64_t *legal, void *last,
                         void *ev_start, void *ev_stop, void *stream);
+/* Timing events for narde_rollout_timed on `device`: a HIP event (returned
+ * as void*) created with hipEventCreateWithFlags(flags); flags 0 = HIP's
+ * default, 0x20000000 = hipEventDisableSystemFence (the event's record does
+ * no system-scope cache write-back / invalidate: a timing-only marker, what
+ * bench.py uses).  elapsed_ms = hipEventElapsedTime (both recorded and
+ * complete). */
+int narde_timing_event_create(int device, unsigned flags, void **event);
+int narde_timing_event_destroy(void *event);
+int narde_timing_event_elapsed_ms(void *start, void *stop, float *ms);
 /* C_0 and M for dice u8[B][2] (NULL = the next step's device dice). */
 int narde_legal_full(narde_env *env, const uint8_t *dice, uint64_t *legal_first, void *stream);
 

@@ -181,3 +181,16 @@ def test_timed_rollout_launcher(rules):
     sa, sb = a.get_state(), b.get_state()
     for k in sa:
         assert torch.equal(sa[k], sb[k]), k
+    # the bench's timing-only events (narde_timing_event_*): the same launch
+    from gym_narde.vector import TimingEvent
+
+    t0, t1 = TimingEvent("cuda:0"), TimingEvent("cuda:0")
+    timed2 = a.rollout_launcher(plies, ba, events=(t0, t1))
+    timed2()
+    plain()
+    torch.cuda.synchronize()
+    assert t0.elapsed_ms(t1) > 0.0
+    for k in ba:
+        assert torch.equal(ba[k], bb[k]), k
+    t0.close()
+    t1.close()

@@ -30,9 +30,21 @@ def main():
         ramp()
     torch.cuda.synchronize()
     out = {"lib": os.path.basename(os.environ.get("NARDE_LIB", "libnarde.so")), "rules": rules}
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    e1.record()
+    # $NARDE_EVENTS: torch (torch.cuda.Event) | nofence | default | todevice
+    # (library TimingEvents with hipEventDisableSystemFence / 0 / ReleaseToDevice)
+    kind = os.environ.get("NARDE_EVENTS", "torch")
+    out["events"] = kind
+    if kind == "torch":
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        e1.record()
+        span_of = lambda: e0.elapsed_time(e1)  # noqa: E731
+    else:
+        from gym_narde.vector import TimingEvent
+
+        fl = {"nofence": TimingEvent.DISABLE_SYSTEM_FENCE, "default": 0, "todevice": 0x40000000}[kind]
+        e0, e1 = TimingEvent("cuda:0", fl), TimingEvent("cuda:0", fl)
+        span_of = lambda: e0.elapsed_ms(e1)  # noqa: E731
     for P in plies:
         b = env.rollout_buffers(P)
         L = env.rollout_launcher(P, b, events=(e0, e1))
@@ -53,7 +65,7 @@ def main():
             L()
             torch.cuda.synchronize()
             trip.append((time.perf_counter() - t0) * 1e6)
-            span.append(e0.elapsed_time(e1) * 1e3)
+            span.append(span_of() * 1e3)
         trip.sort()
         span.sort()
         bare.sort()
