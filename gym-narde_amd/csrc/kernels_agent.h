@@ -290,6 +290,80 @@ __host__ __device__ inline uint64_t eps_to_q32(float epsilon) {
   return (uint64_t)(e * 4294967296.0);
 }
 
+// k_head_policy576: k_policy576 with the head's Q-values computed in the
+// kernel, only for the legal codes: q_c = sum_k f[k] W[c][k] + b[c]
+// (+ addcol[c * ld_w + add_row[row]]: the move-2 head's one-hot column), the
+// masked argmax over them (the first maximum in code order, as
+// torch.argmax).  One wave per env: lane l holds f[4l .. 4l + 3] (F = 256),
+// each legal code costs one coalesced 1-KiB row of W (L2-resident: 576 rows)
+// and a 64-lane sum in a fixed tree order.  The dense head GEMM computes all
+// 576 codes of every env (2 x 65536 x 256 x 576 flop per head); an env has
+// ~6-30 legal codes.  The sums round differently from hipBLASLt's, so a
+// greedy pick can differ from the dense one only between codes whose
+// Q-values tie to fp32 rounding (tests/test_gpu_dqn.py checks the gap).
+// Exploration is k_policy576's, draw for draw.
+constexpr int kHeadF = 256;
+__global__ void __launch_bounds__(256) k_head_policy576(const float* __restrict__ f, int64_t ldf,
+                                                        const float* __restrict__ w, int64_t ldw,
+                                                        const float* __restrict__ bias,
+                                                        const uint64_t* __restrict__ mask, int n, uint32_t k0,
+                                                        uint32_t k1, int head, int64_t* __restrict__ out,
+                                                        const float* __restrict__ eps_p,
+                                                        const int64_t* __restrict__ tag_p,
+                                                        const float* __restrict__ addcol,
+                                                        const int64_t* __restrict__ add_row) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  if (row >= n) return;  // whole waves: the row is uniform over the wave
+  const uint64_t eps_q32 = eps_to_q32(*eps_p);
+  const uint32_t tag = (uint32_t)*tag_p;
+  uint64_t mw[9];
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    mw[j] = mask[(size_t)row * 9 + j];
+    cnt += __builtin_popcountll(mw[j]);
+  }
+  uint32_t r[4];
+  philox4x32_10(tag, (uint32_t)row, 0u, 5u, k0, k1, r);
+  const bool explore = (uint64_t)r[0] < eps_q32;
+  int code = 0;
+  if (cnt > 0 && explore) {
+    int k = (int)mulhi_u32(head ? r[2] : r[1], (uint32_t)cnt);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int c = __builtin_popcountll(mw[j]);
+      if (k >= 0 && k < c) {
+        uint64_t m = mw[j];
+        for (int t = 0; t < k; ++t) m &= m - 1ull;
+        code = 64 * j + __builtin_ctzll(m);
+      }
+      k -= c;
+    }
+  } else if (cnt > 0) {
+    const float4 fv = reinterpret_cast<const float4*>(f + (size_t)row * (size_t)ldf)[lane];
+    const int64_t ar = addcol ? add_row[row] : 0;
+    float best = -__builtin_inff();
+    int bi = 0x7FFFFFFF;
+    for (int j = 0; j < 9; ++j) {
+      uint64_t m = mw[j];
+      while (m) {  // the legal codes of this word, ascending (wave-uniform)
+        const int c = 64 * j + __builtin_ctzll(m);
+        m &= m - 1ull;
+        const float4 wv = reinterpret_cast<const float4*>(w + (size_t)c * (size_t)ldw)[lane];
+        float v = fmaf(fv.w, wv.w, fmaf(fv.z, wv.z, fmaf(fv.y, wv.y, fv.x * wv.x)));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        v += bias[c];
+        if (addcol) v += addcol[(size_t)c * (size_t)ldw + ar];
+        if (v > best) { best = v; bi = c; }  // ascending codes: the first maximum is kept
+      }
+    }
+    code = bi;
+  }
+  if (lane == 0) out[row] = code;
+}
+
 __global__ void __launch_bounds__(256) k_policy576(const float* __restrict__ q, int64_t ldq,
                                                    const uint64_t* __restrict__ mask, int n,
                                                    uint64_t eps_q32, uint32_t k0, uint32_t k1,

@@ -518,6 +518,25 @@ int narde_policy_masked_argmax576_dev(int device, const float* q, int64_t ldq, c
   return check_launch("k_policy576");
 }
 
+int narde_head_policy576_dev(int device, const float* f, int64_t ldf, int64_t feat, const float* w, int64_t ldw,
+                             const float* bias, const uint64_t* mask, int64_t n, const float* epsilon,
+                             uint64_t seed, const int64_t* tag, int head, const float* addcol,
+                             const int64_t* add_row, int64_t* out, void* stream) {
+  if (!f || !w || !bias || !mask || !out || !epsilon || !tag || n < 0 || n > (int64_t(1) << 31) - 4)
+    return fail(NARDE_EINVAL, "bad argument");
+  if (feat != kHeadF || ldf < feat || ldw < feat || (ldf % 4) || (ldw % 4) ||
+      (reinterpret_cast<uintptr_t>(f) % 16) || (reinterpret_cast<uintptr_t>(w) % 16))
+    return fail(NARDE_EINVAL, "features must be 256 wide, rows 16-B aligned");
+  if (addcol && !add_row) return fail(NARDE_EINVAL, "addend column without its rows");
+  if (n == 0) return NARDE_OK;
+  DeviceGuard dg(device);
+  k_head_policy576<<<(int)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(f, ldf, w, ldw, bias, mask, (int)n,
+                                                                        (uint32_t)seed, (uint32_t)(seed >> 32),
+                                                                        head, out, epsilon, tag, addcol,
+                                                                        add_row);
+  return check_launch("k_head_policy576");
+}
+
 int narde_violates_block_rule(int device, const int8_t* boards, int64_t n, uint8_t* out, void* stream) {
   if (!boards || !out || n < 0 || n > (int64_t(1) << 31) - kBlock) return fail(NARDE_EINVAL, "bad argument");
   if (n == 0) return NARDE_OK;

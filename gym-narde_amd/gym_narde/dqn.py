@@ -133,6 +133,41 @@ def policy_576(q, mask576, epsilon, seed, tag, head, out=None, add=None):
     return out
 
 
+def head_policy_576(f, weight, bias, mask576, epsilon, seed, tag, head, out=None, move1=None):
+    """policy_576 with the head fused in (k_head_policy576): the Q-value of
+    each legal code only, q_c = f . weight[c, :256] + bias[c] (+ weight[c,
+    256 + move1] when move1 (B,) is given: the move-2 head's one-hot
+    column), then the masked argmax / exploration of policy_576 (the same
+    draws).  f (B,256) f32, weight (576, >=256) f32 with 16-B aligned rows;
+    epsilon / tag: device scalars or numbers (device scalars: graph-safe).
+    Replaces a dense (B,256)x(256,576) GEMM per head; greedy picks may
+    differ from the dense head's only between codes whose Q-values tie to
+    fp32 rounding."""
+    if f.dtype != torch.float32 or f.dim() != 2 or f.shape[1] != 256 or f.stride(1) != 1:
+        raise ValueError("f must be (B, 256) float32 with unit column stride")
+    if weight.dtype != torch.float32 or weight.shape[0] != MOVES or weight.stride(1) != 1 or weight.shape[1] < 256:
+        raise ValueError("weight must be (576, >=256) float32 with unit column stride")
+    if move1 is not None and weight.shape[1] < 256 + MOVES:
+        raise ValueError("the one-hot column needs the move-2 head's (576, 256 + 576) weight")
+    B = f.shape[0]
+    if out is None:
+        out = torch.empty(B, dtype=torch.int64, device=f.device)
+    eps = torch.as_tensor(epsilon, dtype=torch.float32, device=f.device)
+    tg = torch.as_tensor(tag, dtype=torch.int64, device=f.device)
+    b = bias.contiguous()
+    addcol, rows = None, None
+    if move1 is not None:
+        rows = move1.to(torch.int64).contiguous()
+        addcol = weight.data_ptr() + 256 * weight.element_size()
+    lib = _lib.load()
+    _lib.check(lib.narde_head_policy576_dev(
+        f.device.index, _lib.ptr(f), f.stride(0), 256, _lib.ptr(weight), weight.stride(0), _lib.ptr(b),
+        _lib.ptr(mask576.contiguous()), B, _lib.ptr(eps), int(seed) & (2 ** 64 - 1), _lib.ptr(tg), int(head),
+        addcol, _lib.ptr(rows), _lib.ptr(out), ctypes.c_void_p(torch.cuda.current_stream(f.device).cuda_stream)),
+        "narde_head_policy576_dev")
+    return out
+
+
 TUNED_GEMMS = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tunableop_gfx950.csv")
 
 
@@ -401,7 +436,7 @@ class BatchedDQNDriver:
     def __init__(self, env, obs="tesauro198", train_batch=4096, capacity=1 << 20,
                  learning_rate=1e-4, gamma=0.99, epsilon=1.0, epsilon_min=0.01,
                  epsilon_decay=0.995, target_update=10, updates_per_step=1, shaping=True,
-                 seed=0, fused=True):
+                 seed=0, fused=True, fused_heads=True):
         if env.full:
             raise ValueError("the DQN driver plays the reference's (move1, move2) actions: rules='ref2'")
         self.env, self.dev = env, env.device
@@ -428,6 +463,8 @@ class BatchedDQNDriver:
         # (the 198-float observation only; the torch restatement otherwise)
         self.fused = bool(fused) and obs == "tesauro198"
         self.fused_learner = bool(fused)
+        # the policy heads computed in the policy kernel (legal codes only)
+        self.fused_heads = bool(fused_heads)
         self.seed = seed
         self.tag_t = torch.zeros((), dtype=torch.int64, **z)
         self.steps = 0
@@ -476,6 +513,14 @@ class BatchedDQNDriver:
         env's exact legal masks and the fused policy kernel (epsilon and the
         step tag read from device memory)."""
         f = self.model.features_nograd(x)
+        if self.fused_heads:
+            # both heads inside the policy kernel, legal codes only
+            # (k_head_policy576): no dense (B,256)x(256,576) GEMM per head
+            h1, h2 = self.model.move1_head, self.model.move2_head
+            a1 = head_policy_576(f, h1.weight, h1.bias, self.env.legal_mask(), self.eps_t, self.seed, self.tag_t, 0)
+            m2 = self.env.legal_mask_move2(a1.to(torch.int16))
+            a2 = head_policy_576(f, h2.weight, h2.bias, m2, self.eps_t, self.seed, self.tag_t, 1, move1=a1)
+            return torch.stack([a1, a2], 1)
         a1 = policy_576(self.model.move1_head(f), self.env.legal_mask(), self.eps_t, self.seed,
                         self.tag_t, 0)
         m2 = self.env.legal_mask_move2(a1.to(torch.int16))

@@ -249,6 +249,20 @@ int narde_policy_masked_argmax576_dev(int device, const float *q, int64_t ldq, c
                                       int64_t ld_add, const int64_t *add_row, int64_t *out,
                                       void *stream);
 
+/* narde_policy_masked_argmax576_dev with the head computed inside, for the
+ * legal codes only: q_c = f[row] . w[c][0:256] + bias[c] (+ addcol[c * ldw +
+ * add_row[row]] when addcol is given: the move-2 head's one-hot column of
+ * DecomposedDQN, train_deepq_pytorch.py:184-277), masked argmax (first
+ * maximum in code order) or epsilon exploration (the same draws as
+ * narde_policy_masked_argmax576_dev).  f f32[B][ldf] (feat = 256), w
+ * f32[576][ldw], rows 16-B aligned.  The fp32 sums round differently from a
+ * dense GEMM's; a greedy pick can differ only between codes whose Q-values
+ * tie to rounding. */
+int narde_head_policy576_dev(int device, const float *f, int64_t ldf, int64_t feat, const float *w,
+                             int64_t ldw, const float *bias, const uint64_t *mask, int64_t n,
+                             const float *epsilon, uint64_t seed, const int64_t *tag, int head,
+                             const float *addcol, const int64_t *add_row, int64_t *out, void *stream);
+
 /* One DQN transition for all B envs, fused (the batched trainer of
  * gym_narde/dqn.py, config 4; reward shaping as train_deepq_pytorch.py:
  * 885-912).  After a narde_step: s' = the Tesauro-198 observation of each
