@@ -266,7 +266,8 @@ def test_fused_transition_matches_torch_restatement(shaping, pos):
 # ------------------------------------------------ fused learner kernels
 def test_per_sample_kernel_vs_torch():
     """k_per_sample: for its own uniforms u, idx == torch.searchsorted(cdf,
-    u * total, right=True) clamped, weights == (N p[idx] / total)^-beta / max
+    u * total, right=True) clamped (up to the rounding of the prefix sums),
+    weights == (N p[idx] / total)^-beta / max
     (fp32, 1 ulp of powf), beta annealed and the counter advanced."""
     from gym_narde.dqn import DeviceReplay
 
@@ -282,9 +283,16 @@ def test_per_sample_kernel_vs_torch():
     p = rp.prio ** rp.alpha
     cdf = torch.cumsum(p, 0)
     total = cdf[-1]
-    want = torch.searchsorted(cdf, u * total, right=True).clamp_(max=n - 1)
-    assert torch.equal(idx, want)
-    x = (n * (p[want] / total)) ** (-beta0)
+    v = u * total
+    want = torch.searchsorted(cdf, v, right=True).clamp_(max=n - 1)
+    # torch's cumsum (a rocPRIM look-back scan) does not fix its summation
+    # order, so the kernel's prefix sums and this one may differ by rounding:
+    # a pick may differ only where v lies within rounding of a prefix sum
+    off = idx != want
+    assert float(off.double().mean()) < 1e-3
+    lo = torch.minimum(idx, want)[off]
+    assert bool(((cdf[lo] - v[off]).abs() <= 1e-4 * total).all())
+    x = (n * (p[idx] / total)) ** (-beta0)
     assert torch.allclose(w, x / x.max(), rtol=2e-6, atol=0)
     assert float(rp.beta_t) == pytest.approx(beta0 + rp.beta_increment)
     assert int(rp.sample_ctr) == 1
