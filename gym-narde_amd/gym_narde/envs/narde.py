@@ -139,3 +139,52 @@ class Narde:
     # narde.py:186-192
     def validate_move(self, move, roll, current_player=1):
         return move in self.get_valid_moves(roll, current_player)
+
+    def get_valid_plays(self, roll, current_player=1):
+        """The plays NardeEnv.step (narde_env.py:27-103) carries out for this
+        two-dice roll, as a set of move tuples: (m1, m2) for each m1 of
+        get_valid_moves(roll) and each m2 of get_valid_moves(rest) after m1,
+        where rest is the roll less m1's distance (else its first die, the
+        step's pop(0)); (m1,) when no second move follows m1, and the only
+        play when list #1 has one move (the step then plays it alone:
+        narde_env.py:41-43); set() when no move is legal.  (The step also
+        takes partial actions -- an illegal move-2 code plays m1 alone, an
+        illegal move-1 code nothing; those are not listed.)  The README's
+        get_valid_actions (README.md:156-165) names such a set; the reference
+        code never builds one.  Three batched GPU calls: list #1, every m1
+        applied to a copy of the position, every list #2."""
+        roll = [int(d) for d in roll]
+        if len(roll) != 2 or any(d < 1 or d > 6 for d in roll):
+            raise ValueError("a roll of two dice in 1..6")
+        player = 1 if current_player == 1 else -1
+        listed = self.get_valid_moves(roll, player)
+        if len(listed) <= 1:
+            return {tuple(listed)} if listed else set()
+        first = list(dict.fromkeys(listed))  # distinct, list order
+        n = len(first)
+        board, off, ft, pl = _state_arrays(self, player)
+        board, off, ft, pl = (np.repeat(a, n, axis=0) for a in (board, off, ft, pl))
+        mv = np.array([[f, OFF if t == "off" else t] for f, t in first], np.int8)
+        h = _lib.host_handle()
+        h.call("narde_host_apply_moves", n, _lib.ptr(board), _lib.ptr(off), _lib.ptr(ft), _lib.ptr(pl), _lib.ptr(mv))
+        dice4 = np.zeros((n, 4), np.uint8)
+        for k, (f, t) in enumerate(first):
+            dist = f + 1 if t == "off" else abs(f - t)  # narde_env.py:63-70
+            rest = list(roll)
+            if dist in rest:
+                rest.remove(dist)
+            else:
+                rest.pop(0)
+            dice4[k, 0] = rest[0]
+        count = np.zeros(n, np.int16)
+        moves = np.zeros((n, _lib.MAX_MOVES, 2), np.int8)
+        h.call("narde_host_legal_moves", n, _lib.ptr(board), _lib.ptr(off), _lib.ptr(ft), _lib.ptr(pl),
+               _lib.ptr(dice4), _lib.ptr(count), _lib.ptr(moves))
+        plays = set()
+        for k, m1 in enumerate(first):
+            second = _decode_list(moves[k], count[k])
+            if second:
+                plays.update((m1, m2) for m2 in second)
+            else:
+                plays.add((m1,))
+        return plays

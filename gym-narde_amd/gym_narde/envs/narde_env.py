@@ -78,6 +78,13 @@ class NardeEnv(Env):
         self.current_player = 1 if white_roll > black_roll else -1
         return self._get_obs(), {}
 
+    def get_valid_actions(self, roll):
+        """The README's env.get_valid_actions(roll) (README.md:156-165): the
+        set of plays the next step would carry out for this roll and the
+        current player (Narde.get_valid_plays; moves in the mover's
+        perspective, as get_valid_moves returns them)."""
+        return self.game.get_valid_plays(roll, self.current_player)
+
     def render(self):
         if self.render_mode == "human":
             s = ""

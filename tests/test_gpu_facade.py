@@ -194,3 +194,50 @@ def test_timed_rollout_launcher(rules):
         assert torch.equal(ba[k], bb[k]), k
     t0.close()
     t1.close()
+
+
+def test_get_valid_plays_vs_reference_lists():
+    """Narde.get_valid_plays / NardeEnv.get_valid_actions (the README's
+    get_valid_actions) on 600 golden reference steps: the first moves are
+    exactly the reference's list #1; for the move 1 the reference step played,
+    the second moves are exactly the reference's list #2 after it (captured
+    inside the reference step); a one-move list gives that move alone, an
+    empty list no play."""
+    from gym_narde.envs import NardeEnv
+    from gym_narde.envs.narde import Narde
+
+    d = golden("steps.npz")
+    dec = lambda m: (int(m[0]), "off" if int(m[1]) == 24 else int(m[1]))  # noqa: E731
+    rng = np.random.default_rng(5)
+    seen = {0: 0, 1: 0, 2: 0}
+    for i in rng.choice(len(d["board"]), 600, replace=False):
+        g = Narde()
+        g.board[:] = d["board"][i].astype(np.int32)
+        g.borne_off_white, g.borne_off_black = (int(x) for x in d["off"][i])
+        g.first_turn_white, g.first_turn_black = (bool(x) for x in d["first_turn"][i])
+        player, dice = int(d["player"][i]), [int(x) for x in d["dice"][i]]
+        plays = g.get_valid_plays(dice, player)
+        list1 = [dec(m) for m in d["list1"][i][:d["count1"][i]]]
+        seen[min(len(list1), 2)] += 1
+        if not list1:
+            assert plays == set()
+            continue
+        if len(list1) == 1:
+            assert plays == {(list1[0],)}
+            continue
+        assert {p[0] for p in plays} == set(list1)
+        if d["ncalls"][i] == 2:  # the recorded move 1 was legal: its list #2
+            c1 = int(d["action"][i][0])
+            m1 = (c1 // 24, "off" if (c1 % 24 == 0 and c1 // 24 <= 5) else c1 % 24)
+            list2 = {dec(m) for m in d["list2"][i][:d["count2"][i]]}
+            got = {p[1] for p in plays if p[0] == m1 and len(p) == 2}
+            assert got == list2
+            assert ((m1,) in plays) == (not list2)
+    assert seen[2] > 300
+    # the env method: the same set for the env's own position and player
+    env = NardeEnv()
+    env.reset(seed=3)
+    assert env.get_valid_actions([6, 1]) == env.game.get_valid_plays([6, 1], env.current_player)
+    # the start: one checker may leave the head, the higher die first
+    # (narde.py:94-137), so list #1 holds one move and the step plays it alone
+    assert env.get_valid_actions([6, 1]) == {((23, 17),)}
