@@ -180,3 +180,31 @@ def test_full4_full_batch_window_and_invariants(plies):
                   for k in range(4))
     assert np.array_equal(nplayed, M)
     assert (M == 4).mean() > 0.08
+
+
+@pytest.mark.parametrize("n", [1, 63, 65])
+def test_tiny_batches_both_rules_both_kernels(n):
+    """One env, one wave less one lane, one wave plus one lane: REF2 rollouts
+    of 20 plies (k_rollout_pc<true, true>: non-temporal stores) and 60 plies
+    (<true, false>), FULL4 rollouts of 20 (k_rollout_wave) and 60
+    (k_rollout_full: rule + helper waves) equal the oracle ply for ply."""
+    from gym_narde.vector import VecNardeEnv
+
+    seed, env0 = 4242, 3
+    for rules in ("ref2", "full4"):
+        env = VecNardeEnv(n, device="cuda:0", seed=seed, env_id_offset=env0, rules=rules)
+        ref = O.SelfPlay(n, seed=seed, env0=env0)
+        ref.reset(0)
+        for plies in (20, 60):
+            bufs = env.rollout(plies)
+            rec = ref.run_full(plies) if rules == "full4" else ref.run(plies)
+            assert np.array_equal(np_(bufs["obs"]), rec["obs"].astype(np.int32)), (rules, plies)
+            assert np.array_equal(np_(bufs["reward"]), rec["reward"].astype(np.int32)), (rules, plies)
+            assert np.array_equal(np_(bufs["terminated"]), rec["terminated"]), (rules, plies)
+            if rules == "full4":
+                assert np.array_equal(np_(bufs["actions"]).view(np.uint64), rec["played"]), plies
+            else:
+                assert np.array_equal(np_(bufs["actions"]), rec["action"]), plies
+        st = env.get_state()
+        assert np.array_equal(np_(st["board"]), ref.board), rules
+        assert np.array_equal(np_(env.stats()), ref.stats), rules
