@@ -449,9 +449,19 @@ int narde_apply_moves(narde_env* e, const int8_t* moves, const int8_t* player, v
 int narde_observe(narde_env* e, int32_t* obs, float* tes, void* stream) {
   if (!e) return fail(NARDE_EINVAL, "NULL handle");
   if (!obs && !tes) return NARDE_OK;
+  if (tes && e->n * 198 >= (int64_t(1) << 31)) return fail(NARDE_EINVAL, "too many envs for one observation launch");
   DeviceGuard dg(e->device);
-  k_observe<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, obs, tes);
-  return check_launch("k_observe");
+  if (obs) {
+    k_observe<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, obs);
+    if (const int rc = check_launch("k_observe")) return rc;
+  }
+  if (tes) {
+    const int64_t quads = (e->n * 198 + 3) / 4;
+    k_tesauro198<<<(unsigned)((quads + kBlock - 1) / kBlock), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n,
+                                                                                              tes);
+    return check_launch("k_tesauro198");
+  }
+  return NARDE_OK;
 }
 
 int narde_dqn_transition(narde_env* e, float* state, const int64_t* actions, const int32_t* reward,
