@@ -202,6 +202,198 @@ __global__ void __launch_bounds__(256) k_rowmax_addend(const float* __restrict__
   if (lane == 0) out[i] = m;
 }
 
+// ------------------------------------------- the online heads, gathered
+// The loss reads only q1_i = Q1[i][a1_i] and q2_i = Q2[i][a2_i] (the codes
+// the replay stored), so the learner evaluates those entries instead of the
+// two dense (batch x 256) x (256 x 576) heads, and backpropagates through
+// them alone:
+//   q1_i = f_i . W1[a1_i] + b1[a1_i]
+//   q2_i = (f_i . W2[a2_i][:256] + b2[a2_i]) + W2[a2_i][256 + a1_i]
+//          (DecomposedDQN.move2_from_features' order)
+//   gf_i = g1_i W1[a1_i] + g2_i W2[a2_i][:256]
+//   gW1[c] = sum over {i: a1_i = c} of g1_i f_i, gb1[c] = the sum of those g1_i
+//   gW2[c][:256], gb2[c] likewise over {i: a2_i = c}, and
+//   gW2[c][256 + k] = the sum of g2_i over {i: a2_i = c, a1_i = k}
+// -- the gradient of the dense path (whose other entries get zero), each
+// sum in a fixed order (deterministic).  Codes outside
+// 0..575 are clamped (the ring only holds codes the policy produced).
+constexpr int kHeadF = 256;   // feature width
+constexpr int kCodes = 576;   // move codes
+constexpr int kW2 = kHeadF + kCodes;
+
+__device__ __forceinline__ int clamp_code(int64_t a) {
+  return a < 0 ? 0 : (a >= kCodes ? kCodes - 1 : (int)a);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// q1, q2 of the batch rows: one wave per row, lane j holds features 4j..4j+3
+__global__ void __launch_bounds__(256) k_heads_gather(const float* __restrict__ f, int64_t ldf,
+                                                      const float* __restrict__ w1, int64_t ldw1,
+                                                      const float* __restrict__ b1, const float* __restrict__ w2,
+                                                      int64_t ldw2, const float* __restrict__ b2,
+                                                      const int64_t* __restrict__ a, int n,
+                                                      float* __restrict__ q1, float* __restrict__ q2) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  if (i >= n) return;
+  const int c1 = clamp_code(a[2 * i]), c2 = clamp_code(a[2 * i + 1]);
+  const float4 x = reinterpret_cast<const float4*>(f + (size_t)i * ldf)[lane];
+  const float4 u = reinterpret_cast<const float4*>(w1 + (size_t)c1 * ldw1)[lane];
+  const float4 v = reinterpret_cast<const float4*>(w2 + (size_t)c2 * ldw2)[lane];
+  const float s1 = wave_sum(x.x * u.x + x.y * u.y + x.z * u.z + x.w * u.w);
+  const float s2 = wave_sum(x.x * v.x + x.y * v.y + x.z * v.z + x.w * v.w);
+  if (lane == 0) {
+    q1[i] = s1 + b1[c1];
+    q2[i] = (s2 + b2[c2]) + w2[(size_t)c2 * ldw2 + kHeadF + c1];
+  }
+}
+
+// gf_i = g1_i W1[a1_i] + g2_i W2[a2_i][:256]: one wave per row
+__global__ void __launch_bounds__(256) k_heads_grad_f(const float* __restrict__ g1, const float* __restrict__ g2,
+                                                      const float* __restrict__ w1, int64_t ldw1,
+                                                      const float* __restrict__ w2, int64_t ldw2,
+                                                      const int64_t* __restrict__ a, int n,
+                                                      float* __restrict__ gf) {
+#pragma clang fp contract(off)
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  if (i >= n) return;
+  const int c1 = clamp_code(a[2 * i]), c2 = clamp_code(a[2 * i + 1]);
+  const float4 u = reinterpret_cast<const float4*>(w1 + (size_t)c1 * ldw1)[lane];
+  const float4 v = reinterpret_cast<const float4*>(w2 + (size_t)c2 * ldw2)[lane];
+  const float s = g1[i], t = g2[i];
+  reinterpret_cast<float4*>(gf + (size_t)i * kHeadF)[lane] =
+      make_float4(s * u.x + t * v.x, s * u.y + t * v.y, s * u.z + t * v.z, s * u.w + t * v.w);
+}
+
+// gW1 / gb1 (blocks 0..575) and gW2 / gb2 (blocks 576..1151), one code per
+// block of 16 waves.  Rows go in passes of 4,096, wave w taking rows 256w ..
+// 256w + 255 of each: every lane loads the code, gradient and move-1 code of
+// its 4 rows up front; per 64-row chunk a ballot marks the rows holding this
+// code, and the wave adds them in ascending order -- lane l the feature
+// columns 4l..4l+3 (one 16-byte load of each row, up to 4 rows' loads in
+// flight), and for head 2 the one-hot columns l + 64j, the gradient and code
+// taken from the owning lane (v_readlane).  At the end the 16 waves' partial
+// sums are added in wave order.  A fixed order for given (n, codes):
+// deterministic.  Every element of the block's gradient rows is written (zero
+// where no row holds the code).  Measured at B = 4,096 (config 4): one
+// thread per column over one LDS-staged row list, 157 us (a popular code's
+// list -- hundreds of rows -- was one serial chain of loads); that list split
+// over 8 waves, 38.6 us (the staging loop and the single-wave list build
+// were latency-serialised per block); this form: see DESIGN.md section 11
+// (8 waves of 8 chunks: the same at uniform codes, 20 % slower when one
+// code holds a quarter of the rows; 8 row loads in flight: 10 % slower).
+constexpr int kGwThreads = 1024;
+constexpr int kGwWaves = kGwThreads / 64;
+constexpr int kGwChunks = 4;                         // 64-row chunks per wave per pass
+constexpr int kGwPass = kGwWaves * kGwChunks * 64;   // rows per pass
+constexpr int kGwBatch = 4;                          // row loads in flight per wave
+
+struct GwSums {  // the waves' partial sums
+  float4 f[kGwWaves][64];
+  float oh[kGwWaves][kCodes];
+  float b[kGwWaves];
+};
+
+__global__ void __launch_bounds__(kGwThreads) k_heads_grad_w(const float* __restrict__ g1,
+                                                             const float* __restrict__ g2,
+                                                             const float* __restrict__ f, int64_t ldf,
+                                                             const int64_t* __restrict__ a, int n,
+                                                             float* __restrict__ gw1, float* __restrict__ gb1,
+                                                             float* __restrict__ gw2, float* __restrict__ gb2) {
+#pragma clang fp contract(off)
+  __shared__ GwSums L;
+  const int head = blockIdx.x >= kCodes ? 1 : 0;
+  const int c = (int)blockIdx.x - head * kCodes;
+  const float* __restrict__ g = head ? g2 : g1;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  float oh[kCodes / 64];
+#pragma unroll
+  for (int j = 0; j < kCodes / 64; ++j) oh[j] = 0.0f;
+  float gs = 0.0f;
+  for (int base = 0; base < n; base += kGwPass) {
+    const int r0 = base + wave * kGwChunks * 64;
+    int code[kGwChunks], code1[kGwChunks];
+    float gv[kGwChunks];
+#pragma unroll
+    for (int q = 0; q < kGwChunks; ++q) {
+      const int r = r0 + q * 64 + lane;
+      const bool ok = r < n;
+      const int64_t* ar = a + 2 * (size_t)(ok ? r : 0);
+      code[q] = ok ? clamp_code(ar[head]) : -1;
+      code1[q] = clamp_code(ar[0]);
+      gv[q] = ok ? g[r] : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < kGwChunks; ++q) {
+      uint64_t mask = __ballot(code[q] == c);
+      const float* fq = f + (size_t)(r0 + q * 64) * ldf;
+      while (mask) {  // wave-uniform
+        int bb[kGwBatch];
+#pragma unroll
+        for (int u = 0; u < kGwBatch; ++u) {
+          bb[u] = mask ? __builtin_ctzll(mask) : -1;
+          mask &= mask - 1;
+        }
+        float4 v[kGwBatch];
+#pragma unroll
+        for (int u = 0; u < kGwBatch; ++u)
+          if (bb[u] >= 0) v[u] = reinterpret_cast<const float4*>(fq + (size_t)bb[u] * ldf)[lane];
+#pragma unroll
+        for (int u = 0; u < kGwBatch; ++u) {
+          if (bb[u] < 0) break;
+          const float gi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(gv[q]), bb[u]));
+          acc.x += gi * v[u].x;
+          acc.y += gi * v[u].y;
+          acc.z += gi * v[u].z;
+          acc.w += gi * v[u].w;
+          gs += gi;
+          if (head) {  // the one-hot column of the row's move-1 code
+            const int k1 = __builtin_amdgcn_readlane(code1[q], bb[u]);
+            const bool mine = (k1 & 63) == lane;
+#pragma unroll
+            for (int j = 0; j < kCodes / 64; ++j) oh[j] += mine && (k1 >> 6) == j ? gi : 0.0f;
+          }
+        }
+      }
+    }
+  }
+  L.f[wave][lane] = acc;
+  if (head) {
+#pragma unroll
+    for (int q = 0; q < kCodes / 64; ++q) L.oh[wave][lane + 64 * q] = oh[q];
+  }
+  if (lane == 0) L.b[wave] = gs;
+  __syncthreads();
+  if (t < kHeadF) {
+    const float* fs = reinterpret_cast<const float*>(&L.f[0][0]);
+    float x = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kGwWaves; ++w) x += fs[w * kHeadF + t];
+    (head ? gw2 + (size_t)c * kW2 : gw1 + (size_t)c * kHeadF)[t] = x;
+  }
+  if (head) {
+    for (int col = t; col < kCodes; col += kGwThreads) {
+      float x = 0.0f;
+#pragma unroll
+      for (int w = 0; w < kGwWaves; ++w) x += L.oh[w][col];
+      gw2[(size_t)c * kW2 + kHeadF + col] = x;
+    }
+  }
+  if (t == 0) {
+    float x = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kGwWaves; ++w) x += L.b[w];
+    (head ? gb2 : gb1)[c] = x;
+  }
+}
+
 // --------------------------------------------------------------- the loss
 // t1 = r + (1 - d) * gamma * m1, t2 likewise (m = the target heads' maxima);
 // td = clamp(|t1 - q1| + |t2 - q2|, 0, 100); loss = mean(w (q1 - t1)^2) +
@@ -404,6 +596,40 @@ int narde_rowmax_addend(int device, const float* base, int64_t ld, const float* 
   k_rowmax_addend<<<(unsigned)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(base, ld, tab, ld_tab, rows, (int)n,
                                                                             out);
   return check_launch("k_rowmax_addend");
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0u; }
+
+int narde_dqn_heads_forward(int device, const float* f, int64_t ldf, const float* w1, int64_t ldw1,
+                            const float* b1, const float* w2, int64_t ldw2, const float* b2, const int64_t* a,
+                            int64_t n, float* q1, float* q2, void* stream) {
+  if (!f || !w1 || !b1 || !w2 || !b2 || !a || !q1 || !q2) return bad("NULL argument");
+  if (n < 0 || n > (int64_t(1) << 31) - 4) return bad("bad batch");
+  if (ldf < kHeadF || ldw1 < kHeadF || ldw2 < kW2 || (ldf | ldw1 | ldw2) & 3) return bad("bad leading dimensions");
+  if (!aligned16(f) || !aligned16(w1) || !aligned16(w2)) return bad("f / w1 / w2 must be 16-byte aligned");
+  if (n == 0) return NARDE_OK;
+  DeviceGuard dg(device);
+  k_heads_gather<<<(unsigned)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(f, ldf, w1, ldw1, b1, w2, ldw2, b2, a,
+                                                                           (int)n, q1, q2);
+  return check_launch("k_heads_gather");
+}
+
+int narde_dqn_heads_backward(int device, const float* g1, const float* g2, const float* f, int64_t ldf,
+                             const float* w1, int64_t ldw1, const float* w2, int64_t ldw2, const int64_t* a,
+                             int64_t n, float* gf, float* gw1, float* gb1, float* gw2, float* gb2, void* stream) {
+  if (!g1 || !g2 || !f || !w1 || !w2 || !a || !gf || !gw1 || !gb1 || !gw2 || !gb2) return bad("NULL argument");
+  if (n < 0 || n > (int64_t(1) << 31) - 4) return bad("bad batch");
+  if (ldf < kHeadF || ldw1 < kHeadF || ldw2 < kW2 || (ldw1 | ldw2) & 3) return bad("bad leading dimensions");
+  if (!aligned16(w1) || !aligned16(w2) || !aligned16(gf)) return bad("w1 / w2 / gf must be 16-byte aligned");
+  DeviceGuard dg(device);
+  if (n > 0) {
+    k_heads_grad_f<<<(unsigned)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(g1, g2, w1, ldw1, w2, ldw2, a, (int)n,
+                                                                             gf);
+    const int rc = check_launch("k_heads_grad_f");
+    if (rc != NARDE_OK) return rc;
+  }
+  k_heads_grad_w<<<2 * kCodes, kGwThreads, 0, (hipStream_t)stream>>>(g1, g2, f, ldf, a, (int)n, gw1, gb1, gw2, gb2);
+  return check_launch("k_heads_grad_w");
 }
 
 int narde_dqn_loss(int device, const float* q1, const float* q2, const float* m1, const float* m2, const float* r,

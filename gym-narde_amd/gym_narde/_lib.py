@@ -65,6 +65,10 @@ SIGNATURES = {
     "narde_gather_batch": (_i32, [_i32, _vp, _i64, _i32, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp]),
     "narde_rowmax_addend": (_i32, [_i32, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp]),
+    "narde_dqn_heads_forward": (_i32, [_i32, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp,
+                                       _vp]),
+    "narde_dqn_heads_backward": (_i32, [_i32, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp,
+                                        _vp, _vp, _vp, _vp]),
     "narde_dqn_loss": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, ctypes.c_float, _vp, _vp, _vp,
                               _vp, _vp, _vp]),
     "narde_prio_update": (_i32, [_i32, _vp, _vp, _i64, ctypes.c_float, _vp, _vp, _vp, ctypes.c_float,

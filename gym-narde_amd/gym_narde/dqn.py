@@ -211,6 +211,62 @@ def rowmax_addend(base, tab, rows, out=None):
     return out
 
 
+class GatheredHeads(torch.autograd.Function):
+    """(q1, q2) = the online heads at the stored codes a (B,2):
+    model.move1_head(f).gather(1, a[:, :1]) and
+    model.move2_from_features(f, a[:, 0]).gather(1, a[:, 1:]), squeezed --
+    the only entries the loss reads (train_deepq_pytorch.py:653-720).
+    Forward and backward are three HIP kernels (narde_dqn_heads_forward /
+    _backward: per-row dot products; per-code sums over the rows holding the
+    code, deterministic) instead of the two dense (B,256)x(256,576) heads,
+    their backward GEMMs, the bias-grad reductions and the gather/scatter
+    and index_add chains autograd builds around them."""
+
+    @staticmethod
+    def forward(ctx, f, w1, b1, w2, b2, a):
+        n = f.shape[0]
+        if f.dtype != torch.float32 or f.dim() != 2 or f.shape[1] != 256 or f.stride(1) != 1:
+            raise ValueError("f must be (B, 256) float32 with unit column stride")
+        if tuple(w1.shape) != (MOVES, 256) or tuple(w2.shape) != (MOVES, 256 + MOVES):
+            raise ValueError("w1 (576, 256), w2 (576, 832)")
+        if not (w1.is_contiguous() and w2.is_contiguous() and b1.is_contiguous() and b2.is_contiguous()):
+            raise ValueError("contiguous head parameters")
+        a = a.contiguous()
+        if a.dtype != torch.int64 or tuple(a.shape) != (n, 2):
+            raise ValueError("a must be (B, 2) int64")
+        q1 = torch.empty(n, dtype=torch.float32, device=f.device)
+        q2 = torch.empty_like(q1)
+        _lib.check(_lib.load().narde_dqn_heads_forward(
+            f.device.index, _lib.ptr(f), f.stride(0), _lib.ptr(w1), w1.stride(0), _lib.ptr(b1), _lib.ptr(w2),
+            w2.stride(0), _lib.ptr(b2), _lib.ptr(a), n, _lib.ptr(q1), _lib.ptr(q2), _stream(f.device)),
+            "narde_dqn_heads_forward")
+        ctx.save_for_backward(f, w1, w2, a)
+        return q1, q2
+
+    @staticmethod
+    def backward(ctx, g1, g2):
+        f, w1, w2, a = ctx.saved_tensors
+        n = f.shape[0]
+        # (torch materialises an unused output's grad as zeros; a broadcast
+        # grad arrives with stride 0)
+        g1, g2 = g1.to(torch.float32).contiguous(), g2.to(torch.float32).contiguous()
+        gf = torch.empty((n, 256), dtype=torch.float32, device=f.device)
+        gw1, gw2 = torch.empty_like(w1), torch.empty_like(w2)
+        gb1 = torch.empty(MOVES, dtype=torch.float32, device=f.device)
+        gb2 = torch.empty_like(gb1)
+        _lib.check(_lib.load().narde_dqn_heads_backward(
+            f.device.index, _lib.ptr(g1), _lib.ptr(g2), _lib.ptr(f), f.stride(0), _lib.ptr(w1), w1.stride(0), _lib.ptr(w2),
+            w2.stride(0), _lib.ptr(a), n, _lib.ptr(gf), _lib.ptr(gw1), _lib.ptr(gb1), _lib.ptr(gw2),
+            _lib.ptr(gb2), _stream(f.device)), "narde_dqn_heads_backward")
+        return gf, gw1, gb1, gw2, gb2, None
+
+
+def gathered_heads(model, f, a):
+    """GatheredHeads.apply on a DecomposedDQN's heads."""
+    h1, h2 = model.move1_head, model.move2_head
+    return GatheredHeads.apply(f, h1.weight, h1.bias, h2.weight, h2.bias, a)
+
+
 class DQNLoss(torch.autograd.Function):
     """The decomposed loss of train_deepq_pytorch.py:653-720 as one kernel
     (k_dqn_loss): forward returns the loss and writes the TD errors into
@@ -436,7 +492,7 @@ class BatchedDQNDriver:
     def __init__(self, env, obs="tesauro198", train_batch=4096, capacity=1 << 20,
                  learning_rate=1e-4, gamma=0.99, epsilon=1.0, epsilon_min=0.01,
                  epsilon_decay=0.995, target_update=10, updates_per_step=1, shaping=True,
-                 seed=0, fused=True, fused_heads=True):
+                 seed=0, fused=True, fused_heads=True, gathered_heads=True):
         if env.full:
             raise ValueError("the DQN driver plays the reference's (move1, move2) actions: rules='ref2'")
         self.env, self.dev = env, env.device
@@ -465,6 +521,9 @@ class BatchedDQNDriver:
         self.fused_learner = bool(fused)
         # the policy heads computed in the policy kernel (legal codes only)
         self.fused_heads = bool(fused_heads)
+        # the fused learner's online heads at the stored codes only
+        # (GatheredHeads) instead of dense heads + gather
+        self.gathered_heads = bool(gathered_heads)
         self.seed = seed
         self.tag_t = torch.zeros((), dtype=torch.int64, **z)
         self.steps = 0
@@ -669,8 +728,11 @@ class BatchedDQNDriver:
         idx, w = rp.sample_fused(self.train_batch, self.seed)
         s, ns, a, r, d = rp.gather(idx)
         f = self.model.features(s)
-        q1 = self.model.move1_head(f).gather(1, a[:, :1]).squeeze(1)
-        q2 = self.model.move2_from_features(f, a[:, 0]).gather(1, a[:, 1:]).squeeze(1)
+        if self.gathered_heads:
+            q1, q2 = gathered_heads(self.model, f, a)
+        else:
+            q1 = self.model.move1_head(f).gather(1, a[:, :1]).squeeze(1)
+            q2 = self.model.move2_from_features(f, a[:, 0]).gather(1, a[:, 1:]).squeeze(1)
         with torch.no_grad():
             tf = self.target.features_nograd(ns)
             m1, am1 = self.target.move1_head(tf).max(1)

@@ -322,6 +322,30 @@ int narde_gather_batch(int device, const int64_t *idx, int64_t batch, int state_
 int narde_rowmax_addend(int device, const float *base, int64_t ld, const float *tab,
                         int64_t ld_tab, const int64_t *rows, int64_t n, float *out, void *stream);
 
+/* The online network's two heads (DecomposedDQN.move1_head / move2_head,
+ * train_deepq_pytorch.py:184-222) at the stored codes only -- what the loss
+ * of train_deepq_pytorch.py:653-720 reads (q.gather(1, action)):
+ *   q1[i] = f[i] . w1[a1] + b1[a1],
+ *   q2[i] = (f[i] . w2[a2][:256] + b2[a2]) + w2[a2][256 + a1]
+ * with (a1, a2) = a[i][0..1] (i64; codes clamped to 0..575), f f32[n][ldf]
+ * (256 features), w1 f32[576][ldw1 >= 256], w2 f32[576][ldw2 >= 832] (the
+ * move-2 head's weight: 256 feature columns, then 576 one-hot columns);
+ * f, w1, w2 16-byte aligned, leading dimensions multiples of 4. */
+int narde_dqn_heads_forward(int device, const float *f, int64_t ldf, const float *w1,
+                            int64_t ldw1, const float *b1, const float *w2, int64_t ldw2,
+                            const float *b2, const int64_t *a, int64_t n, float *q1, float *q2,
+                            void *stream);
+
+/* The backward of narde_dqn_heads_forward for dloss/dq1 = g1, dloss/dq2 = g2
+ * (f32[n]): gf f32[n][256] (dense, 16-byte aligned), and the heads' whole
+ * gradients gw1 f32[576][256], gb1 f32[576], gw2 f32[576][832], gb2
+ * f32[576] (every element written; zero for codes no row holds).  Each sum
+ * runs in a fixed order: deterministic. */
+int narde_dqn_heads_backward(int device, const float *g1, const float *g2, const float *f,
+                             int64_t ldf, const float *w1, int64_t ldw1, const float *w2,
+                             int64_t ldw2, const int64_t *a, int64_t n, float *gf, float *gw1,
+                             float *gb1, float *gw2, float *gb2, void *stream);
+
 /* The decomposed DQN loss (train_deepq_pytorch.py:653-720) on batch rows:
  * t = r + (1 - d) * gamma * m (m1/m2 the target heads' maxima), td =
  * clamp(|t1 - q1| + |t2 - q2|, 0, 100), *loss = mean(w (q1 - t1)^2) +

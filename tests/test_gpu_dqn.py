@@ -479,3 +479,59 @@ def test_head_policy_kernel_vs_fp64_heads():
             explored = got != head_policy_576(f, w1, b1, words, zero, 11, tag, head)
             assert torch.equal(got[explored], want[explored])
             assert bool(m.gather(1, got.view(-1, 1)).squeeze(1)[m.any(1)].all())
+
+
+@pytest.mark.parametrize("n", [4096, 5000, 37])
+def test_gathered_heads_vs_dense_autograd(n):
+    """GatheredHeads (narde_dqn_heads_forward / _backward) == the dense heads
+    + gather of _update_torch under torch autograd: q1, q2 and every gradient
+    (features, both heads' weights and biases) to fp32 rounding; codes
+    skewed so some hold hundreds of rows and most of the 576 hold none; a
+    row count past one LDS tile (4,096) and a ragged one; deterministic
+    from call to call."""
+    import copy
+
+    from gym_narde.dqn import DecomposedDQN, gathered_heads
+
+    torch.manual_seed(5)
+    model = DecomposedDQN(198).cuda()
+    ref = copy.deepcopy(model)
+    g = torch.Generator(device="cuda:0").manual_seed(9)
+    f0 = torch.relu(torch.randn((n, 256), device="cuda:0", generator=g))
+    skew = torch.randint(0, 40, (n, 2), device="cuda:0", generator=g)
+    wide = torch.randint(0, 576, (n, 2), device="cuda:0", generator=g)
+    a = torch.where(torch.rand((n, 2), device="cuda:0", generator=g) < 0.7, skew, wide).to(torch.int64)
+    a[: n // 10, 0] = 0  # the no-move code, common in the ring
+    up1 = torch.randn(n, device="cuda:0", generator=g)
+    up2 = torch.randn(n, device="cuda:0", generator=g)
+
+    def run(m, gathered):
+        f = f0.clone().requires_grad_(True)
+        if gathered:
+            q1, q2 = gathered_heads(m, f, a)
+        else:
+            q1 = m.move1_head(f).gather(1, a[:, :1]).squeeze(1)
+            q2 = m.move2_from_features(f, a[:, 0]).gather(1, a[:, 1:]).squeeze(1)
+        for p in m.parameters():
+            p.grad = None
+        ((q1 * up1).sum() + (q2 * up2).sum()).backward()
+        heads = [m.move1_head.weight.grad, m.move1_head.bias.grad, m.move2_head.weight.grad,
+                 m.move2_head.bias.grad]
+        return q1.detach(), q2.detach(), f.grad, [h.clone() for h in heads]
+
+    q1, q2, gf, gh = run(model, True)
+    r1, r2, rf, rh = run(ref, False)
+    assert torch.allclose(q1, r1, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(q2, r2, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(gf, rf, rtol=1e-5, atol=1e-6)
+    for x, y in zip(gh, rh):
+        assert x.shape == y.shape
+        assert torch.allclose(x, y, rtol=1e-4, atol=1e-4), float((x - y).abs().max())
+    # rows no code holds: exactly zero, as the dense path's
+    used1 = torch.zeros(576, dtype=torch.bool, device="cuda:0")
+    used1[a[:, 0]] = True
+    assert bool((gh[0][~used1] == 0).all()) and bool((gh[1][~used1] == 0).all())
+    # deterministic: a second call gives the same bits
+    s1, s2, sf, sh = run(model, True)
+    assert torch.equal(s1, q1) and torch.equal(s2, q2) and torch.equal(sf, gf)
+    assert all(torch.equal(x, y) for x, y in zip(sh, gh))

@@ -1,5 +1,6 @@
 """Profiling target for the config-4 DQN driver (rocprofv3 --kernel-trace):
-B envs, graph-captured step, N replays.  argv: [B] [steps] [eager]"""
+B envs, graph-captured step, N replays.  argv: [B] [steps] [eager];
+$NARDE_GATHERED=0 takes the dense online heads in the learner."""
 import os
 import sys
 import time
@@ -16,7 +17,8 @@ eager = len(sys.argv) > 3 and sys.argv[3] == "eager"
 if os.environ.get("NARDE_TUNED_GEMMS", "1") == "1":
     use_tuned_gemms()
 env = VecNardeEnv(B, device="cuda:0", seed=1)
-drv = BatchedDQNDriver(env, train_batch=4096, capacity=max(1 << 20, 4 * B))
+drv = BatchedDQNDriver(env, train_batch=4096, capacity=max(1 << 20, 4 * B),
+                       gathered_heads=os.environ.get("NARDE_GATHERED", "1") == "1")
 if not eager:
     drv.capture_graph(warmup=2)
 for _ in range(3):
