@@ -69,6 +69,7 @@ SIGNATURES = {
                                        _vp]),
     "narde_dqn_heads_backward": (_i32, [_i32, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp,
                                         _vp, _vp, _vp, _vp]),
+    "narde_relu_bias_grad": (_i32, [_i32, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp]),
     "narde_dqn_loss": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, ctypes.c_float, _vp, _vp, _vp,
                               _vp, _vp, _vp]),
     "narde_prio_update": (_i32, [_i32, _vp, _vp, _i64, ctypes.c_float, _vp, _vp, _vp, ctypes.c_float,

@@ -267,6 +267,50 @@ def gathered_heads(model, f, a):
     return GatheredHeads.apply(f, h1.weight, h1.bias, h2.weight, h2.bias, a)
 
 
+class LinearReLU(torch.autograd.Function):
+    """relu(x W^T + b) (one of DecomposedDQN.feature_network's Linear + ReLU
+    pairs) with the backward's ReLU mask and bias gradient in one HIP kernel
+    (narde_relu_bias_grad: deterministic column sums) instead of autograd's
+    threshold_backward + column reduction; the two GEMMs stay hipBLASLt.
+    `scratch`: a device buffer for the kernel (relu_bias_grad_scratch)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, scratch):
+        h = torch._addmm_activation(b, x, w.t())
+        ctx.save_for_backward(x, w, h)
+        ctx.scratch = scratch
+        return h
+
+    @staticmethod
+    def backward(ctx, gh):
+        x, w, h = ctx.saved_tensors
+        gh = gh.contiguous()
+        n, cols = h.shape
+        g = torch.empty_like(h)
+        db = torch.empty(cols, dtype=torch.float32, device=h.device)
+        sc = ctx.scratch
+        if sc.numel() < -(-n // 64) * cols:
+            raise ValueError("relu_bias_grad scratch too small")
+        _lib.check(_lib.load().narde_relu_bias_grad(
+            h.device.index, _f32(gh), _f32(h), n, cols, _lib.ptr(g), _lib.ptr(db), _f32(sc), _stream(h.device)),
+            "narde_relu_bias_grad")
+        dx = g @ w if ctx.needs_input_grad[0] else None
+        return dx, g.t() @ x, db, None
+
+
+def relu_bias_grad_scratch(rows, cols, device):
+    """The scratch narde_relu_bias_grad needs for (rows, cols)."""
+    return torch.empty(-(-rows // 64) * cols, dtype=torch.float32, device=device)
+
+
+def features_fused(model, x, scratch):
+    """model.features(x) as two LinearReLU layers (same parameters, same
+    forward values; gradients to fp32 rounding)."""
+    l1, l2 = model.feature_network[0], model.feature_network[2]
+    h = LinearReLU.apply(x, l1.weight, l1.bias, scratch)
+    return LinearReLU.apply(h, l2.weight, l2.bias, scratch)
+
+
 class DQNLoss(torch.autograd.Function):
     """The decomposed loss of train_deepq_pytorch.py:653-720 as one kernel
     (k_dqn_loss): forward returns the loss and writes the TD errors into
@@ -492,7 +536,7 @@ class BatchedDQNDriver:
     def __init__(self, env, obs="tesauro198", train_batch=4096, capacity=1 << 20,
                  learning_rate=1e-4, gamma=0.99, epsilon=1.0, epsilon_min=0.01,
                  epsilon_decay=0.995, target_update=10, updates_per_step=1, shaping=True,
-                 seed=0, fused=True, fused_heads=True, gathered_heads=True):
+                 seed=0, fused=True, fused_heads=True, gathered_heads=True, fused_features=True):
         if env.full:
             raise ValueError("the DQN driver plays the reference's (move1, move2) actions: rules='ref2'")
         self.env, self.dev = env, env.device
@@ -524,6 +568,10 @@ class BatchedDQNDriver:
         # the fused learner's online heads at the stored codes only
         # (GatheredHeads) instead of dense heads + gather
         self.gathered_heads = bool(gathered_heads)
+        # ... and its feature layers' ReLU mask + bias gradients in one kernel
+        # each (LinearReLU)
+        self.fused_features = bool(fused_features)
+        self._rb_scratch = relu_bias_grad_scratch(self.train_batch, 256, self.dev)
         self.seed = seed
         self.tag_t = torch.zeros((), dtype=torch.int64, **z)
         self.steps = 0
@@ -727,7 +775,7 @@ class BatchedDQNDriver:
         rp = self.replay
         idx, w = rp.sample_fused(self.train_batch, self.seed)
         s, ns, a, r, d = rp.gather(idx)
-        f = self.model.features(s)
+        f = features_fused(self.model, s, self._rb_scratch) if self.fused_features else self.model.features(s)
         if self.gathered_heads:
             q1, q2 = gathered_heads(self.model, f, a)
         else:

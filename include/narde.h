@@ -346,6 +346,13 @@ int narde_dqn_heads_backward(int device, const float *g1, const float *g2, const
                              int64_t ldw2, const int64_t *a, int64_t n, float *gf, float *gw1,
                              float *gb1, float *gw2, float *gb2, void *stream);
 
+/* The backward of h = relu(x W^T + b) up to the weight GEMM (the learner's
+ * feature layers, train_deepq_pytorch.py:184-201): g = gh * (h > 0) and db =
+ * the column sums of g, for gh, h, g f32[n][cols] (cols <= 4096).
+ * scratch: f32[ceil(n / 64) * cols] of device memory.  Deterministic. */
+int narde_relu_bias_grad(int device, const float *gh, const float *h, int64_t n, int64_t cols,
+                         float *g, float *db, float *scratch, void *stream);
+
 /* The decomposed DQN loss (train_deepq_pytorch.py:653-720) on batch rows:
  * t = r + (1 - d) * gamma * m (m1/m2 the target heads' maxima), td =
  * clamp(|t1 - q1| + |t2 - q2|, 0, 100), *loss = mean(w (q1 - t1)^2) +

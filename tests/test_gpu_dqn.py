@@ -535,3 +535,43 @@ def test_gathered_heads_vs_dense_autograd(n):
     s1, s2, sf, sh = run(model, True)
     assert torch.equal(s1, q1) and torch.equal(s2, q2) and torch.equal(sf, gf)
     assert all(torch.equal(x, y) for x, y in zip(sh, gh))
+
+
+@pytest.mark.parametrize("n", [4096, 1000, 37])
+def test_fused_feature_layers_vs_module_autograd(n):
+    """features_fused (LinearReLU: narde_relu_bias_grad for the ReLU mask and
+    the bias gradient) == model.features under torch autograd: forward
+    values, the weight / bias / input gradients of both layers to fp32
+    rounding (the weight GEMMs are the same hipBLASLt calls); ragged row
+    counts (partial 64-row slices); repeated calls give the same bits."""
+    import copy
+
+    from gym_narde.dqn import DecomposedDQN, features_fused, relu_bias_grad_scratch
+
+    torch.manual_seed(7)
+    model = DecomposedDQN(198).cuda()
+    ref = copy.deepcopy(model)
+    g = torch.Generator(device="cuda:0").manual_seed(2)
+    x0 = torch.randn((n, 198), device="cuda:0", generator=g)
+    up = torch.randn((n, 256), device="cuda:0", generator=g)
+    scratch = relu_bias_grad_scratch(n, 256, "cuda:0")
+
+    def run(m, fused):
+        x = x0.clone().requires_grad_(True)
+        f = features_fused(m, x, scratch) if fused else m.features(x)
+        for p in m.parameters():
+            p.grad = None
+        (f * up).sum().backward()
+        grads = [m.feature_network[i].weight.grad.clone() for i in (0, 2)]
+        grads += [m.feature_network[i].bias.grad.clone() for i in (0, 2)]
+        return f.detach(), x.grad, grads
+
+    f, gx, gr = run(model, True)
+    rf, rgx, rgr = run(ref, False)
+    assert torch.allclose(f, rf, rtol=1e-5, atol=1e-5)
+    assert torch.allclose(gx, rgx, rtol=1e-4, atol=1e-5)
+    for a, b in zip(gr, rgr):
+        assert torch.allclose(a, b, rtol=1e-4, atol=1e-4), float((a - b).abs().max())
+    f2, gx2, gr2 = run(model, True)
+    assert torch.equal(f2, f) and torch.equal(gx2, gx)
+    assert all(torch.equal(a, b) for a, b in zip(gr2, gr))

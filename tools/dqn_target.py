@@ -1,6 +1,7 @@
 """Profiling target for the config-4 DQN driver (rocprofv3 --kernel-trace):
 B envs, graph-captured step, N replays.  argv: [B] [steps] [eager];
-$NARDE_GATHERED=0 takes the dense online heads in the learner."""
+$NARDE_GATHERED=0 takes the dense online heads in the learner,
+$NARDE_FUSED_FEATURES=0 autograd's feature-layer backward."""
 import os
 import sys
 import time
@@ -18,7 +19,8 @@ if os.environ.get("NARDE_TUNED_GEMMS", "1") == "1":
     use_tuned_gemms()
 env = VecNardeEnv(B, device="cuda:0", seed=1)
 drv = BatchedDQNDriver(env, train_batch=4096, capacity=max(1 << 20, 4 * B),
-                       gathered_heads=os.environ.get("NARDE_GATHERED", "1") == "1")
+                       gathered_heads=os.environ.get("NARDE_GATHERED", "1") == "1",
+                       fused_features=os.environ.get("NARDE_FUSED_FEATURES", "1") == "1")
 if not eager:
     drv.capture_graph(warmup=2)
 for _ in range(3):
