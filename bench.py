@@ -266,9 +266,10 @@ def main():
     ramp_n += 3 if len(calls) == 1 else 6
 
     run_plies(args.warmup)
-    # per-env statistics land here; at N > 1 the timed region ends with the
-    # one RCCL all-gather of every rank's episode totals (24 B per rank)
-    stats_buf = torch.empty((per, 3), dtype=torch.int32, device=dev)
+    # the episode totals land here (VecNardeEnv.totals: one kernel, 64
+    # partial rows); at N > 1 the timed region ends with the one RCCL
+    # all-gather of every rank's rows (1.5 KB per rank), summed afterwards
+    rows_buf = torch.empty((64, 3), dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -284,7 +285,7 @@ def main():
     launches = sizes
     t_sub = time.perf_counter()
     if world > 1:
-        totals = D.gather_totals(env.stats(out=stats_buf))
+        gathered = D.gather_total_rows(env.totals(out=rows_buf))
     torch.cuda.synchronize()
     t_wait = time.perf_counter()
     barrier()
@@ -296,7 +297,8 @@ def main():
                "close": round((elapsed - (t_wait - t0)) * 1e6, 1)}
     span_ms = ev0.elapsed_ms(ev1)
     if world == 1:
-        totals = D.gather_totals(env.stats(out=stats_buf))
+        gathered = D.gather_total_rows(env.totals(out=rows_buf))
+    totals = gathered.sum(1)
     # algorithmic bytes of every launch in the span (a last partial launch
     # included), and the mean duration of a full-length launch
     span_bytes = sum(launch_bytes(per, p, is_full4) for p in launches)

@@ -6,6 +6,7 @@
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int kTotalRows = NARDE_TOTAL_ROWS;  // narde_get_totals' partial rows
 
 struct Planes {
   uint4* p0;

@@ -134,6 +134,36 @@ __global__ void __launch_bounds__(kBlock) k_get_stats(Planes pl, int n, int32_t*
   out[3 * i] = s.x; out[3 * i + 1] = s.y; out[3 * i + 2] = s.z;
 }
 
+// Per-rank totals of the statistics as kTotalRows partial rows (row b: the
+// envs of the b-th contiguous range), int64: one launch, no cross-block
+// combine (a last-block combine needs a device-scope fence per block, which
+// writes back the XCD's L2); the reader adds the rows.
+__global__ void __launch_bounds__(kBlock) k_get_totals(Planes pl, int n, int64_t* __restrict__ rows) {
+  __shared__ long long red[kBlock / 64][3];
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int per = (n + kTotalRows - 1) / kTotalRows;
+  const int i0 = b * per, i1 = min(n, i0 + per);
+  long long e = 0, w = 0, k = 0;
+  for (int i = i0 + (int)threadIdx.x; i < i1; i += kBlock) {
+    const int4 s = pl.stats[i];
+    e += s.x; w += s.y; k += s.z;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    e += __shfl_xor(e, o, 64);
+    w += __shfl_xor(w, o, 64);
+    k += __shfl_xor(k, o, 64);
+  }
+  if (lane == 0) { red[wave][0] = e; red[wave][1] = w; red[wave][2] = k; }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    long long t = 0;
+#pragma unroll
+    for (int q = 0; q < kBlock / 64; ++q) t += red[q][threadIdx.x];
+    rows[3 * b + threadIdx.x] = (int64_t)t;
+  }
+}
+
 // execute_rotated_move (narde.py:36-56,108-125) of one move per env.  The
 // reference executes any (from, to) it is handed; the moves this record can
 // hold are those whose source has one of the mover's checkers and whose

@@ -439,6 +439,13 @@ int narde_get_stats(narde_env* e, int32_t* stats, void* stream) {
   return check_launch("k_get_stats");
 }
 
+int narde_get_totals(narde_env* e, int64_t* rows, void* stream) {
+  if (!e || !rows) return fail(NARDE_EINVAL, "NULL argument");
+  DeviceGuard dg(e->device);
+  k_get_totals<<<kTotalRows, kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rows);
+  return check_launch("k_get_totals");
+}
+
 int narde_apply_moves(narde_env* e, const int8_t* moves, const int8_t* player, void* stream) {
   if (!e || !moves) return fail(NARDE_EINVAL, "NULL argument");
   DeviceGuard dg(e->device);

@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("NARDE_LIB", os.path.join(HERE, "libnarde.so"))
 OK = 0
 OFF = 24
 MAX_MOVES = 64
+TOTAL_ROWS = 64  # NARDE_TOTAL_ROWS
 DICE_ALL36 = 0
 DICE_NODOUBLES = 1
 
@@ -48,6 +49,7 @@ SIGNATURES = {
     "narde_timing_event_elapsed_ms": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_float)]),
     "narde_legal_full": (_i32, [_vp, _vp, _vp, _vp]),
     "narde_get_stats": (_i32, [_vp, _vp, _vp]),
+    "narde_get_totals": (_i32, [_vp, _vp, _vp]),
     "narde_apply_moves": (_i32, [_vp, _vp, _vp, _vp]),
     "narde_observe": (_i32, [_vp, _vp, _vp, _vp]),
     "narde_legal_mask576": (_i32, [_vp, _vp, _vp]),

@@ -349,6 +349,18 @@ class VecNardeEnv:
         self.handle.call("narde_get_stats", _lib.ptr(out), self._s())
         return out
 
+    def totals(self, out=None):
+        """(64,3) int64 partial sums of stats() over contiguous env ranges
+        (narde_get_totals: one launch); .sum(0) gives {episodes, white
+        points, black points} of the handle (into `out` if given)."""
+        if out is None:
+            out = self.torch.empty((_lib.TOTAL_ROWS, 3), dtype=self.torch.int64, device=self.device)
+        elif (tuple(out.shape) != (_lib.TOTAL_ROWS, 3) or out.dtype != self.torch.int64
+              or out.device != self.device or not out.is_contiguous()):
+            raise ValueError("out must be a contiguous (64,3) int64 tensor on the env's device")
+        self.handle.call("narde_get_totals", _lib.ptr(out), self._s())
+        return out
+
     def get_state(self):
         B, t, dev = self.num_envs, self.torch, self.device
         st = dict(board=t.empty((B, 24), dtype=t.int8, device=dev),

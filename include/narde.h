@@ -197,6 +197,14 @@ int narde_legal_full(narde_env *env, const uint8_t *dice, uint64_t *legal_first,
  * points} since the last reset of that env. */
 int narde_get_stats(narde_env *env, int32_t *stats, void *stream);
 
+/* The same statistics summed over the handle's envs, as NARDE_TOTAL_ROWS
+ * partial rows i64[NARDE_TOTAL_ROWS][3] (row b: the b-th contiguous range
+ * of envs); the totals are the column sums.  One launch -- what a sharded
+ * self-play run all-gathers per rank (the reference's returns, collected
+ * by its training loops: train_deepq_pytorch.py:855-1081). */
+#define NARDE_TOTAL_ROWS 64
+int narde_get_totals(narde_env *env, int64_t *rows, void *stream);
+
 /* execute_rotated_move(move, player) per env: moves i8[B][2] in the
  * perspective of player[B] (+1/-1; NULL = each env's current mover);
  * from < 0 skips the env.  Clears that player's first_turn flag.  A move the

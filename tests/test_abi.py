@@ -73,6 +73,7 @@ def test_argument_errors_are_einval_before_any_device_call():
         ("narde_per_sample", (0, N, N, 100, 64, 0, N, N, 0.001, N, N, N, N, N)),
         ("narde_gather_batch", (0, N, 64, 198, N, 64, 128, N, N, N, N, N, N, N, N, N)),
         ("narde_rowmax_addend", (0, N, 576, N, 576, N, 64, N, N)),
+        ("narde_get_totals", (N, N, N)),
         ("narde_dqn_heads_forward", (0, N, 256, N, 256, N, N, 832, N, N, 64, N, N, N)),
         ("narde_dqn_heads_backward", (0, N, N, N, 256, N, 256, N, 832, N, 64, N, N, N, N, N, N)),
         ("narde_relu_bias_grad", (0, N, N, 64, 256, N, N, N, N)),

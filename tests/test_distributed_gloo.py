@@ -45,6 +45,17 @@ def _shard_selfplay(lib, first, per):
     return st
 
 
+def _rows_of(st, nrows=64):
+    """VecNardeEnv.totals()'s partial rows (narde_get_totals: row b sums
+    the b-th contiguous range of ceil(n / 64) envs), restated on the host."""
+    n = st.shape[0]
+    per = -(-n // nrows)
+    rows = np.zeros((nrows, 3), np.int64)
+    for b in range(nrows):
+        rows[b] = st[b * per:min(n, (b + 1) * per)].astype(np.int64).sum(0)
+    return rows
+
+
 def _rank_main(rank, world, port, lib_path, out_path):
     import sys
 
@@ -61,10 +72,12 @@ def _rank_main(rank, world, port, lib_path, out_path):
     first, per = D.env_shard(B, r, w)
     st = _shard_selfplay(ctypes.CDLL(lib_path), first, per)
     gathered = D.gather_stats(torch.from_numpy(st))
-    totals = D.gather_totals(torch.from_numpy(st))  # what bench.py's timed region gathers
+    totals = D.gather_totals(torch.from_numpy(st))
+    rows = D.gather_total_rows(torch.from_numpy(_rows_of(st)))  # what bench.py's timed region gathers
     if r == 0:
         np.save(out_path, gathered.numpy())
         np.save(out_path + ".totals.npy", totals.numpy())
+        np.save(out_path + ".rows.npy", rows.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
@@ -93,6 +106,8 @@ def test_gloo_shards_equal_single_process(tmp_path, hostcheck, world):
     totals = np.load(out + ".totals.npy")  # (world, 3): each rank's shard summed
     per = B // world
     assert np.array_equal(totals, sp.stats.astype(np.int64).reshape(world, per, 3).sum(1))
+    rows = np.load(out + ".rows.npy")  # (world, 64, 3) partial rows per rank
+    assert rows.shape == (world, 64, 3) and np.array_equal(rows.sum(1), totals)
     from gym_narde.distributed import summarize
 
     s = summarize(torch.from_numpy(gathered))
@@ -106,3 +121,11 @@ def test_gather_totals_without_process_group():
     tot = gather_totals(st)
     assert tot.dtype == torch.int64 and tot.tolist() == [[4, 2, 6]]
     assert summarize(tot) == {"episodes": 4, "white_points": 2, "black_points": 6}
+
+
+def test_gather_total_rows_without_process_group():
+    from gym_narde.distributed import gather_total_rows
+
+    rows = torch.arange(12, dtype=torch.int64).reshape(4, 3)
+    out = gather_total_rows(rows)
+    assert out.shape == (1, 4, 3) and torch.equal(out[0], rows)

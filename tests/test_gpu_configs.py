@@ -75,6 +75,13 @@ def test_config4_eight_shards_of_65536():
 
     st = torch.cat([D.gather_stats(e.stats()) for e in shards])
     assert torch.equal(st, whole.stats())
+    # the per-rank totals the bench gathers (one kernel per shard) add up to
+    # the whole batch's, and each shard's rows to its own statistics
+    rows = torch.cat([D.gather_total_rows(e.totals()) for e in shards])
+    assert rows.shape == (W, 64, 3)
+    for r, e in enumerate(shards):
+        assert torch.equal(rows[r].sum(0), e.stats().to(torch.int64).sum(0)), r
+    assert torch.equal(rows.sum((0, 1)), whole.totals().sum(0))
     s = D.summarize(st)
     assert s["episodes"] > S * W // 4  # ~340 plies: several hundred thousand games ended
     for e in shards + [whole]:
@@ -303,9 +310,12 @@ st = env.stats()
 g = D.gather_stats(st)  # all_gather_into_tensor over RCCL on device tensors
 torch.cuda.synchronize()
 assert g.is_cuda and g.shape == st.shape and torch.equal(g, st)
-tot = D.gather_totals(st)  # the bench's timed-region gather: per-rank totals
+tot = D.gather_totals(st)  # per-rank totals
 torch.cuda.synchronize()
 assert tot.is_cuda and tot.shape == (1, 3) and torch.equal(tot[0], st.to(torch.int64).sum(0))
+rows = D.gather_total_rows(env.totals())  # the bench's timed-region gather: one kernel + one all-gather
+torch.cuda.synchronize()
+assert rows.is_cuda and rows.shape == (1, 64, 3) and torch.equal(rows.sum(1), tot)
 t = torch.tensor([1.5, 2.5], dtype=torch.float64, device="cuda:0")
 dist.all_reduce(t, op=dist.ReduceOp.MAX)  # the bench's max-over-ranks timing
 dist.barrier()
