@@ -90,68 +90,86 @@ __device__ __forceinline__ float block_sum(float v, float* lds) {
 // with cdf[k] > v_j (torch.searchsorted(right=True)), clamped to n - 1;
 // w_j = (n * p[idx] / total)^-beta normalised by the batch max.  Then beta
 // <- min(1, beta + beta_inc) and *counter += 1.
-// One sample per thread over ceil(batch / 256) blocks (a single block would
-// pull every search through one CU's L1); the batch max meets in
-// scratch[0] (atomicMax on the float's bits: the weights are positive) and
-// the last block to finish (ticket scratch[1]) normalises, steps beta and
-// the counter, and clears the scratch for the next call.
-constexpr int kSampleThreads = 256;
+// One WAVE per sample (4 per block): a 64-ary search -- each round the 64
+// lanes load 64 evenly spaced pivots of the current range and a ballot
+// picks the first pivot > v, so 1M rows take 4 dependent rounds instead of
+// a binary search's 20 -- then lane 0 writes idx and the unnormalised w.
+// k_per_finish (one block, after the kernel boundary) takes the batch max,
+// normalises, and steps beta and the counter.
+// (One sample per thread with a binary search and the last block
+// normalising behind a ticket: 16.3 us at batch 4,096 over 1M rows, 13.4 of
+// them the search's dependent loads; the wave search with every block's
+// max meeting in one word by atomicMax: 17.2 + 4.5 us -- 1,024 atomics on
+// one address serialise.)
+constexpr int kSampleWaves = 4;
 
-__global__ void __launch_bounds__(kSampleThreads) k_per_sample(const float* __restrict__ p,
-                                                               const float* __restrict__ cdf, int64_t n,
-                                                               int batch, uint32_t k0, uint32_t k1,
-                                                               int64_t* __restrict__ counter,
-                                                               double* __restrict__ beta, double beta_inc,
-                                                               int64_t* __restrict__ idx_out,
-                                                               float* __restrict__ w_out,
-                                                               float* __restrict__ u_out,
-                                                               uint32_t* __restrict__ scratch) {
-  __shared__ float red[kSampleThreads / 64];
-  __shared__ bool last;
-  const int j = blockIdx.x * kSampleThreads + threadIdx.x;
-  float x = 0.0f;
-  if (j < batch) {
+__global__ void __launch_bounds__(64 * kSampleWaves) k_per_sample(const float* __restrict__ p,
+                                                                  const float* __restrict__ cdf, int64_t n,
+                                                                  int batch, uint32_t k0, uint32_t k1,
+                                                                  const int64_t* __restrict__ counter,
+                                                                  const double* __restrict__ beta,
+                                                                  int64_t* __restrict__ idx_out,
+                                                                  float* __restrict__ w_out,
+                                                                  float* __restrict__ u_out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = blockIdx.x * kSampleWaves + wave;
+  if (j < batch) {  // wave-uniform
     const float total = cdf[n - 1];
     uint32_t r[4];
     narde::philox4x32_10((uint32_t)*counter, (uint32_t)j, 0u, 7u, k0, k1, r);
     const float u = (float)(r[0] >> 8) * (1.0f / 16777216.0f);
-    if (u_out) u_out[j] = u;
     const float v = u * total;
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (cdf[mid] > v) hi = mid;
-      else lo = mid + 1;
+    // the first k in [lo, lo + len) with cdf[k] > v, or lo + len if none
+    int64_t lo = 0, len = n;
+    bool split = false;  // a split range ends in a row > v
+    while (len > 1) {
+      const int64_t step = (len + 63) / 64;
+      const int64_t off = (int64_t)(lane + 1) * step - 1;
+      const int64_t piv = lo + (off < len ? off : len - 1);
+      const uint64_t hit = __ballot(cdf[piv] > v);
+      if (hit == 0ull) {  // only possible in the first round: no row > v
+        lo += len;
+        len = 0;
+        break;
+      }
+      const int64_t f = (int64_t)__builtin_ctzll(hit);
+      const int64_t nlo = lo + f * step;
+      const int64_t end = lo + len;
+      len = (nlo + step < end ? nlo + step : end) - nlo;
+      lo = nlo;
+      split = true;
     }
+    if (len == 1 && !split && !(cdf[lo] > v)) lo += 1;  // n == 1: the range was never split
     const int64_t k = lo < n - 1 ? lo : n - 1;
-    x = powf((float)n * (p[k] / total), -(float)*beta);
-    idx_out[j] = k;
-    w_out[j] = x;
+    const float x = powf((float)n * (p[k] / total), -(float)*beta);
+    if (lane == 0) {
+      idx_out[j] = k;
+      w_out[j] = x;
+      if (u_out) u_out[j] = u;
+    }
   }
-  __threadfence();  // this thread's idx/w writes before the block's ticket (release)
-  // block max, then the grid max in scratch[0]
+}
+
+// the batch max of w (one block, in LDS), every w normalised by it, then
+// beta and the counter stepped
+__global__ void __launch_bounds__(1024) k_per_finish(int batch, int64_t* __restrict__ counter,
+                                                     double* __restrict__ beta, double beta_inc,
+                                                     float* __restrict__ w_out) {
+  __shared__ float red[16];
+  float m = 0.0f;
+  for (int i = threadIdx.x; i < batch; i += 1024) m = fmaxf(m, w_out[i]);
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o, 64));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    float m = red[0];
-    for (int w = 1; w < kSampleThreads / 64; ++w) m = fmaxf(m, red[w]);
-    atomicMax(&scratch[0], __float_as_uint(m));
-    __threadfence();
-    last = atomicAdd(&scratch[1], 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();  // acquire: every block's w writes are visible
-  const float wmax = __uint_as_float(atomicAdd(&scratch[0], 0u));
-  for (int i = threadIdx.x; i < batch; i += kSampleThreads) w_out[i] = w_out[i] / wmax;
+  float wmax = red[0];
+#pragma unroll
+  for (int q = 1; q < 16; ++q) wmax = fmaxf(wmax, red[q]);
+  for (int i = threadIdx.x; i < batch; i += 1024) w_out[i] = w_out[i] / wmax;
   if (threadIdx.x == 0) {
     const double b = *beta + beta_inc;
     *beta = b < 1.0 ? b : 1.0;
     *counter += 1;
-    scratch[0] = 0u;
-    scratch[1] = 0u;
   }
 }
 
@@ -623,14 +641,16 @@ extern "C" {
 int narde_per_sample(int device, const float* p, const float* cdf, int64_t n, int64_t batch, uint64_t seed,
                      int64_t* counter, double* beta, double beta_inc, int64_t* idx, float* w, float* u,
                      uint32_t* scratch, void* stream) {
-  if (!p || !cdf || !counter || !beta || !idx || !w || !scratch) return bad("NULL argument");
+  if (!p || !cdf || !counter || !beta || !idx || !w) return bad("NULL argument");
   if (n <= 0 || batch <= 0 || batch > (int64_t(1) << 24)) return bad("need n > 0 and 0 < batch <= 2^24");
   DeviceGuard dg(device);
-  const unsigned blocks = (unsigned)((batch + kSampleThreads - 1) / kSampleThreads);
-  k_per_sample<<<blocks, kSampleThreads, 0, (hipStream_t)stream>>>(p, cdf, n, (int)batch, (uint32_t)seed,
-                                                                   (uint32_t)(seed >> 32), counter, beta, beta_inc,
-                                                                   idx, w, u, scratch);
-  return check_launch("k_per_sample");
+  const unsigned blocks = (unsigned)((batch + kSampleWaves - 1) / kSampleWaves);
+  k_per_sample<<<blocks, 64 * kSampleWaves, 0, (hipStream_t)stream>>>(p, cdf, n, (int)batch, (uint32_t)seed,
+                                                                      (uint32_t)(seed >> 32), counter, beta, idx, w, u);
+  const int rc = check_launch("k_per_sample");
+  if (rc != NARDE_OK) return rc;
+  k_per_finish<<<1, 1024, 0, (hipStream_t)stream>>>((int)batch, counter, beta, beta_inc, w);
+  return check_launch("k_per_finish");
 }
 
 int narde_gather_batch(int device, const int64_t* idx, int64_t batch, int state_size, const float* obs,

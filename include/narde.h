@@ -312,7 +312,8 @@ int narde_dqn_transition(narde_env *env, float *state, const int64_t *actions,
  * seed) (24-bit uniform, written to u if non-NULL), idx_j = first k with
  * cdf[k] > u_j * cdf[n-1] (clamped to n-1), w_j = (n p[idx_j] /
  * cdf[n-1])^-beta / max_j; then beta = min(1, beta + beta_inc), counter += 1.
- * scratch: u32[2] of zeros, left zeroed (the grid's max and finish ticket). */
+ * scratch: unused (may be NULL; kept for the ABI).  Two
+ * launches: a 64-ary search, one wave per sample, then the normalisation. */
 int narde_per_sample(int device, const float *p, const float *cdf, int64_t n, int64_t batch,
                      uint64_t seed, int64_t *counter, double *beta, double beta_inc, int64_t *idx,
                      float *w, float *u, uint32_t *scratch, void *stream);

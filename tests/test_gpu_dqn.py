@@ -575,3 +575,42 @@ def test_fused_feature_layers_vs_module_autograd(n):
     f2, gx2, gr2 = run(model, True)
     assert torch.equal(f2, f) and torch.equal(gx2, gx)
     assert all(torch.equal(a, b) for a, b in zip(gr2, gr))
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 4097, 300000])
+def test_per_sample_search_exact_on_given_cdf(n):
+    """narde_per_sample's 64-ary search (one wave per sample) on a GIVEN
+    prefix sum: idx == torch.searchsorted(cdf, u * cdf[-1], right=True)
+    clamped to n - 1, exactly, with runs of zero-priority rows (flat
+    stretches of the cdf, the ring's pending rows) and ragged sizes; the
+    weights normalised by their max; the scratch word left zero."""
+    import ctypes
+
+    from gym_narde import _lib
+
+    g = torch.Generator(device="cuda:0").manual_seed(n)
+    p = torch.rand(n, device="cuda:0", generator=g) + 0.05
+    if n > 4:
+        p[torch.rand(n, device="cuda:0", generator=g) < 0.3] = 0.0  # pending rows
+        p[0] = 0.0
+        p[n // 2:n // 2 + min(100, n // 4)] = 0.0
+    p[-1] = 0.5  # (u * total may round to total: the clamp then picks the last row)
+    cdf = torch.cumsum(p, 0)
+    B = 4096
+    idx = torch.empty(B, dtype=torch.int64, device="cuda:0")
+    w = torch.empty(B, device="cuda:0")
+    u = torch.empty(B, device="cuda:0")
+    ctr = torch.zeros((), dtype=torch.int64, device="cuda:0")
+    beta = torch.full((), 0.4, dtype=torch.float64, device="cuda:0")
+    scratch = torch.zeros(2, dtype=torch.int32, device="cuda:0")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    P = _lib.ptr
+    _lib.check(_lib.load().narde_per_sample(0, P(p), P(cdf), n, B, 77, P(ctr), P(beta), 0.001, P(idx), P(w), P(u),
+                                            P(scratch), st), "narde_per_sample")
+    torch.cuda.synchronize()
+    want = torch.searchsorted(cdf, u * cdf[-1], right=True).clamp_(max=n - 1)
+    assert torch.equal(idx, want)
+    x = (n * (p[idx] / cdf[-1])) ** (-0.4)
+    assert torch.allclose(w, x / x.max(), rtol=2e-6, atol=0)
+    assert int(scratch.abs().sum()) == 0 and int(ctr) == 1
+    assert float(beta) == pytest.approx(0.401)
