@@ -311,10 +311,11 @@ __global__ void __launch_bounds__(256) k_head_policy576(const float* __restrict_
                                                         const float* __restrict__ bias,
                                                         const uint64_t* __restrict__ mask, int n, uint32_t k0,
                                                         uint32_t k1, int head, int64_t* __restrict__ out,
-                                                        const float* __restrict__ eps_p,
+                                                        int64_t ld_out, int16_t* __restrict__ out16,
+                                                        int64_t ld_out16, const float* __restrict__ eps_p,
                                                         const int64_t* __restrict__ tag_p,
                                                         const float* __restrict__ addcol,
-                                                        const int64_t* __restrict__ add_row) {
+                                                        const int64_t* __restrict__ add_row, int64_t ld_row) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
   if (row >= n) return;  // whole waves: the row is uniform over the wave
@@ -345,7 +346,7 @@ __global__ void __launch_bounds__(256) k_head_policy576(const float* __restrict_
     }
   } else if (cnt > 0) {
     const float4 fv = reinterpret_cast<const float4*>(f + (size_t)row * (size_t)ldf)[lane];
-    const int64_t ar = addcol ? add_row[row] : 0;
+    const int64_t ar = addcol ? add_row[(size_t)row * (size_t)ld_row] : 0;
     float best = -__builtin_inff();
     int bi = 0x7FFFFFFF;
     for (int j = 0; j < 9; ++j) {
@@ -364,7 +365,10 @@ __global__ void __launch_bounds__(256) k_head_policy576(const float* __restrict_
     }
     code = bi;
   }
-  if (lane == 0) out[row] = code;
+  if (lane == 0) {  // strided: straight into a column of the (B, 2) action rows
+    out[(size_t)row * (size_t)ld_out] = code;
+    if (out16) out16[(size_t)row * (size_t)ld_out16] = (int16_t)code;
+  }
 }
 
 __global__ void __launch_bounds__(256) k_policy576(const float* __restrict__ q, int64_t ldq,

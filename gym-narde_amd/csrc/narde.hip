@@ -538,9 +538,11 @@ int narde_policy_masked_argmax576_dev(int device, const float* q, int64_t ldq, c
 int narde_head_policy576_dev(int device, const float* f, int64_t ldf, int64_t feat, const float* w, int64_t ldw,
                              const float* bias, const uint64_t* mask, int64_t n, const float* epsilon,
                              uint64_t seed, const int64_t* tag, int head, const float* addcol,
-                             const int64_t* add_row, int64_t* out, void* stream) {
+                             const int64_t* add_row, int64_t ld_row, int64_t* out, int64_t ld_out,
+                             int16_t* out16, int64_t ld_out16, void* stream) {
   if (!f || !w || !bias || !mask || !out || !epsilon || !tag || n < 0 || n > (int64_t(1) << 31) - 4)
     return fail(NARDE_EINVAL, "bad argument");
+  if (ld_out < 1 || (out16 && ld_out16 < 1) || (addcol && ld_row < 1)) return fail(NARDE_EINVAL, "bad strides");
   if (feat != kHeadF || ldf < feat || ldw < feat || (ldf % 4) || (ldw % 4) ||
       (reinterpret_cast<uintptr_t>(f) % 16) || (reinterpret_cast<uintptr_t>(w) % 16))
     return fail(NARDE_EINVAL, "features must be 256 wide, rows 16-B aligned");
@@ -549,8 +551,8 @@ int narde_head_policy576_dev(int device, const float* f, int64_t ldf, int64_t fe
   DeviceGuard dg(device);
   k_head_policy576<<<(int)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(f, ldf, w, ldw, bias, mask, (int)n,
                                                                         (uint32_t)seed, (uint32_t)(seed >> 32),
-                                                                        head, out, epsilon, tag, addcol,
-                                                                        add_row);
+                                                                        head, out, ld_out, out16, ld_out16,
+                                                                        epsilon, tag, addcol, add_row, ld_row);
   return check_launch("k_head_policy576");
 }
 

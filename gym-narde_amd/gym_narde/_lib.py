@@ -59,7 +59,7 @@ SIGNATURES = {
     "narde_policy_masked_argmax576_dev": (_i32, [_i32, _vp, _i64, _vp, _i64, _vp, _u64, _vp, _i32, _vp,
                                                  _i64, _vp, _vp, _vp]),
     "narde_head_policy576_dev": (_i32, [_i32, _vp, _i64, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _u64, _vp, _i32,
-                                        _vp, _vp, _vp, _vp]),
+                                        _vp, _vp, _i64, _vp, _i64, _vp, _i64, _vp]),
     "narde_dqn_transition": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp, _vp, _vp, _vp,
                                     _vp, _vp, _vp, _i64, _vp]),
     "narde_per_sample": (_i32, [_i32, _vp, _vp, _i64, _i64, _u64, _vp, _vp, ctypes.c_double, _vp, _vp, _vp,

@@ -133,7 +133,7 @@ def policy_576(q, mask576, epsilon, seed, tag, head, out=None, add=None):
     return out
 
 
-def head_policy_576(f, weight, bias, mask576, epsilon, seed, tag, head, out=None, move1=None):
+def head_policy_576(f, weight, bias, mask576, epsilon, seed, tag, head, out=None, move1=None, out16=None):
     """policy_576 with the head fused in (k_head_policy576): the Q-value of
     each legal code only, q_c = f . weight[c, :256] + bias[c] (+ weight[c,
     256 + move1] when move1 (B,) is given: the move-2 head's one-hot
@@ -152,19 +152,30 @@ def head_policy_576(f, weight, bias, mask576, epsilon, seed, tag, head, out=None
     B = f.shape[0]
     if out is None:
         out = torch.empty(B, dtype=torch.int64, device=f.device)
+
+    def vec1(t, dtype, what):  # (B,) of dtype, any positive stride (a column of (B, 2) rows)
+        if t.dtype != dtype or t.dim() != 1 or t.shape[0] != B or t.stride(0) < 1:
+            raise ValueError(f"{what} must be ({B},) {dtype}")
+        return t
+
+    vec1(out, torch.int64, "out")
+    if out16 is not None:
+        vec1(out16, torch.int16, "out16")
     eps = torch.as_tensor(epsilon, dtype=torch.float32, device=f.device)
     tg = torch.as_tensor(tag, dtype=torch.int64, device=f.device)
     b = bias.contiguous()
     addcol, rows = None, None
     if move1 is not None:
-        rows = move1.to(torch.int64).contiguous()
+        rows = move1 if move1.dtype == torch.int64 else move1.to(torch.int64)
+        vec1(rows, torch.int64, "move1")
         addcol = weight.data_ptr() + 256 * weight.element_size()
     lib = _lib.load()
     _lib.check(lib.narde_head_policy576_dev(
         f.device.index, _lib.ptr(f), f.stride(0), 256, _lib.ptr(weight), weight.stride(0), _lib.ptr(b),
         _lib.ptr(mask576.contiguous()), B, _lib.ptr(eps), int(seed) & (2 ** 64 - 1), _lib.ptr(tg), int(head),
-        addcol, _lib.ptr(rows), _lib.ptr(out), ctypes.c_void_p(torch.cuda.current_stream(f.device).cuda_stream)),
-        "narde_head_policy576_dev")
+        addcol, _lib.ptr(rows), rows.stride(0) if rows is not None else 1, _lib.ptr(out), out.stride(0),
+        _lib.ptr(out16), out16.stride(0) if out16 is not None else 1,
+        ctypes.c_void_p(torch.cuda.current_stream(f.device).cuda_stream)), "narde_head_policy576_dev")
     return out
 
 
@@ -623,11 +634,17 @@ class BatchedDQNDriver:
         if self.fused_heads:
             # both heads inside the policy kernel, legal codes only
             # (k_head_policy576): no dense (B,256)x(256,576) GEMM per head
+            # codes written straight into the (B, 2) action rows (and move 1
+            # as int16 for the move-2 mask): no stack / dtype-cast kernels
             h1, h2 = self.model.move1_head, self.model.move2_head
-            a1 = head_policy_576(f, h1.weight, h1.bias, self.env.legal_mask(), self.eps_t, self.seed, self.tag_t, 0)
-            m2 = self.env.legal_mask_move2(a1.to(torch.int16))
-            a2 = head_policy_576(f, h2.weight, h2.bias, m2, self.eps_t, self.seed, self.tag_t, 1, move1=a1)
-            return torch.stack([a1, a2], 1)
+            acts = torch.empty((x.shape[0], 2), dtype=torch.int64, device=self.dev)
+            m1 = torch.empty(x.shape[0], dtype=torch.int16, device=self.dev)
+            head_policy_576(f, h1.weight, h1.bias, self.env.legal_mask(), self.eps_t, self.seed, self.tag_t, 0,
+                            out=acts[:, 0], out16=m1)
+            m2 = self.env.legal_mask_move2(m1)
+            head_policy_576(f, h2.weight, h2.bias, m2, self.eps_t, self.seed, self.tag_t, 1, out=acts[:, 1],
+                            move1=acts[:, 0])
+            return acts
         a1 = policy_576(self.model.move1_head(f), self.env.legal_mask(), self.eps_t, self.seed,
                         self.tag_t, 0)
         m2 = self.env.legal_mask_move2(a1.to(torch.int16))

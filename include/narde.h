@@ -265,11 +265,15 @@ int narde_policy_masked_argmax576_dev(int device, const float *q, int64_t ldq, c
  * narde_policy_masked_argmax576_dev).  f f32[B][ldf] (feat = 256), w
  * f32[576][ldw], rows 16-B aligned.  The fp32 sums round differently from a
  * dense GEMM's; a greedy pick can differ only between codes whose Q-values
- * tie to rounding. */
+ * tie to rounding.  The codes go to out[row * ld_out] (i64) and, if out16 is
+ * given, out16[row * ld_out16] (i16): straight into a column of the (B, 2)
+ * action rows; add_row is read as add_row[row * ld_row]. */
 int narde_head_policy576_dev(int device, const float *f, int64_t ldf, int64_t feat, const float *w,
                              int64_t ldw, const float *bias, const uint64_t *mask, int64_t n,
                              const float *epsilon, uint64_t seed, const int64_t *tag, int head,
-                             const float *addcol, const int64_t *add_row, int64_t *out, void *stream);
+                             const float *addcol, const int64_t *add_row, int64_t ld_row,
+                             int64_t *out, int64_t ld_out, int16_t *out16, int64_t ld_out16,
+                             void *stream);
 
 /* One DQN transition for all B envs, fused (the batched trainer of
  * gym_narde/dqn.py, config 4; reward shaping as train_deepq_pytorch.py:

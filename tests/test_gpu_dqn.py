@@ -614,3 +614,33 @@ def test_per_sample_search_exact_on_given_cdf(n):
     assert torch.allclose(w, x / x.max(), rtol=2e-6, atol=0)
     assert int(scratch.abs().sum()) == 0 and int(ctr) == 1
     assert float(beta) == pytest.approx(0.401)
+
+
+def test_head_policy_strided_outputs_equal_contiguous():
+    """k_head_policy576 writing straight into the columns of (B, 2) action
+    rows (int64, stride 2), move 1 also as int16, and reading move 1 from
+    such a column: the same codes as the contiguous calls."""
+    from gym_narde.dqn import head_policy_576
+    from gym_narde.vector import VecNardeEnv
+
+    n = 4099
+    env = VecNardeEnv(n, device="cuda:0", seed=29)
+    env.selfplay(23)
+    g = torch.Generator(device="cuda:0").manual_seed(8)
+    f = torch.relu(torch.randn((n, 256), device="cuda:0", generator=g))
+    w1 = torch.randn((576, 256), device="cuda:0", generator=g) * 0.06
+    w2 = torch.randn((576, 256 + 576), device="cuda:0", generator=g) * 0.06
+    b1 = torch.randn(576, device="cuda:0", generator=g) * 0.1
+    b2 = torch.randn(576, device="cuda:0", generator=g) * 0.1
+    eps = torch.tensor(0.3, device="cuda:0")
+    tag = torch.tensor(9, dtype=torch.int64, device="cuda:0")
+    words = env.legal_mask()
+    a1 = head_policy_576(f, w1, b1, words, eps, 5, tag, 0)
+    m2 = env.legal_mask_move2(a1.to(torch.int16))
+    a2 = head_policy_576(f, w2, b2, m2, eps, 5, tag, 1, move1=a1)
+    acts = torch.full((n, 2), -7, dtype=torch.int64, device="cuda:0")
+    m1 = torch.empty(n, dtype=torch.int16, device="cuda:0")
+    head_policy_576(f, w1, b1, words, eps, 5, tag, 0, out=acts[:, 0], out16=m1)
+    head_policy_576(f, w2, b2, env.legal_mask_move2(m1), eps, 5, tag, 1, out=acts[:, 1], move1=acts[:, 0])
+    assert torch.equal(acts[:, 0], a1) and torch.equal(acts[:, 1], a2)
+    assert torch.equal(m1.to(torch.int64), a1)
