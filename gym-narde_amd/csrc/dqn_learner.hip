@@ -530,7 +530,9 @@ __global__ void __launch_bounds__(kLearnThreads) k_prio_update(const int64_t* __
                                                                float eps, float* __restrict__ prio,
                                                                float* __restrict__ max_prio,
                                                                float* __restrict__ epsilon, float eps_min,
-                                                               float eps_decay) {
+                                                               float eps_decay, int64_t* __restrict__ cursor,
+                                                               int64_t cursor_add, int64_t cursor_mod,
+                                                               int64_t* __restrict__ tag) {
   __shared__ float red[kLearnThreads / 64];
   float m = -__builtin_inff();
   for (int j = threadIdx.x; j < batch; j += kLearnThreads) {
@@ -545,6 +547,9 @@ __global__ void __launch_bounds__(kLearnThreads) k_prio_update(const int64_t* __
       const float e = *epsilon;
       *epsilon = e > eps_min ? e * eps_decay : e;
     }
+    // the driver's step bookkeeping, folded in (two torch launches fewer)
+    if (cursor) *cursor = (*cursor + cursor_add) % cursor_mod;
+    if (tag) *tag += 1;
   }
 }
 
@@ -740,12 +745,15 @@ int narde_dqn_loss(int device, const float* q1, const float* q2, const float* m1
 }
 
 int narde_prio_update(int device, const int64_t* idx, const float* td, int64_t batch, float eps, float* prio,
-                      float* max_prio, float* epsilon, float eps_min, float eps_decay, void* stream) {
+                      float* max_prio, float* epsilon, float eps_min, float eps_decay, int64_t* cursor,
+                      int64_t cursor_add, int64_t cursor_mod, int64_t* tag, void* stream) {
   if (!idx || !td || !prio || !max_prio) return bad("NULL argument");
   if (batch <= 0 || batch > (int64_t(1) << 24)) return bad("bad batch");
+  if (cursor && (cursor_mod <= 0 || cursor_add < 0)) return bad("bad cursor step");
   DeviceGuard dg(device);
   k_prio_update<<<1, kLearnThreads, 0, (hipStream_t)stream>>>(idx, td, (int)batch, eps, prio, max_prio, epsilon,
-                                                              eps_min, eps_decay);
+                                                              eps_min, eps_decay, cursor, cursor_add, cursor_mod,
+                                                              tag);
   return check_launch("k_prio_update");
 }
 

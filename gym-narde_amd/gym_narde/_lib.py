@@ -75,7 +75,7 @@ SIGNATURES = {
     "narde_dqn_loss": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, ctypes.c_float, _vp, _vp, _vp,
                               _vp, _vp, _vp]),
     "narde_prio_update": (_i32, [_i32, _vp, _vp, _i64, ctypes.c_float, _vp, _vp, _vp, ctypes.c_float,
-                                 ctypes.c_float, _vp]),
+                                 ctypes.c_float, _vp, _i64, _i64, _vp, _vp]),
     "narde_adam_clip": (_i32, [_i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_float, ctypes.c_float,
                                ctypes.c_float, ctypes.c_float, ctypes.c_float, _vp, _vp]),
     "narde_violates_block_rule": (_i32, [_i32, _vp, _i64, _vp, _vp]),

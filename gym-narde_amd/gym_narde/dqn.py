@@ -328,7 +328,10 @@ class DQNLoss(torch.autograd.Function):
     `td`; the saved dloss/dq1, dloss/dq2 make the backward one multiply."""
 
     @staticmethod
-    def forward(ctx, q1, q2, m1, m2, r, d, w, gamma, td, loss_copy):
+    def compute(q1, q2, m1, m2, r, d, w, gamma, td, loss_copy):
+        """(loss, dloss/dq1, dloss/dq2) without autograd: the learner hands
+        the gradients to torch.autograd.backward((q1, q2), (g1, g2)) itself
+        (the backward's `go * g` multiplies are two launches for go = 1)."""
         B = q1.shape[0]
         loss = torch.empty((), dtype=torch.float32, device=q1.device)
         g1, g2 = torch.empty_like(q1), torch.empty_like(q2)
@@ -336,6 +339,11 @@ class DQNLoss(torch.autograd.Function):
             q1.device.index, _f32(q1), _f32(q2), _f32(m1), _f32(m2), _f32(r), _f32(d), _f32(w), B,
             float(gamma), _f32(td), _lib.ptr(loss), None if loss_copy is None else _f32(loss_copy),
             _lib.ptr(g1), _lib.ptr(g2), _stream(q1.device)), "narde_dqn_loss")
+        return loss, g1, g2
+
+    @staticmethod
+    def forward(ctx, q1, q2, m1, m2, r, d, w, gamma, td, loss_copy):
+        loss, g1, g2 = DQNLoss.compute(q1, q2, m1, m2, r, d, w, gamma, td, loss_copy)
         ctx.save_for_backward(g1, g2)
         return loss
 
@@ -522,13 +530,16 @@ class DeviceReplay:
             _lib.ptr(a), _lib.ptr(r), _lib.ptr(d), _stream(self.obs.device)), "narde_gather_batch")
         return s, ns, a, r, d
 
-    def update_fused(self, idx, td, epsilon=None, eps_min=0.0, eps_decay=1.0):
+    def update_fused(self, idx, td, epsilon=None, eps_min=0.0, eps_decay=1.0, cursor_add=0, tag=None):
         """update() as k_prio_update (+ the driver's epsilon decay when an
-        epsilon device scalar is given)."""
+        epsilon device scalar is given; + the write cursor's advance by
+        cursor_add rows and the driver's step tag + 1, when given -- the
+        step's bookkeeping folded into this launch)."""
         _lib.check(_lib.load().narde_prio_update(
             idx.device.index, _lib.ptr(idx), _f32(td), idx.shape[0], float(self.epsilon), _lib.ptr(self.prio),
             _lib.ptr(self.max_prio), None if epsilon is None else _lib.ptr(epsilon), float(eps_min),
-            float(eps_decay), _stream(idx.device)), "narde_prio_update")
+            float(eps_decay), _lib.ptr(self.pos_t) if cursor_add else None, int(cursor_add), self.capacity,
+            _lib.ptr(tag), _stream(idx.device)), "narde_prio_update")
 
 
 class BatchedDQNDriver:
@@ -597,6 +608,7 @@ class BatchedDQNDriver:
         self.last_loss = None
         self.graph = None
         self._capturing = False
+        self._fold = None  # (cursor rows, tag) the next fused update advances
 
     @property
     def epsilon(self):
@@ -671,11 +683,20 @@ class BatchedDQNDriver:
         x = self.state
         actions = self.act(x)
         _, reward, term, trunc, info = self.env.step(actions.to(torch.int16))
+        # when the fused learner runs this step, the ring cursor's advance and
+        # the step tag's increment ride in its last kernel (k_prio_update)
+        n, rp = self.env.num_envs, self.replay
         if self.fused:
-            self._transition_fused(actions, reward, term, trunc, info["legal"])
+            self._transition_fused(actions, reward, term, trunc, info["legal"], advance_cursor=False)
         else:
             self._transition_torch(actions, reward, term, trunc, info["legal"])
-        self.tag_t.add_(1)
+        fold = self.fused_learner and self.updates_per_step >= 1 and rp.size >= self.train_batch
+        if fold:
+            self._fold = (n if self.fused else 0, self.tag_t)
+        else:
+            if self.fused:
+                rp.pos_t.add_(n).remainder_(rp.capacity)
+            self.tag_t.add_(1)
         loss = None
         for _ in range(self.updates_per_step):
             loss = self._update_body()
@@ -712,7 +733,7 @@ class BatchedDQNDriver:
         self.replay.add(actions, r, nxt, done)
         self.state.copy_(nxt)
 
-    def _transition_fused(self, actions, reward, term, trunc, legal):
+    def _transition_fused(self, actions, reward, term, trunc, legal, advance_cursor=True):
         rp, n = self.replay, self.env.num_envs
         if not (self.state.is_contiguous() and actions.is_contiguous() and actions.dtype == torch.int64):
             raise ValueError("state / actions layout")
@@ -722,7 +743,8 @@ class BatchedDQNDriver:
             int(self.shaping), _lib.ptr(rp.obs), _lib.ptr(rp.action), _lib.ptr(rp.reward), _lib.ptr(rp.done),
             _lib.ptr(rp.prio), _lib.ptr(rp.max_prio), _lib.ptr(rp.pos_t), rp.capacity,
             ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream))
-        rp.pos_t.add_(n).remainder_(rp.capacity)
+        if advance_cursor:
+            rp.pos_t.add_(n).remainder_(rp.capacity)
         rp.advance(n)
 
     def _host_after_step(self, trained):
@@ -805,11 +827,13 @@ class BatchedDQNDriver:
             base2 = torch.nn.functional.linear(tf, wt[:, :256], self.target.move2_head.bias)
             m2 = rowmax_addend(base2, wt[:, 256:].t().contiguous(), am1)
         td = torch.empty_like(r)
-        loss = DQNLoss.apply(q1, q2, m1, m2, r, d, w, self.gamma, td, self.loss_t)
+        _, g1, g2 = DQNLoss.compute(q1.detach(), q2.detach(), m1, m2, r, d, w, self.gamma, td, self.loss_t)
         self.fopt.zero_grad(set_to_none=True)
-        loss.backward()
+        torch.autograd.backward((q1, q2), (g1, g2))  # = loss.backward(): dloss/dq from k_dqn_loss
         self.fopt.step()  # clip_grad_norm_(10) + Adam
-        rp.update_fused(idx, td, self.eps_t, self.epsilon_min, self.epsilon_decay)
+        cursor_add, tag = self._fold if self._fold is not None else (0, None)
+        self._fold = None
+        rp.update_fused(idx, td, self.eps_t, self.epsilon_min, self.epsilon_decay, cursor_add=cursor_add, tag=tag)
         if self._capturing:
             return self.loss_t
         self._after_update()

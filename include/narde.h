@@ -376,10 +376,14 @@ int narde_dqn_loss(int device, const float *q1, const float *q2, const float *m1
                    float *td, float *loss, float *loss_copy, float *g1, float *g2, void *stream);
 
 /* prio[idx_j] = td_j + eps; *max_prio = max(*max_prio, max_j); then, if
- * epsilon is non-NULL, *epsilon *= eps_decay when *epsilon > eps_min. */
+ * epsilon is non-NULL, *epsilon *= eps_decay when *epsilon > eps_min; if
+ * cursor is non-NULL, *cursor = (*cursor + cursor_add) % cursor_mod (the
+ * replay ring's write cursor); if tag is non-NULL, *tag += 1 (the driver's
+ * step tag) -- device scalars a step's bookkeeping advances. */
 int narde_prio_update(int device, const int64_t *idx, const float *td, int64_t batch, float eps,
                       float *prio, float *max_prio, float *epsilon, float eps_min,
-                      float eps_decay, void *stream);
+                      float eps_decay, int64_t *cursor, int64_t cursor_add, int64_t cursor_mod,
+                      int64_t *tag, void *stream);
 
 /* torch.nn.utils.clip_grad_norm_(max_norm) + one torch.optim.Adam step
  * (train_deepq_pytorch.py's optimizer) over n_tensors <= 8 fp32 parameter

@@ -78,7 +78,7 @@ def test_argument_errors_are_einval_before_any_device_call():
         ("narde_dqn_heads_backward", (0, N, N, N, 256, N, 256, N, 832, N, 64, N, N, N, N, N, N)),
         ("narde_relu_bias_grad", (0, N, N, 64, 256, N, N, N, N)),
         ("narde_dqn_loss", (0, N, N, N, N, N, N, N, 64, 0.99, N, N, N, N, N, N)),
-        ("narde_prio_update", (0, N, N, 64, 0.01, N, N, N, 0.01, 0.995, N)),
+        ("narde_prio_update", (0, N, N, 64, 0.01, N, N, N, 0.01, 0.995, N, 0, 1, N, N)),
         ("narde_adam_clip", (0, 0, N, N, N, N, N, N, 1e-3, 0.9, 0.999, 1e-8, 10.0, N, N)),
     ]
     for name, args in cases:
