@@ -609,6 +609,7 @@ class BatchedDQNDriver:
         self.graph = None
         self._capturing = False
         self._fold = None  # (cursor rows, tag) the next fused update advances
+        self._wm_rows, self._wm_ver = None, -1  # _target_onehot_rows' cache
 
     @property
     def epsilon(self):
@@ -825,7 +826,7 @@ class BatchedDQNDriver:
             m1, am1 = self.target.move1_head(tf).max(1)
             wt = self.target.move2_head.weight
             base2 = torch.nn.functional.linear(tf, wt[:, :256], self.target.move2_head.bias)
-            m2 = rowmax_addend(base2, wt[:, 256:].t().contiguous(), am1)
+            m2 = rowmax_addend(base2, self._target_onehot_rows(), am1)
         td = torch.empty_like(r)
         _, g1, g2 = DQNLoss.compute(q1.detach(), q2.detach(), m1, m2, r, d, w, self.gamma, td, self.loss_t)
         self.fopt.zero_grad(set_to_none=True)
@@ -871,7 +872,23 @@ class BatchedDQNDriver:
         self._after_update()
         return self.loss_t
 
+    def _target_onehot_rows(self):
+        """The target move-2 head's one-hot columns as rows (576, 576),
+        cached: the target changes only at its sync (refreshed in place
+        there, outside any captured graph), so the step does not copy 1.3 MB
+        per update; a stale cache (weights changed in place elsewhere) is
+        caught by the tensor's version counter."""
+        wt = self.target.move2_head.weight
+        if self._wm_rows is None or self._wm_ver != wt._version:
+            self._wm_rows = wt[:, 256:].t().contiguous()
+            self._wm_ver = wt._version
+        return self._wm_rows
+
     def _after_update(self):
         self.train_steps += 1
         if self.train_steps % self.target_update == 0:
             self.target.load_state_dict(self.model.state_dict())
+            if self._wm_rows is not None:  # in place: a captured graph holds its address
+                wt = self.target.move2_head.weight
+                self._wm_rows.copy_(wt[:, 256:].t())
+                self._wm_ver = wt._version

@@ -644,3 +644,31 @@ def test_head_policy_strided_outputs_equal_contiguous():
     head_policy_576(f, w2, b2, env.legal_mask_move2(m1), eps, 5, tag, 1, out=acts[:, 1], move1=acts[:, 0])
     assert torch.equal(acts[:, 0], a1) and torch.equal(acts[:, 1], a2)
     assert torch.equal(m1.to(torch.int64), a1)
+
+
+def test_target_onehot_rows_cache_follows_target_syncs():
+    """The learner's cached (576, 576) one-hot rows of the target move-2 head
+    equal the target's weights after every sync, eagerly and across graph
+    replays (refreshed in place outside the graph)."""
+    from gym_narde.dqn import BatchedDQNDriver
+    from gym_narde.vector import VecNardeEnv
+
+    env = VecNardeEnv(2048, device="cuda:0", seed=17)
+    drv = BatchedDQNDriver(env, capacity=1 << 13, train_batch=512, seed=4, target_update=2)
+
+    def fresh():
+        return drv.target.move2_head.weight[:, 256:].t()
+
+    for _ in range(8):
+        drv.step()
+    torch.cuda.synchronize()
+    assert drv._wm_rows is not None and torch.equal(drv._target_onehot_rows(), fresh())
+    drv.capture_graph(warmup=2)
+    syncs = 0
+    for _ in range(6):
+        before = drv.train_steps
+        drv.step()
+        syncs += (drv.train_steps // 2) - (before // 2)
+    torch.cuda.synchronize()
+    assert syncs >= 2
+    assert torch.equal(drv._wm_rows, fresh())
