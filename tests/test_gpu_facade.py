@@ -241,3 +241,22 @@ def test_get_valid_plays_vs_reference_lists():
     # the start: one checker may leave the head, the higher die first
     # (narde.py:94-137), so list #1 holds one move and the step plays it alone
     assert env.get_valid_actions([6, 1]) == {((23, 17),)}
+
+
+@pytest.mark.parametrize("n", [1, 37, 64, 65, 4099])
+def test_totals_rows_equal_stats(n):
+    """VecNardeEnv.totals() (narde_get_totals: 64 partial rows over
+    contiguous env ranges) sums to stats(), for batches smaller than, equal
+    to and just above the row count (rows past the last env are zero)."""
+    from gym_narde.vector import VecNardeEnv
+
+    env = VecNardeEnv(n, device="cuda:0", seed=n)
+    env.selfplay(300)
+    rows = env.totals()
+    st = env.stats().to(torch.int64)
+    assert rows.shape == (64, 3) and rows.dtype == torch.int64
+    assert torch.equal(rows.sum(0), st.sum(0))
+    per = -(-n // 64)
+    for b in range(64):
+        assert torch.equal(rows[b], st[b * per:min(n, (b + 1) * per)].sum(0)), b
+    env.close()
