@@ -7,15 +7,24 @@
 // kernel boundary costs ~4.5 us on MI355X even inside a CUDA graph).  These
 // kernels fold the chains that are not GEMMs:
 //   k_per_sample       prioritized sampling (PrioritizedReplayBuffer.sample,
-//                      :279-342): inverse-CDF search, importance weights,
-//                      beta annealing -- one block;
+//   + k_per_finish     :279-342): a 64-ary inverse-CDF search per wave,
+//                      importance weights, then their normalisation and the
+//                      beta / counter step in one block;
 //   k_gather_batch     the minibatch rows of the replay ring;
+//   k_heads_gather     the online heads at the stored codes only (what the
+//   + k_heads_grad_f   loss reads) and their backward: per-row dot products,
+//   + k_heads_grad_w   per-code gradient sums in a fixed order;
+//   k_relu_grad_partial  a feature layer's ReLU mask + bias gradient (column
+//   + k_bias_grad_sum    sums of 64-row blocks, then the blocks in order);
 //   k_rowmax_addend    the target move-2 head's max over codes with the
 //                      one-hot column added on the fly;
 //   k_dqn_loss         targets, TD errors, the decomposed loss (:653-720) and
 //                      its gradient w.r.t. the two Q-values -- one block;
-//   k_prio_update      new priorities |td| + eps, the running max priority and
-//                      the per-update epsilon decay (:745-746) -- one block.
+//   k_prio_update      new priorities |td| + eps, the running max priority,
+//                      the per-update epsilon decay (:745-746) and the
+//                      step's cursor / tag advance -- one block;
+//   k_grad_sqnorm      clip_grad_norm_ + Adam: per-block squared-norm
+//   + k_adam           partials, then every block adds them in order.
 // Every scalar the driver updates per step (sampling counter, beta, max
 // priority, epsilon) lives in device memory, so a captured graph replays
 // with current values.  fp32 throughout, the same operation order as the
