@@ -91,7 +91,8 @@ __global__ void __launch_bounds__(kBlock) k_tesauro198(Planes pl, int n, float* 
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int c = c0 + q;
-    nv[q] = c < 198 ? tes_value(a0, b0, c) : tes_value(a1, b1, c - 198);
+    const bool nx = c >= 198;  // the record first, then one evaluation (not both)
+    nv[q] = tes_value(nx ? a1 : a0, nx ? b1 : b0, nx ? c - 198 : c);
   }
   if (e0 + 4u <= total) {
     *reinterpret_cast<float4*>(tes + e0) = make_float4(nv[0], nv[1], nv[2], nv[3]);
@@ -184,7 +185,8 @@ __global__ void __launch_bounds__(kBlock) k_dqn_transition(TransArgs t, int obs_
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int c = c0 + q;
-    nv[q] = c < 198 ? tes_value(a0, b0, c) : tes_value(a1, b1, c - 198);
+    const bool nx = c >= 198;  // the record first, then one evaluation (not both)
+    nv[q] = tes_value(nx ? a1 : a0, nx ? b1 : b0, nx ? c - 198 : c);
   }
   if (vec) {
     typedef float v4f __attribute__((ext_vector_type(4)));
