@@ -96,7 +96,8 @@ __device__ __forceinline__ float block_sum(float v, float* lds) {
 // ---------------------------------------------------------------- sampling
 // batch draws u_j = Philox4x32-10({*counter, j, 0, 7}, seed) r0 / 2^32 (24
 // significant bits, as torch.rand), v_j = u_j * total; idx_j = the first k
-// with cdf[k] > v_j (torch.searchsorted(right=True)), clamped to n - 1;
+// with cdf[k] > v_j (torch.searchsorted(right=True)), clamped to n - 1, and
+// moved to the nearest row with p > 0 if p[k] == 0 (nearest_positive);
 // w_j = (n * p[idx] / total)^-beta normalised by the batch max.  Then beta
 // <- min(1, beta + beta_inc) and *counter += 1.
 // One WAVE per sample (4 per block): a 64-ary search -- each round the 64
@@ -111,6 +112,23 @@ __device__ __forceinline__ float block_sum(float v, float* lds) {
 // max meeting in one word by atomicMax: 17.2 + 4.5 us -- 1,024 atomics on
 // one address serialise.)
 constexpr int kSampleWaves = 4;
+
+// the last row before k with p > 0, else the first one after k, else k
+// (all rows zero: the caller never samples then); wave-uniform, lane l
+// looks at row k - 1 - l (k + 1 + l) each round
+__device__ __noinline__ int64_t nearest_positive(const float* __restrict__ p, int64_t n, int64_t k, int lane) {
+  for (int64_t hi = k - 1; hi >= 0; hi -= 64) {
+    const int64_t r = hi - lane;
+    const uint64_t hit = __ballot(r >= 0 && p[r] > 0.0f);
+    if (hit) return hi - (int64_t)__builtin_ctzll(hit);
+  }
+  for (int64_t lo = k + 1; lo < n; lo += 64) {
+    const int64_t r = lo + lane;
+    const uint64_t hit = __ballot(r < n && p[r] > 0.0f);
+    if (hit) return lo + (int64_t)__builtin_ctzll(hit);
+  }
+  return k;
+}
 
 __global__ void __launch_bounds__(64 * kSampleWaves) k_per_sample(const float* __restrict__ p,
                                                                   const float* __restrict__ cdf, int64_t n,
@@ -149,7 +167,14 @@ __global__ void __launch_bounds__(64 * kSampleWaves) k_per_sample(const float* _
       split = true;
     }
     if (len == 1 && !split && !(cdf[lo] > v)) lo += 1;  // n == 1: the range was never split
-    const int64_t k = lo < n - 1 ? lo : n - 1;
+    int64_t k = lo < n - 1 ? lo : n - 1;
+    // never a zero-priority (pending) row: the clamp above (u * total
+    // rounded up to total) or a prefix sum whose flat run steps by an ulp
+    // (a scan's association differs across tiles) can land on one, and its
+    // weight (n * 0)^-beta = inf would turn the batch's weights into NaN.
+    // Take the last row before k with p > 0 (64 rows per round; the first
+    // one after k if there is none), as DeviceReplay.sample() does.
+    if (!(p[k] > 0.0f)) k = nearest_positive(p, n, k, lane);
     const float x = powf((float)n * (p[k] / total), -(float)*beta);
     if (lane == 0) {
       idx_out[j] = k;
@@ -220,7 +245,8 @@ __global__ void __launch_bounds__(256) k_rowmax_addend(const float* __restrict__
   const int i = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
   if (i >= n) return;
   const float* br = base + (size_t)i * (size_t)ld;
-  const float* tr = tab + (size_t)rows[i] * (size_t)ld_tab;
+  const int64_t ri = rows[i] < 0 ? 0 : (rows[i] > 575 ? 575 : rows[i]);  // a move-1 code: one table row each
+  const float* tr = tab + (size_t)ri * (size_t)ld_tab;
   float m = -__builtin_inff();
 #pragma unroll
   for (int j = 0; j < 9; ++j) m = fmaxf(m, br[64 * j + lane] + tr[64 * j + lane]);

@@ -290,6 +290,21 @@ __global__ void __launch_bounds__(kBlock) k_mask576_move2(Planes pl, int n, Rng 
 // reference's "no move" code, :504-505).  Draws: Philox4x32-10({tag, row, 0,
 // 5}, seed): r0 < epsilon * 2^32 explores, one shared decision for both
 // heads of a step (same tag); the pick is mulhi(r1 or r2 by head, count).
+// a move-1 code used as an index (the one-hot column / table row), kept in
+// [0, 576) whatever the caller's buffer holds
+__device__ __forceinline__ int64_t clamp_code(int64_t c) { return c < 0 ? 0 : (c > 575 ? 575 : c); }
+
+// torch.argmax's order for (value, code) candidates: a NaN beats every
+// number (the lowest code among NaNs), else the larger value, the lower
+// code on ties; oi < 0 is "no candidate"
+__device__ __forceinline__ bool argmax_takes(float ov, int oi, float best, int bi) {
+  if (oi < 0) return false;
+  if (bi < 0) return true;
+  const bool on = __builtin_isnan(ov), bn = __builtin_isnan(best);
+  if (on || bn) return on && (!bn || oi < bi);
+  return ov > best || (ov == best && oi < bi);
+}
+
 __host__ __device__ inline uint64_t eps_to_q32(float epsilon) {
   const double e = epsilon <= 0.0f ? 0.0 : (epsilon >= 1.0f ? 1.0 : (double)epsilon);
   return (uint64_t)(e * 4294967296.0);
@@ -348,9 +363,10 @@ __global__ void __launch_bounds__(256) k_head_policy576(const float* __restrict_
     }
   } else if (cnt > 0) {
     const float4 fv = reinterpret_cast<const float4*>(f + (size_t)row * (size_t)ldf)[lane];
-    const int64_t ar = addcol ? add_row[(size_t)row * (size_t)ld_row] : 0;
-    float best = -__builtin_inff();
-    int bi = 0x7FFFFFFF;
+    // the one-hot column's index is a move-1 code: kept inside [0, 576)
+    const int64_t ar = addcol ? clamp_code(add_row[(size_t)row * (size_t)ld_row]) : 0;
+    float best = 0.0f;
+    int bi = -1;  // cnt > 0: the first legal code always takes it
     for (int j = 0; j < 9; ++j) {
       uint64_t m = mw[j];
       while (m) {  // the legal codes of this word, ascending (wave-uniform)
@@ -362,7 +378,9 @@ __global__ void __launch_bounds__(256) k_head_policy576(const float* __restrict_
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
         v += bias[c];
         if (addcol) v += addcol[(size_t)c * (size_t)ldw + ar];
-        if (v > best) { best = v; bi = c; }  // ascending codes: the first maximum is kept
+        // ascending codes: the first maximum is kept, a NaN beats every
+        // number and the first NaN is kept (torch.argmax's rule)
+        if (bi < 0 || v > best || (__builtin_isnan(v) && !__builtin_isnan(best))) { best = v; bi = c; }
       }
     }
     code = bi;
@@ -413,23 +431,25 @@ __global__ void __launch_bounds__(256) k_policy576(const float* __restrict__ q, 
     const float* qr = q + (size_t)row * (size_t)ldq;
     // optional addend row (the move-2 head's one-hot column, DecomposedDQN):
     // v = q[row][c] + add_tab[add_row[row]][c], the same single fp32 add
-    const float* ar = add_tab ? add_tab + (size_t)add_row[row] * (size_t)ld_add : nullptr;
-    float best = -__builtin_inff();
-    int bi = 0x7FFFFFFF;
+    // (the table has one row per move-1 code: the row index kept in [0, 576))
+    const float* ar = add_tab ? add_tab + (size_t)clamp_code(add_row[row]) * (size_t)ld_add : nullptr;
+    float best = 0.0f;
+    int bi = -1;  // -1: no legal code in this lane
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
       if ((mw[j] >> lane) & 1ull) {
         const float v = ar ? qr[64 * j + lane] + ar[64 * j + lane] : qr[64 * j + lane];
-        if (v > best) { best = v; bi = 64 * j + lane; }  // j ascending: first max kept
+        // j ascending: the first maximum kept; a NaN beats every number
+        if (bi < 0 || v > best || (__builtin_isnan(v) && !__builtin_isnan(best))) { best = v; bi = 64 * j + lane; }
       }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       const float ov = __shfl_xor(best, o, 64);
       const int oi = __shfl_xor(bi, o, 64);
-      if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+      if (argmax_takes(ov, oi, best, bi)) { best = ov; bi = oi; }
     }
-    code = bi;
+    code = bi;  // cnt > 0: some lane held a legal code
   }
   if (lane == 0) out[row] = code;
 }

@@ -86,6 +86,26 @@ def expand_mask(mask576):
     return bits.view(mask576.shape[0], MOVES).bool()
 
 
+def nearest_positive(p, idx):
+    """A sampled row never has priority 0 (a pending row: its weight would be
+    inf and the batch's weights NaN): where p[idx] == 0 take the last row
+    before idx with p > 0, else the first one after it -- k_per_sample's
+    rule.  Only a rounded-up u * total (the clamp to n - 1) or a prefix sum
+    whose flat run steps by an ulp can pick such a row."""
+    bad = ~(p[idx] > 0)  # (no host-side early exit: graph-capturable)
+    n = p.shape[0]
+    ar = torch.arange(n, device=p.device)
+    pos = p > 0
+    last = torch.where(pos, ar, torch.full_like(ar, -1)).cummax(0).values  # last positive <= i
+    nxt = torch.where(pos, ar, torch.full_like(ar, n)).flip(0).cummin(0).values.flip(0)  # first >= i
+    before = last[(idx - 1).clamp(min=0)]
+    before = torch.where(idx > 0, before, torch.full_like(before, -1))
+    after = nxt[(idx + 1).clamp(max=n - 1)]
+    after = torch.where(idx < n - 1, after, torch.full_like(after, n))
+    fix = torch.where(before >= 0, before, torch.where(after < n, after, idx))
+    return torch.where(bad, fix, idx)
+
+
 def masked_argmax(scores, mask):
     """argmax over legal entries; 0 where nothing is legal (the reference's
     'no move' code, train_deepq_pytorch.py:504-505).  Torch reference of
@@ -101,8 +121,10 @@ def policy_576(q, mask576, epsilon, seed, tag, head, out=None, add=None):
     intermediates.  Same tag for both heads of a step = one shared explore
     decision per env.  epsilon / tag may be Python numbers or device scalars
     (f32 / int64 0-d tensors, read by the kernel at run time: graph-safe).
-    add = (table (R,576) f32, rows (B,) int64): greedy values become
-    q[i] + table[rows[i]] (one fp32 add, fused)."""
+    add = (table (576,576) f32, rows (B,) int64): greedy values become
+    q[i] + table[rows[i]] (one fp32 add, fused).  Greedy picks follow
+    torch.argmax over the legal codes: the first maximum, a NaN Q-value
+    beating every number (the first NaN); a legal code is always returned."""
     q = q.contiguous()
     if q.dtype != torch.float32 or q.shape[1] != MOVES:
         raise ValueError("q must be (B, 576) float32")
@@ -117,8 +139,10 @@ def policy_576(q, mask576, epsilon, seed, tag, head, out=None, add=None):
         tab, rows, ld = None, None, 0
         if add is not None:
             tab, rows = add
-            if tab.dtype != torch.float32 or tab.dim() != 2 or tab.shape[1] != MOVES or tab.stride(1) != 1:
-                raise ValueError("add table must be (R, 576) float32 with unit column stride")
+            if (tab.dtype != torch.float32 or tab.dim() != 2 or tuple(tab.shape) != (MOVES, MOVES)
+                    or tab.stride(1) != 1):
+                raise ValueError("add table must be (576, 576) float32 with unit column stride "
+                                 "(one row per move-1 code; the kernel keeps row indices in 0..575)")
             rows = rows.to(torch.int64).contiguous()
             if rows.shape != (q.shape[0],):
                 raise ValueError("add rows must be (B,)")
@@ -485,7 +509,7 @@ class DeviceReplay:
         # inverse-CDF sampling (torch.multinomial over 1M categories spends
         # ~0.5 ms renormalising one huge row); pending rows have p = 0
         u = torch.rand(batch, device=p.device, generator=generator) * total
-        idx = torch.searchsorted(cdf, u, right=True).clamp_(max=n - 1)
+        idx = nearest_positive(p, torch.searchsorted(cdf, u, right=True).clamp_(max=n - 1))
         probs_idx = p[idx] / total
         w = (n * probs_idx) ** (-self.beta_t)
         w = w / w.max()

@@ -361,6 +361,24 @@ class VecNardeEnv:
         self.handle.call("narde_get_totals", _lib.ptr(out), self._s())
         return out
 
+    def totals_launcher(self, out):
+        """totals(out) pre-bound: a zero-argument callable making exactly one
+        ctypes call (one launch on the stream current NOW); returns out."""
+        t = self.torch
+        if (tuple(out.shape) != (_lib.TOTAL_ROWS, 3) or out.dtype != t.int64 or out.device != self.device
+                or not out.is_contiguous()):
+            raise ValueError("out must be a contiguous (64,3) int64 tensor on the env's device")
+        fn, args = self.handle.lib.narde_get_totals, (self.handle.h, _lib.ptr(out), self._s())
+
+        def launch():
+            rc = fn(*args)
+            if rc:
+                _lib.check(rc, "narde_get_totals")
+            return out
+
+        launch.out = out
+        return launch
+
     def get_state(self):
         B, t, dev = self.num_envs, self.torch, self.device
         st = dict(board=t.empty((B, 24), dtype=t.int8, device=dev),

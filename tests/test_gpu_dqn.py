@@ -672,3 +672,101 @@ def test_target_onehot_rows_cache_follows_target_syncs():
     torch.cuda.synchronize()
     assert syncs >= 2
     assert torch.equal(drv._wm_rows, fresh())
+
+
+def test_policies_nan_rows_follow_torch_argmax():
+    """A diverging learner's NaN Q-values: both policy
+    kernels return a legal code per torch.argmax's rule over the legal codes
+    -- the first NaN if any, else the first maximum -- never a sentinel; a
+    move-1 code outside 0..575 as the one-hot column index is clamped (no
+    out-of-bounds read)."""
+    from gym_narde.dqn import expand_mask, head_policy_576, masked_argmax, policy_576
+    from gym_narde.vector import VecNardeEnv
+
+    n = 4096
+    env = VecNardeEnv(n, device="cuda:0", seed=29)
+    env.selfplay(41)
+    words = env.legal_mask()
+    m = expand_mask(words)
+    has = m.any(1)
+    g = torch.Generator(device="cuda:0").manual_seed(5)
+    f = torch.relu(torch.randn((n, 256), device="cuda:0", generator=g))
+    f[: n // 4] = float("nan")  # every code's Q is NaN
+    w1 = torch.randn((576, 256), device="cuda:0", generator=g) * 0.06
+    w1[300] = float("nan")  # one NaN code in every row (first NaN wins where legal)
+    b1 = torch.randn(576, device="cuda:0", generator=g) * 0.1
+    zero = torch.zeros((), device="cuda:0")
+    tag = torch.zeros((), dtype=torch.int64, device="cuda:0")
+    q = (f @ w1.t() + b1).contiguous()
+    want = masked_argmax(q, m)
+    # the dense policy kernel equals torch.argmax over the masked row exactly
+    got = policy_576(q, words, 0.0, seed=1, tag=0, head=0)
+    assert torch.equal(got, want)
+    # the fused heads: same rule (NaN rows are exact; finite rows within rounding)
+    a1 = head_policy_576(f, w1, b1, words, zero, 1, tag, 0)
+    nanrow = torch.isnan(q).logical_and(m).any(1)
+    assert torch.equal(a1[nanrow], want[nanrow])
+    rows = torch.arange(n, device="cuda:0")
+    assert bool(m[rows, a1][has].all()) and bool((a1[~has] == 0).all())
+    assert int(a1.min()) >= 0 and int(a1.max()) < 576
+    # move 2 with out-of-range move-1 codes (as a NaN-era sentinel would be)
+    w2 = torch.randn((576, 256 + 576), device="cuda:0", generator=g) * 0.06
+    b2 = torch.randn(576, device="cuda:0", generator=g) * 0.1
+    bogus = torch.full((n,), 2 ** 31 - 1, dtype=torch.int64, device="cuda:0")
+    bogus[::3] = -5
+    a2 = head_policy_576(f, w2, b2, words, zero, 1, tag, 1, move1=bogus)
+    assert bool(m[rows, a2][has].all())
+    tab = torch.randn((576, 576), device="cuda:0", generator=g)
+    a2d = policy_576(q, words, 0.0, seed=1, tag=0, head=1, add=(tab, bogus))
+    assert torch.equal(a2d, masked_argmax(q + tab[bogus.clamp(0, 575)], m))
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_sampler_never_returns_zero_priority_rows(fused):
+    """a prefix sum whose flat run (pending rows, p = 0)
+    steps up -- a scan's association differs across tiles -- or u * total
+    rounded up to total must not pick a zero-priority row, whose weight would
+    be inf and turn the batch's weights NaN.  A deliberately stepped cdf puts
+    a third of the mass on pending rows: every pick has p > 0, the weights
+    are finite, and the kernel's picks equal the torch rule
+    (nearest_positive) on the same uniforms."""
+    from gym_narde import _lib
+    from gym_narde.dqn import DeviceReplay, nearest_positive
+
+    n, B = 6000, 4096
+    p = torch.rand(n, device="cuda:0") + 0.05
+    p[2000:3000] = 0.0  # a pending run in the middle (a wrapped ring)
+    p[n - 500:] = 0.0  # ... and at the end (the fill phase)
+    p[:10] = 0.0  # ... and at the start
+    cdf = torch.cumsum(p, 0)
+    step = float(cdf[-1]) * 0.25
+    cdf[2500:3000] += step  # a flat run that steps up (mass on pending rows)
+    cdf[3000:] += step
+    cdf[n - 200:] += step  # ... and the tail past the last positive row
+    if fused:
+        import ctypes
+
+        idx = torch.empty(B, dtype=torch.int64, device="cuda:0")
+        w = torch.empty(B, device="cuda:0")
+        u = torch.empty(B, device="cuda:0")
+        ctr = torch.zeros((), dtype=torch.int64, device="cuda:0")
+        beta = torch.full((), 0.4, dtype=torch.float64, device="cuda:0")
+        scratch = torch.zeros(2, dtype=torch.int32, device="cuda:0")
+        st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        P = _lib.ptr
+        _lib.check(_lib.load().narde_per_sample(0, P(p), P(cdf), n, B, 3, P(ctr), P(beta), 0.001, P(idx), P(w),
+                                                P(u), P(scratch), st), "narde_per_sample")
+        torch.cuda.synchronize()
+        raw = torch.searchsorted(cdf, u * cdf[-1], right=True).clamp_(max=n - 1)
+        assert bool((p[raw] == 0).float().mean() > 0.2)  # the stepped runs were hit
+        assert torch.equal(idx, nearest_positive(p, raw))
+    else:
+        rp = DeviceReplay(n, 4, "cuda:0", stride=1)
+        rp.prio.copy_(p ** (1 / rp.alpha))
+        rp.size = n - 1  # rows = size + stride = n
+        idx, w = rp.sample(B)
+    assert bool((p[idx] > 0).all())
+    assert bool(torch.isfinite(w).all()) and float(w.max()) == pytest.approx(1.0)
+    # the rule itself: the last positive row before, else the first after
+    k = torch.tensor([2500, 5999, 0, 5, 10, 1999], device="cuda:0")
+    assert nearest_positive(p, k).tolist() == [1999, 5499, 10, 10, 10, 1999]

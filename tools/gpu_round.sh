@@ -2,9 +2,9 @@
 # One gpurun call's worth of evidence (run on the MI355X box from the repo root):
 #   gpurun --timeout 1100 -- bash tools/gpu_round.sh [tag]
 # GPU parity tests, smoke, the bench line, the rocprofv3 kernel-trace summary of
-# the same bench command (without the config-4 DQN leg, which is traced on its
-# own below: once, the default bench's DQN graph replay hit a GPU exception
-# under kernel tracing -- never without the profiler), and two separate PMC passes (FETCH_SIZE, WRITE_SIZE)
+# the same bench command (config-4 DQN leg included: the round-2 exception
+# under kernel tracing and its fixes are in DESIGN.md section 6; the DQN step
+# is also traced on its own below), and two separate PMC passes (FETCH_SIZE, WRITE_SIZE)
 # over k_rollout at the bench shape.  Every GPU step has its own time limit
 # and the steps are chained with && so the first failure ends the call.
 set -o pipefail
@@ -22,7 +22,7 @@ timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
   && timeout -k 10 300 python bench.py > "$OUT/bench_n1.json" 2> "$OUT/bench_n1.err" \
   && echo "[gpu_round] $(date +%T) rocprof kernel trace" \
   && (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
-        -d "$OUT/rocprof" -o bench -- python3 "$ROOT/bench.py" --no-cpu-baseline --dqn-steps 0 \
+        -d "$OUT/rocprof" -o bench -- python3 "$ROOT/bench.py" --no-cpu-baseline \
         > "$OUT/rocprof_bench.log" 2>&1) \
   && echo "[gpu_round] $(date +%T) pmc FETCH_SIZE" \
   && (cd /tmp && timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --output-format csv \
