@@ -310,6 +310,78 @@ __host__ __device__ inline uint64_t eps_to_q32(float epsilon) {
   return (uint64_t)(e * 4294967296.0);
 }
 
+// the roll of env i for the play-set kernels: given (roll order) or the
+// next step's device dice; false for a given die outside 1..6 (no play)
+__device__ __forceinline__ bool play_dice(const Side& s, const Rng& g, int i, const uint8_t* __restrict__ dice,
+                                          int& d0, int& d1) {
+  if (dice) {
+    d0 = dice[2 * i];
+    d1 = dice[2 * i + 1];
+  } else {
+    uint32_t r[4];
+    ply_draw(g, s.t, (uint32_t)i, r);
+    dice_from(r[0], g.dice_mode, d0, d1);
+  }
+  return (uint32_t)(d0 - 1) <= 5u && (uint32_t)(d1 - 1) <= 5u;
+}
+
+// The play set per env (narde_rules.h play_walk): list #1 compact, the word
+// of every list-#1 entry at table[i][k][p] (k = 0 the higher die's list, 1
+// the lower's; 0 where (k, p) is no entry) and the play count.  One lane
+// per env; the 192-B table row is zeroed, then the entries written.
+__global__ void __launch_bounds__(kBlock) k_play_set(Planes pl, int n, Rng g, const uint8_t* __restrict__ dice,
+                                                     int kind, uint64_t* __restrict__ legal,
+                                                     uint32_t* __restrict__ table, int32_t* __restrict__ count) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const Side s = side_from_record(pl.p0[i], pl.p1[i]);
+  uint32_t* row = table + (size_t)i * 48;
+  uint4* row4 = reinterpret_cast<uint4*>(row);
+#pragma unroll
+  for (int q = 0; q < 12; ++q) row4[q] = make_uint4(0u, 0u, 0u, 0u);
+  int d0, d1;
+  if (!play_dice(s, g, i, dice, d0, d1)) {
+    if (legal) legal[i] = 0ull;
+    count[i] = 0;
+    return;
+  }
+  Legal l;
+  legal2(s, d0, d1, l);
+  if (legal) legal[i] = compact_legal(l);
+  count[i] = play_walk(s, d0, d1, kind, l, [&](int k, int p, int, uint32_t w, bool) { row[k * 24 + p] = w; });
+}
+
+// The batched driver's exploration (train_deepq_pytorch.py:514-515:
+// np.random.rand() <= epsilon, then random.choice(valid_move_combinations)):
+// the rows whose shared explore draw (Philox4x32-10({tag, row, 0, 5}, seed)
+// r0 < epsilon * 2^32, the policy kernels' decision) takes the ε-branch
+// get play mulhi(r1, count) of act()'s combination list -- uniform over
+// (move 1, move 2) combinations, duplicates included -- as the two codes of
+// their (B, 2) action row; other rows are left as the heads wrote them.  A
+// row with no play keeps the heads' 0.
+__global__ void __launch_bounds__(kBlock) k_explore_plays(Planes pl, int n, Rng g,
+                                                          const uint8_t* __restrict__ dice,
+                                                          const float* __restrict__ eps_p,
+                                                          const int64_t* __restrict__ tag_p, uint32_t k0,
+                                                          uint32_t k1, int64_t* __restrict__ out, int64_t ld_out) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  uint32_t r[4];
+  philox4x32_10((uint32_t)*tag_p, (uint32_t)i, 0u, 5u, k0, k1, r);
+  if (!((uint64_t)r[0] < eps_to_q32(*eps_p))) return;
+  const Side s = side_from_record(pl.p0[i], pl.p1[i]);
+  int d0, d1;
+  if (!play_dice(s, g, i, dice, d0, d1)) return;
+  Legal l;
+  legal2(s, d0, d1, l);
+  const int cnt = play_walk(s, d0, d1, kPlayAct, l, [](int, int, int, uint32_t, bool) {});
+  if (cnt == 0) return;
+  int c1, c2;
+  play_codes_act(s, d0, d1, l, (int)mulhi_u32(r[1], (uint32_t)cnt), c1, c2);
+  out[(size_t)i * (size_t)ld_out] = c1;
+  out[(size_t)i * (size_t)ld_out + 1] = c2;
+}
+
 // k_head_policy576: k_policy576 with the head's Q-values computed in the
 // kernel, only for the legal codes: q_c = sum_k f[k] W[c][k] + b[c]
 // (+ addcol[c * ld_w + add_row[row]]: the move-2 head's one-hot column), the

@@ -506,6 +506,27 @@ int narde_legal_mask576_move2(narde_env* e, const int16_t* move1, const uint8_t*
   return check_launch("k_mask576_move2");
 }
 
+int narde_play_set(narde_env* e, const uint8_t* dice, int kind, uint64_t* legal, uint32_t* table, int32_t* count,
+                   void* stream) {
+  if (!e || !table || !count) return fail(NARDE_EINVAL, "NULL argument");
+  if (kind != kPlayAct && kind != kPlayStep) return fail(NARDE_EINVAL, "kind must be 0 (act) or 1 (step)");
+  DeviceGuard dg(e->device);
+  k_play_set<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), dice, kind, legal, table,
+                                                             count);
+  return check_launch("k_play_set");
+}
+
+int narde_explore_plays(narde_env* e, const uint8_t* dice, const float* epsilon, uint64_t seed, const int64_t* tag,
+                        int64_t* out, int64_t ld_out, void* stream) {
+  if (!e || !epsilon || !tag || !out) return fail(NARDE_EINVAL, "NULL argument");
+  if (ld_out < 2) return fail(NARDE_EINVAL, "action rows hold two codes (ld_out >= 2)");
+  DeviceGuard dg(e->device);
+  k_explore_plays<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), dice, epsilon, tag,
+                                                                  (uint32_t)seed, (uint32_t)(seed >> 32), out,
+                                                                  ld_out);
+  return check_launch("k_explore_plays");
+}
+
 int narde_policy_masked_argmax576(int device, const float* q, int64_t ldq, const uint64_t* mask, int64_t n,
                                   float epsilon, uint64_t seed, uint32_t tag, int head, int64_t* out,
                                   void* stream) {

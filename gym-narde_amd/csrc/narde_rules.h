@@ -524,6 +524,100 @@ NARDE_FN void env_step(Side& s, int d0, int d1, int code1, int code2, bool polic
   if (flip_always || !o.term) side_flip(s);
 }
 
+// ============================================================ play sets
+// The plays of a two-dice roll (the README's get_valid_actions,
+// README.md:156-165; VecNardeEnv.play_set), per entry of list #1 in list
+// order (the higher die's sources ascending, then the lower die's; doubles:
+// the same die twice, NardeEnv's list with its duplicates) -- the second
+// moves that follow it:
+//   kPlayAct  DQNAgent.act's valid_move_combinations
+//             (train_deepq_pytorch.py:430-507): the remaining die is the
+//             roll less the die act() matches to move 1 -- the first die in
+//             roll order equal to the distance, for a bear-off from p the
+//             first one >= p + 1 -- and its list is get_valid_moves([rem])
+//             on the PRE-move board (:486); an empty one gives (move 1, 0);
+//   kPlayStep what NardeEnv.step carries out (narde_env.py:45-93): move 1
+//             applied, rem = the roll less its distance (else pop(0)),
+//             get_valid_moves([rem]) on the POST-move board; a one-entry
+//             list #1 is played alone whatever the action.
+// Entry word: second-move sources (24 bits) | rem << 24 | kPlayValid.
+// Plays counted: kPlayAct every entry (duplicates included) times
+// max(1, |second list|) -- len(valid_move_combinations); kPlayStep the
+// distinct plays (a move listed under both dice -- doubles, or a bear-off
+// both dice reach -- once), 1 for a one-entry list.
+constexpr int kPlayAct = 0;
+constexpr int kPlayStep = 1;
+constexpr uint32_t kPlayValid = 1u << 27;
+
+// visit(k, p, die, word, dup) for every entry of list #1 in list order;
+// returns the play count.  l: legal2(s, d0, d1) (dice in roll order).
+template <class F>
+NARDE_FN int play_walk(const Side& s, int d0, int d1, int kind, const Legal& l, F&& visit) {
+  const int n1 = l.count;
+  const Blocks bl = block_info(s.O, s.P);
+  // act: the two one-die lists of the pre-move board (rem is d0 or d1)
+  const uint32_t M0 = die_filter(s.O, s.S1o, bl, die_candidates(s.O, s.P, d0), d0);
+  const uint32_t M1 = d1 == d0 ? M0 : die_filter(s.O, s.S1o, bl, die_candidates(s.O, s.P, d1), d1);
+  int count = 0;
+  for (int k = 0; k < 2; ++k) {
+    const int die = l.d[k];
+    uint32_t m = l.L[k];
+    while (m) {
+      const int p = __builtin_ctz(m);
+      m &= m - 1u;
+      const bool off = p < die;
+      const bool dup = k == 1 && ((l.L[0] >> p) & 1u) && (l.d[0] == l.d[1] || off);
+      uint32_t word;
+      if (kind == kPlayAct) {
+        const bool first = off ? d0 >= p + 1 : d0 == die;  // act() matched roll[0]
+        const int rem = first ? d1 : d0;
+        word = (first ? M1 : M0) | ((uint32_t)rem << 24) | kPlayValid;
+        const int c2 = __builtin_popcount(word & 0xFFFFFFu);
+        count += c2 > 0 ? c2 : 1;
+      } else if (n1 == 1) {
+        word = kPlayValid;  // narde_env.py:41-43: played alone
+        count = 1;
+      } else {
+        Side c = s;
+        apply_move(c, p, off ? OFF : p - die);
+        const int dist = off ? p + 1 : die;
+        const int rem = (d0 == dist) ? d1 : ((d1 == dist) ? d0 : d1);
+        const uint32_t L2 = die_filter(c.O, c.S1o, block_info(c.O, c.P), die_candidates(c.O, c.P, rem), rem);
+        word = L2 | ((uint32_t)rem << 24) | kPlayValid;
+        if (!dup) {
+          const int c2 = __builtin_popcount(L2);
+          count += c2 > 0 ? c2 : 1;
+        }
+      }
+      visit(k, p, die, word, dup);
+    }
+  }
+  return count;
+}
+
+// the play of act-kind index j (0 <= j < count) -> (move-1 code, move-2
+// code) as act() writes them (from * 24 + to, 'off' -> to 0; no second
+// move -> 0)
+NARDE_FN void play_codes_act(const Side& s, int d0, int d1, const Legal& l, int j, int& c1, int& c2) {
+  c1 = 0;
+  c2 = 0;
+  int left = j;
+  bool found = false;
+  play_walk(s, d0, d1, kPlayAct, l, [&](int, int p, int die, uint32_t word, bool) {
+    if (found) return;
+    const uint32_t m2 = word & 0xFFFFFFu;
+    const int w = m2 ? __builtin_popcount(m2) : 1;
+    if (left >= w) { left -= w; return; }
+    found = true;
+    c1 = encode_move(p, p < die ? OFF : p - die);
+    if (m2) {
+      const int rem = (int)((word >> 24) & 7u);
+      const int q = select_bit(m2, left);
+      c2 = encode_move(q, q < rem ? OFF : q - rem);
+    }
+  });
+}
+
 // ============================================================ FULL4 turns
 // Build extension: one
 // step = the mover's WHOLE turn -- four sub-moves on doubles, the

@@ -582,9 +582,17 @@ class BatchedDQNDriver:
     def __init__(self, env, obs="tesauro198", train_batch=4096, capacity=1 << 20,
                  learning_rate=1e-4, gamma=0.99, epsilon=1.0, epsilon_min=0.01,
                  epsilon_decay=0.995, target_update=10, updates_per_step=1, shaping=True,
-                 seed=0, fused=True, fused_heads=True, gathered_heads=True, fused_features=True):
+                 seed=0, fused=True, fused_heads=True, gathered_heads=True, fused_features=True,
+                 explore="plays"):
         if env.full:
             raise ValueError("the DQN driver plays the reference's (move1, move2) actions: rules='ref2'")
+        if explore not in ("plays", "codes"):
+            raise ValueError("explore must be 'plays' (the reference's act()) or 'codes'")
+        # the epsilon-branch law: "plays" = random.choice over act()'s
+        # (move1, move2) combinations (train_deepq_pytorch.py:430-515, second
+        # moves listed on the pre-move board), k_explore_plays; "codes" = each
+        # head uniform over its own legal codes (the policy kernels alone)
+        self.explore = explore
         self.env, self.dev = env, env.device
         self.obs_kind = obs
         self.state_size = 198 if obs == "tesauro198" else 24
@@ -666,7 +674,12 @@ class BatchedDQNDriver:
     def act(self, x):
         """Masked epsilon-greedy (move1, move2) codes for the next step: the
         env's exact legal masks and the fused policy kernel (epsilon and the
-        step tag read from device memory)."""
+        step tag read from device memory).  Greedy: move 1 = the masked
+        argmax over the move-1 codes the step accepts, move 2 = the masked
+        argmax over the codes the step accepts after it (post-move).
+        Exploring rows (one shared draw per row and step): explore="plays"
+        draws one of act()'s (move1, move2) combinations uniformly
+        (k_explore_plays), as random.choice(valid_move_combinations)."""
         f = self.model.features_nograd(x)
         if self.fused_heads:
             # both heads inside the policy kernel, legal codes only
@@ -681,6 +694,8 @@ class BatchedDQNDriver:
             m2 = self.env.legal_mask_move2(m1)
             head_policy_576(f, h2.weight, h2.bias, m2, self.eps_t, self.seed, self.tag_t, 1, out=acts[:, 1],
                             move1=acts[:, 0])
+            if self.explore == "plays":
+                self.env.explore_plays(acts, self.eps_t, self.seed, self.tag_t)
             return acts
         a1 = policy_576(self.model.move1_head(f), self.env.legal_mask(), self.eps_t, self.seed,
                         self.tag_t, 0)
@@ -691,7 +706,10 @@ class BatchedDQNDriver:
         base = torch.nn.functional.linear(f, w[:, :256], self.model.move2_head.bias)
         wm_rows = w[:, 256:].t().contiguous()
         a2 = policy_576(base, m2, self.eps_t, self.seed, self.tag_t, 1, add=(wm_rows, a1))
-        return torch.stack([a1, a2], 1)
+        acts = torch.stack([a1, a2], 1)
+        if self.explore == "plays":
+            self.env.explore_plays(acts, self.eps_t, self.seed, self.tag_t)
+        return acts
 
     def step(self):
         """One env step for every env + the updates; returns the last loss

@@ -73,6 +73,42 @@ def decode_played(word):
     return out
 
 
+PLAY_KINDS = {"act": 0, "step": 1}
+
+
+def decode_play_set(legal, words, kind="act"):
+    """One env's play set (VecNardeEnv.play_set: its compact list #1 and
+    its (2, 24) entry words) in the reference's terms.
+    kind "act": DQNAgent.act's valid_move_combinations
+    (train_deepq_pytorch.py:430-507) -- a list of (move1_code, move2_code)
+    in act()'s order, duplicates included ('off' coded as to = 0, no second
+    move as 0).  kind "step": the set of plays NardeEnv.step carries out
+    (narde_env.py:45-93) as move tuples ((m1, m2), or (m1,) alone), as
+    Narde.get_valid_plays returns them."""
+    c = int(np.uint64(np.int64(legal)))
+    w = np.asarray(words).astype(np.int64).reshape(2, 24)
+    masks = (c & 0xFFFFFF, (c >> 24) & 0xFFFFFF)
+    dies = ((c >> 48) & 0xF, (c >> 52) & 0xF)
+    entries = [(k, p, dies[k]) for k in range(2) if dies[k] for p in range(24) if (masks[k] >> p) & 1]
+    out = [] if kind == "act" else set()
+    for k, p, d in entries:
+        wd = int(w[k, p])
+        m2, rem = wd & 0xFFFFFF, (wd >> 24) & 7
+        seconds = [(q, "off" if q < rem else q - rem) for q in range(24) if (m2 >> q) & 1]
+        m1 = (p, "off" if p < d else p - d)
+        if kind == "act":
+            c1 = p * 24 + (0 if m1[1] == "off" else m1[1])
+            if not seconds:
+                out.append((c1, 0))
+            for q, t in seconds:
+                out.append((c1, q * 24 + (0 if t == "off" else t)))
+        elif len(entries) == 1 or not seconds:
+            out.add((m1,))
+        else:
+            out.update((m1, m2_) for m2_ in seconds)
+    return out
+
+
 class VecNardeEnv:
     def __init__(self, num_envs, device=None, seed=0, env_id_offset=0, dice_mode="all36",
                  max_episode_steps=1000, autoreset=True, rules="ref2"):
@@ -233,6 +269,45 @@ class VecNardeEnv:
                          self._s())
         self._keep = (m1, d)
         return out
+
+    def play_set(self, dice=None, kind="act"):
+        """The plays of each env's two-dice roll (narde_play_set; the
+        README's get_valid_actions, README.md:156-165) for dice (B,2) in roll
+        order or the next step's device dice.  Returns (legal (B,) int64
+        compact list #1, words (B,2,24) int32 -- per list-#1 entry its
+        second-move sources | rem << 24 | 1 << 27, count (B,) int32 plays).
+        kind "act": DQNAgent.act's combinations, second moves on the
+        PRE-move board (train_deepq_pytorch.py:430-507); "step": the plays
+        NardeEnv.step carries out, second moves on the POST-move board
+        (narde_env.py:45-93).  decode_play_set() turns one env's row into
+        the reference's list / set."""
+        if kind not in PLAY_KINDS:
+            raise ValueError(f"kind must be one of {tuple(PLAY_KINDS)}")
+        B, t = self.num_envs, self.torch
+        d = None if dice is None else self._dev(dice, t.uint8, (B, 2))
+        legal = t.empty(B, dtype=t.int64, device=self.device)
+        words = t.empty((B, 2, 24), dtype=t.int32, device=self.device)
+        count = t.empty(B, dtype=t.int32, device=self.device)
+        self.handle.call("narde_play_set", _lib.ptr(d), PLAY_KINDS[kind], _lib.ptr(legal), _lib.ptr(words),
+                         _lib.ptr(count), self._s())
+        self._keep = (d,)
+        return legal, words, count
+
+    def explore_plays(self, actions, epsilon, seed, tag, dice=None):
+        """The DQN driver's exploration (narde_explore_plays): rows whose
+        explore draw ({tag, row, 0, 5}, seed) is below epsilon get a play
+        drawn uniformly from act()'s combination list written into their
+        (B, 2) int64 action row (in place); epsilon (f32) and tag (int64)
+        are device scalars (graph-safe)."""
+        B, t = self.num_envs, self.torch
+        if (actions.dtype != t.int64 or tuple(actions.shape) != (B, 2) or actions.stride(1) != 1
+                or actions.device != self.device):
+            raise ValueError(f"actions must be ({B}, 2) int64 rows on the env's device")
+        d = None if dice is None else self._dev(dice, t.uint8, (B, 2))
+        self.handle.call("narde_explore_plays", _lib.ptr(d), _lib.ptr(epsilon), int(seed) & (2 ** 64 - 1),
+                         _lib.ptr(tag), _lib.ptr(actions), actions.stride(0), self._s())
+        self._keep = (d,)
+        return actions
 
     def legal_full(self, dice=None):
         """FULL4: (B,) int64 legal words (first sub-move set | max dice << 56)

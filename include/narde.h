@@ -231,6 +231,35 @@ int narde_legal_mask576(narde_env *env, uint64_t *mask, void *stream);
 int narde_legal_mask576_move2(narde_env *env, const int16_t *move1, const uint8_t *dice,
                               uint64_t *mask, void *stream);
 
+/* The plays of each env's two-dice roll (the README's get_valid_actions,
+ * README.md:156-165), for dice u8[B][2] in roll order (NULL = the next
+ * step's device dice).  Replaces the per-env Python lists of
+ * DQNAgent.act (train_deepq_pytorch.py:430-507, kind 0) and the (m1, m2)
+ * set NardeEnv.step carries out (narde_env.py:45-93, kind 1; the facade's
+ * Narde.get_valid_plays).  Outputs: legal u64[B] (optional) = list #1 in
+ * the compact format above; table u32[B][2][24]: for each list-#1 entry
+ * (k = 0 the higher die's list, k = 1 the lower's; source p) the word
+ * second-move sources (24 bits) | rem << 24 | 1 << 27, 0 where (k, p) is no
+ * entry -- kind 0: rem = the roll less the die act() matches to move 1
+ * (exact distance in roll order; a bear-off from p: the first die >= p+1),
+ * its list get_valid_moves([rem]) on the pre-move board; kind 1: move 1
+ * applied, rem per the step's bookkeeping, list #2 on the post-move board
+ * (a one-entry list #1: word 1 << 27, played alone); count i32[B]: kind 0
+ * len(valid_move_combinations) (every entry, duplicates included, times
+ * max(1, |its list|)), kind 1 the number of distinct plays.  A die outside
+ * 1..6: list 0, count 0. */
+int narde_play_set(narde_env *env, const uint8_t *dice, int kind, uint64_t *legal, uint32_t *table,
+                   int32_t *count, void *stream);
+
+/* The DQN driver's exploration (train_deepq_pytorch.py:514-515): for the
+ * rows whose explore draw Philox4x32-10({*tag, row, 0, 5}, seed) r0 <
+ * *epsilon * 2^32 (the policy kernels' shared decision), writes play
+ * mulhi(r1, count) of act()'s combination list (kind 0 above: uniform over
+ * (move1, move2) combinations) into out[row * ld_out + 0..1] (int64 codes);
+ * other rows, and rows with no play, are left untouched.  dice as above. */
+int narde_explore_plays(narde_env *env, const uint8_t *dice, const float *epsilon, uint64_t seed,
+                        const int64_t *tag, int64_t *out, int64_t ld_out, void *stream);
+
 /* Masked epsilon-greedy over the 576 codes (the policy of
  * train_deepq_pytorch.py:411-600, batched; stateless): q f32[n][ldq]
  * (ldq >= 576) Q-values, mask u64[n][9] legal codes (the two mask entry

@@ -86,6 +86,43 @@ void hc_step_batch(int64_t n, int8_t* board, uint8_t* off, uint8_t* ft, int8_t* 
   }
 }
 
+// k_play_set's per-lane body (narde_rules.h play_walk); dice in roll order
+void hc_play_set(int64_t n, const int8_t* board, const uint8_t* off, const uint8_t* ft, const int8_t* player,
+                 const uint8_t* dice, int kind, uint64_t* legal, uint32_t* table, int32_t* count) {
+  for (int64_t i = 0; i < n; ++i) {
+    const Side s = load(board + i * 24, off + 2 * i, ft + 2 * i, player[i], 0);
+    uint32_t* row = table + i * 48;
+    memset(row, 0, 48 * sizeof(uint32_t));
+    const int d0 = dice[2 * i], d1 = dice[2 * i + 1];
+    if (d0 < 1 || d0 > 6 || d1 < 1 || d1 > 6) {
+      legal[i] = 0;
+      count[i] = 0;
+      continue;
+    }
+    Legal l;
+    legal2(s, d0, d1, l);
+    legal[i] = (uint64_t)l.L[0] | ((uint64_t)l.L[1] << 24) | ((uint64_t)l.d[0] << 48) | ((uint64_t)l.d[1] << 52);
+    count[i] = play_walk(s, d0, d1, kind, l, [&](int k, int p, int, uint32_t w, bool) { row[k * 24 + p] = w; });
+  }
+}
+
+// play_codes_act for every play index j < count of env 0's roll (dice in
+// roll order): codes[2 j], codes[2 j + 1]
+int hc_play_codes_act(const int8_t* board, const uint8_t* off, const uint8_t* ft, int8_t player,
+                      const uint8_t* dice, int16_t* codes, int cap) {
+  const Side s = load(board, off, ft, player, 0);
+  Legal l;
+  legal2(s, dice[0], dice[1], l);
+  const int cnt = play_walk(s, dice[0], dice[1], kPlayAct, l, [](int, int, int, uint32_t, bool) {});
+  for (int j = 0; j < cnt && j < cap; ++j) {
+    int c1, c2;
+    play_codes_act(s, dice[0], dice[1], l, j, c1, c2);
+    codes[2 * j] = (int16_t)c1;
+    codes[2 * j + 1] = (int16_t)c2;
+  }
+  return cnt;
+}
+
 void hc_reset_batch(int64_t n, int64_t env0, uint64_t seed, uint32_t epoch, int8_t* board,
                     uint8_t* off, uint8_t* ft, int8_t* player, uint16_t* elapsed) {
   for (int64_t i = 0; i < n; ++i) {

@@ -41,11 +41,14 @@ def make(n=4096, **kw):
     return env, BatchedDQNDriver(env, capacity=1 << 16, train_batch=1024, **kw)
 
 
-@pytest.mark.parametrize("obs", ["tesauro198", "int24"])
-def test_driver_actions_are_legal_and_learning_runs(obs):
+@pytest.mark.parametrize("obs,explore", [("tesauro198", "plays"), ("int24", "plays"), ("tesauro198", "codes")])
+def test_driver_actions_are_legal_and_learning_runs(obs, explore):
+    """Every action is legal: greedy and explore="codes" rows per the env's
+    acceptance masks; explore="plays" rows one of act()'s combinations."""
+    from conftest import in_act_plays
     from gym_narde.dqn import expand_mask
 
-    env, drv = make(obs=obs)
+    env, drv = make(obs=obs, explore=explore)
     n = env.num_envs
     for step in range(12):
         x = drv.state
@@ -53,11 +56,13 @@ def test_driver_actions_are_legal_and_learning_runs(obs):
         a = drv.act(x)
         m2 = expand_mask(env.legal_mask_move2(a[:, 0].to(torch.int16)))
         rows = torch.arange(n, device=a.device)
-        has1 = m1.any(1)
-        assert bool(m1[rows, a[:, 0]][has1].all())
-        assert bool((a[:, 0][~has1] == 0).all())
-        has2 = m2.any(1)
-        assert bool(m2[rows, a[:, 1]][has2].all())
+        has1, has2 = m1.any(1), m2.any(1)
+        ok1 = torch.where(has1, m1[rows, a[:, 0]], a[:, 0] == 0)
+        ok2 = ~has2 | m2[rows, a[:, 1]]
+        if explore == "codes":
+            assert bool(ok1.all()) and bool(ok2.all())
+        else:
+            assert bool((in_act_plays(*env.play_set(kind="act"), a) | (ok1 & ok2)).all())
         drv.step()  # (draws its own actions; the env advances)
     torch.cuda.synchronize()
     assert drv.replay.size == 12 * n
@@ -101,7 +106,7 @@ def test_reference_step_accepts_driver_actions():
 
     from gym_narde.dqn import expand_mask
 
-    env, drv = make(n=2048)
+    env, drv = make(n=2048, explore="codes")
     env.selfplay(40)
     drv.resync()
     has1 = expand_mask(env.legal_mask()).any(1).cpu().numpy()
