@@ -42,7 +42,7 @@ class NardeEnv(Env):
     @staticmethod
     def _code(c):
         c = int(c)
-        return c if 0 <= c < 576 else -1  # never matches a listed move (narde_env.py:255)
+        return c if 0 <= c < 576 else -1  # never matches a listed move (`move1 in valid_moves`, narde_env.py:63)
 
     def step(self, action):
         # narde_env.py:29 -- two draws from the global legacy RNG, roll order kept

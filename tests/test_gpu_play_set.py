@@ -152,8 +152,9 @@ def test_explore_plays_draws_act_combinations(eps):
 
 def test_driver_explores_over_act_combinations():
     """BatchedDQNDriver(explore="plays") at epsilon 1: every row's action is
-    one of act()'s combinations for the step's own dice; the step that
-    follows plays move 1 whenever its code is one the step accepts."""
+    one of act()'s combinations for the step's own dice, and its move 1 is
+    a code the step accepts unless it is act()'s (f, 0)/(f, 'off') code
+    collision."""
     from gym_narde.dqn import BatchedDQNDriver, expand_mask
     from gym_narde.vector import VecNardeEnv, decode_play_set
 
@@ -172,5 +173,10 @@ def test_driver_explores_over_act_combinations():
         assert tuple(got[i]) in set(decode_play_set(legal[i], words[i], "act")), f"env {i}"
     rows = torch.arange(env.num_envs, device="cuda:0")
     ok = acc1[rows, a[:, 0]] | ~acc1.any(1)
-    assert float(ok.float().mean()) > 0.99  # act()'s (f, 0) codes, f <= 5, aside
+    # the only move-1 codes of act()'s list the step does not accept: a
+    # normal move (f, 0), f <= 5, whose code f * 24 the step decodes as
+    # (f, 'off') (narde_env.py:50-53) -- the reference's own collision
+    quirk = (a[:, 0] % 24 == 0) & (a[:, 0] // 24 <= 5)
+    assert bool((ok | quirk).all())
+    assert float(ok.float().mean()) > 0.8
     env.close()

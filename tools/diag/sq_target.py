@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """rocprofv3 --pmc target for SQ issue counters: 3 k_rollout launches with
 outputs, then 3 stats-only, at the bench shape, for the libnarde.so named by
-$NARDE_LIB (default: the in-tree build).  DIAGNOSTIC."""
+$NARDE_LIB (default: the in-tree build).  argv: rules (ref2 / full4), plies
+per launch (default 100).  DIAGNOSTIC."""
 import os
 import sys
 
@@ -14,12 +15,13 @@ from gym_narde.vector import VecNardeEnv  # noqa: E402
 
 def main():
     rules = sys.argv[1] if len(sys.argv) > 1 else "ref2"
+    P = int(sys.argv[2]) if len(sys.argv) > 2 else 100
     env = VecNardeEnv(65536, device="cuda:0", seed=0, rules=rules)
-    bufs = env.rollout_buffers(100)
+    bufs = env.rollout_buffers(P)
     for _ in range(3):
-        env.rollout(100, bufs)
+        env.rollout(P, bufs)
     for _ in range(3):
-        env.selfplay(100)
+        env.selfplay(P)
     torch.cuda.synchronize()
     env.close()
 
