@@ -14,6 +14,7 @@ struct Outs {
   uint64_t* __restrict__ legal;   // [.][n] compact list #1 (FULL4: C_0 | M<<56)
   int16_t* __restrict__ act_out;  // [.][n][2] REF2 codes used
   uint64_t* __restrict__ played;  // [.][n] FULL4 sub-moves (from, die) x 4
+  int64_t* __restrict__ totals;   // [workgroup][3] statistics after the launch (wg_totals), or null
 };
 
 struct StepArgs {
@@ -171,6 +172,47 @@ __device__ __forceinline__ void add_stats(int4* __restrict__ stats, int i, const
   }
 }
 
+// add_stats, returning env i's statistics after it when `want` (read even
+// if this launch finished no episode of the env); zeros otherwise
+__device__ __forceinline__ int4 stats_after(int4* __restrict__ stats, int i, const int4& st, bool want) {
+  int4 cur = make_int4(0, 0, 0, 0);
+  if (st.x || want) {
+    cur = stats[i];
+    cur.x += st.x; cur.y += st.y; cur.z += st.z;
+    if (st.x) stats[i] = cur;
+  }
+  return cur;
+}
+
+// The rollout's episode totals without a second launch: every thread of
+// the workgroup passes its env's statistics after the launch (zeros for
+// threads with no env), and the workgroup writes their sum
+// {episodes, white points, black points} to rows[blockIdx.x] -- one row per
+// 256 envs (every rollout kernel holds 256 envs per workgroup).  A
+// workgroup barrier: every thread must call it.  (narde_get_totals after
+// the launch costs a second dispatch; right behind a launch bracketed by
+// timing markers its host call also blocked for ~110 us,
+// tools/diag/gpu_benchcmp2.sh.)
+__device__ __forceinline__ void wg_totals(const int4& cum, int64_t* __restrict__ rows) {
+  __shared__ long long red[16][3];
+  long long e = cum.x, w = cum.y, k = cum.z;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    e += __shfl_xor(e, o, 64);
+    w += __shfl_xor(w, o, 64);
+    k += __shfl_xor(k, o, 64);
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[wave][0] = e; red[wave][1] = w; red[wave][2] = k; }
+  __syncthreads();
+  if (threadIdx.x < 3) {
+    long long t = 0;
+    const int nw = (int)(blockDim.x >> 6);
+    for (int q = 0; q < nw; ++q) t += red[q][threadIdx.x];
+    rows[3 * blockIdx.x + threadIdx.x] = (int64_t)t;
+  }
+}
+
 // NardeEnv.step for every env (API step; one ply of self-play when the
 // actions are NULL).  kFull: FULL4 whole turns (TurnOut), else REF2 (StepOut).
 template <bool kFull>
@@ -221,12 +263,15 @@ __global__ void __launch_bounds__(kBlock, 1) k_rollout_wave(Planes pl, int n, Rn
         p == 0);
     if (kOut && valid) store_outs(out, (size_t)p * n + i, s, o, term, trunc, nullptr, false);
   }
-  if (!valid) return;
-  uint4 ra, rb;
-  side_to_record(s, ra, rb);
-  pl.p0[i] = ra;
-  pl.p1[i] = rb;
-  add_stats(pl.stats, i, st);
+  int4 cum = make_int4(0, 0, 0, 0);
+  if (valid) {
+    uint4 ra, rb;
+    side_to_record(s, ra, rb);
+    pl.p0[i] = ra;
+    pl.p1[i] = rb;
+    cum = stats_after(pl.stats, i, st, out.totals != nullptr);
+  }
+  if (out.totals) wg_totals(cum, out.totals);
 }
 
 // ---------------------------------------------------------------------------
@@ -341,6 +386,7 @@ __global__ void __launch_bounds__(kFxThreads) k_rollout_full(Planes pl, int n, R
   FxLds& M = fx[grp];
   const int i = blockIdx.x * kFxEnvs + grp * 64 + lane;
   const bool valid = i < n;
+  int4 cum = make_int4(0, 0, 0, 0);  // the env's statistics after the launch (wg_totals)
   if (wave < kFxGroups) {
     M.post[lane] = 0u;
     M.back[lane] = 0u;
@@ -414,12 +460,13 @@ __global__ void __launch_bounds__(kFxThreads) k_rollout_full(Planes pl, int n, R
       }
     }
     lds_publish(&M.fin, 1u);
-    if (!valid) return;
-    uint4 ra, rb;
-    side_to_record(s, ra, rb);
-    pl.p0[i] = ra;
-    pl.p1[i] = rb;
-    add_stats(pl.stats, i, st);
+    if (valid) {
+      uint4 ra, rb;
+      side_to_record(s, ra, rb);
+      pl.p0[i] = ra;
+      pl.p1[i] = rb;
+      cum = stats_after(pl.stats, i, st, out.totals != nullptr);
+    }
   } else {
     // ---- helper wave: the posted (block-bound) turns
     uint32_t done = 0u;  // parks of rule lane `lane` answered
@@ -468,6 +515,7 @@ __global__ void __launch_bounds__(kFxThreads) k_rollout_full(Planes pl, int n, R
       __builtin_amdgcn_s_sleep(24);
     }
   }
+  if (out.totals) wg_totals(cum, out.totals);
 }
 
 // ---------------------------------------------------------------------------
@@ -664,13 +712,15 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
     pc_block(nb - 1, plies, p0, np);
     pc_emit<kNt>(L, (nb - 1) % kPcSlots, np, p0, n, wg_env0, cw, lane, out);
   }
+  int4 cum = make_int4(0, 0, 0, 0);
   if (producer && valid) {
     uint4 ra, rb;
     side_to_record(s, ra, rb);
     pl.p0[i] = ra;
     pl.p1[i] = rb;
-    add_stats(pl.stats, i, st);
+    cum = stats_after(pl.stats, i, st, out.totals != nullptr);
   }
+  if (out.totals) wg_totals(cum, out.totals);
 }
 
 }  // namespace

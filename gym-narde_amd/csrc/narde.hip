@@ -383,18 +383,19 @@ int narde_selfplay_full(narde_env* e, int plies, void* stream) {
 
 int narde_rollout_timed(narde_env* e, int full, int plies, int32_t* obs, int32_t* reward, uint8_t* terminated,
                         uint8_t* truncated, uint64_t* legal, void* last, void* ev_start, void* ev_stop,
-                        void* stream) {
+                        int64_t* totals, void* stream) {
   if (!e || plies < 0) return fail(NARDE_EINVAL, "bad argument");
+  if (totals && plies == 0) return fail(NARDE_EINVAL, "totals rows need a launch (plies > 0)");
   DeviceGuard dg(e->device);
   const bool any = obs || reward || terminated || truncated || legal || last;
   if (ev_start && hipEventRecord((hipEvent_t)ev_start, (hipStream_t)stream) != hipSuccess)
     return fail(NARDE_EHIP, "hipEventRecord(ev_start) failed");
   int rc = NARDE_OK;
   if (plies > 0 && full) {
-    const Outs out{obs, reward, terminated, truncated, legal, nullptr, (uint64_t*)last};
+    const Outs out{obs, reward, terminated, truncated, legal, nullptr, (uint64_t*)last, totals};
     rc = launch_rollout_full(e, plies, out, any, (hipStream_t)stream);
   } else if (plies > 0) {
-    const Outs out{obs, reward, terminated, truncated, legal, (int16_t*)last, nullptr};
+    const Outs out{obs, reward, terminated, truncated, legal, (int16_t*)last, nullptr, totals};
     rc = launch_rollout_ref2(e, plies, out, any, (hipStream_t)stream);
   }
   if (rc) return rc;

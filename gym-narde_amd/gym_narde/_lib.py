@@ -14,6 +14,11 @@ OK = 0
 OFF = 24
 MAX_MOVES = 64
 TOTAL_ROWS = 64  # NARDE_TOTAL_ROWS
+
+
+def wg_rows(num_envs):
+    """NARDE_WG_ROWS: rows of narde_rollout_timed's per-workgroup totals."""
+    return (int(num_envs) + 255) // 256
 DICE_ALL36 = 0
 DICE_NODOUBLES = 1
 
@@ -43,7 +48,7 @@ SIGNATURES = {
     "narde_step_full": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i32, _vp]),
     "narde_rollout_full": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "narde_selfplay_full": (_i32, [_vp, _i32, _vp]),
-    "narde_rollout_timed": (_i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "narde_rollout_timed": (_i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "narde_timing_event_create": (_i32, [_i32, ctypes.c_uint, ctypes.POINTER(_vp)]),
     "narde_timing_event_destroy": (_i32, [_vp]),
     "narde_timing_event_elapsed_ms": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_float)]),

@@ -374,7 +374,7 @@ class VecNardeEnv:
                          _lib.ptr(bufs["legal"]), _lib.ptr(bufs["actions"]), self._s())
         return bufs
 
-    def rollout_launcher(self, plies, bufs, events=None):
+    def rollout_launcher(self, plies, bufs, events=None, totals=None):
         """rollout(plies, bufs) pre-bound: a zero-argument callable that makes
         exactly one ctypes call (one kernel launch on the stream current
         NOW), for hot loops where the per-call Python of rollout() would
@@ -382,10 +382,22 @@ class VecNardeEnv:
         events = (start, stop) torch.cuda.Event or TimingEvent (either None): recorded on
         that stream right before / after the launch, inside the same call
         (narde_rollout_timed); a torch event must have been recorded once
-        already (it creates its HIP event at its first record)."""
+        already (it creates its HIP event at its first record).
+        totals: a (wg_rows(B), 3) int64 device tensor the launch fills with
+        the statistics after it summed per 256 envs (.sum(0) = the
+        handle's {episodes, white points, black points}) -- no second launch."""
         for v in bufs.values():
             if v is not None and v.shape[0] < plies:
                 raise ValueError("rollout buffer shorter than plies")
+        if totals is not None:
+            t = self.torch
+            if (tuple(totals.shape) != (_lib.wg_rows(self.num_envs), 3) or totals.dtype != t.int64
+                    or totals.device != self.device or not totals.is_contiguous()):
+                raise ValueError(f"totals must be a contiguous ({_lib.wg_rows(self.num_envs)}, 3) int64 "
+                                 "tensor on the env's device")
+            if plies <= 0:
+                raise ValueError("totals need a launch (plies > 0)")
+            events = events if events is not None else (None, None)
         bufargs = (_lib.ptr(bufs["obs"]), _lib.ptr(bufs["reward"]), _lib.ptr(bufs["terminated"]),
                    _lib.ptr(bufs["truncated"]), _lib.ptr(bufs["legal"]), _lib.ptr(bufs["actions"]))
         if events is None:
@@ -402,7 +414,8 @@ class VecNardeEnv:
                     raise ValueError("record each event once before binding it (its HIP event is created then)")
                 evs.append(ctypes.c_void_p(ev.cuda_event) if ev is not None else None)
             fn, name = self.handle.lib.narde_rollout_timed, "narde_rollout_timed"
-            args = (self.handle.h, int(self.full), int(plies)) + bufargs + (evs[0], evs[1], self._s())
+            args = (self.handle.h, int(self.full), int(plies)) + bufargs + (evs[0], evs[1], _lib.ptr(totals),
+                                                                            self._s())
 
         def launch():
             rc = fn(*args)
@@ -411,6 +424,7 @@ class VecNardeEnv:
 
         launch.bufs = bufs  # keeps the buffers referenced as long as the launcher
         launch.events = events
+        launch.totals = totals
         return launch
 
     def stats(self, out=None):

@@ -177,10 +177,16 @@ int narde_selfplay_full(narde_env *env, int plies, void *stream);
  * narde_rollout_full (full = 1; `last` = played u64[plies][B]) with HIP
  * events recorded on `stream` just before the launch (ev_start) and just
  * after it (ev_stop), each optional (NULL): a timed launch is one call
- * instead of three (bench.py's timed region).  plies = 0 launches nothing. */
+ * instead of three (bench.py's timed region).  totals (optional): the
+ * launch also writes the statistics of narde_get_stats after it, summed per
+ * workgroup of 256 envs, as i64[NARDE_WG_ROWS(B)][3] {episodes, white
+ * points, black points} (row r: envs 256 r .. 256 r + 255) -- the self-play
+ * driver's per-run result with no second launch.  plies = 0 launches
+ * nothing (and then totals must be NULL). */
+#define NARDE_WG_ROWS(num_envs) (((num_envs) + 255) / 256)
 int narde_rollout_timed(narde_env *env, int full, int plies, int32_t *obs, int32_t *reward,
                         uint8_t *terminated, uint8_t *truncated, uint64_t *legal, void *last,
-                        void *ev_start, void *ev_stop, void *stream);
+                        void *ev_start, void *ev_stop, int64_t *totals, void *stream);
 /* Timing events for narde_rollout_timed on `device`: a HIP event (returned
  * as void*) created with hipEventCreateWithFlags(flags); flags 0 = HIP's
  * default, 0x20000000 = hipEventDisableSystemFence (the event's record does

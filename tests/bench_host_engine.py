@@ -19,7 +19,6 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "tests", "hostcheck", "build", "libhostcheck.so")
-TOTAL_ROWS = 64  # narde_get_totals' partial rows (include/narde.h)
 
 NAME = "host rehearsal (tests/hostcheck: narde_rules.h on the CPU) -- not a measurement"
 
@@ -69,30 +68,27 @@ class HostVecEnv:
         self.t += plies
         return bufs
 
-    def rollout_launcher(self, plies, bufs, events=None):
+    def rollout_launcher(self, plies, bufs, events=None, totals=None):
         ev0, ev1 = events if events is not None else (None, None)
 
         def launch():
             if ev0 is not None:
                 ev0.t = time.perf_counter()
             self.rollout(plies, bufs)
+            if totals is not None:
+                totals.copy_(self.wg_totals())
             if ev1 is not None:
                 ev1.t = time.perf_counter()
 
         return launch
 
-    def totals(self, out=None):
-        """narde_get_totals restated: row b sums the b-th contiguous range
-        of ceil(n / 64) envs."""
-        per = -(-self.n // TOTAL_ROWS)
-        rows = np.zeros((TOTAL_ROWS, 3), np.int64)
-        for b in range(TOTAL_ROWS):
-            rows[b] = self.stats[b * per:min(self.n, (b + 1) * per)].astype(np.int64).sum(0)
-        t = torch.from_numpy(rows)
-        if out is not None:
-            out.copy_(t)
-            return out
-        return t
+    def wg_totals(self):
+        """narde_rollout_timed's totals rows restated: row r sums the
+        statistics of envs 256 r .. 256 r + 255."""
+        rows = -(-self.n // 256)
+        pad = np.zeros((rows * 256, 3), np.int64)
+        pad[:self.n] = self.stats
+        return torch.from_numpy(pad.reshape(rows, 256, 3).sum(1))
 
     def close(self):
         pass

@@ -336,3 +336,29 @@ def test_rccl_world1_process_group_gathers_device_stats():
     r = subprocess.run([sys.executable, "-c", _NCCL_CHILD, ROOT], env=env, capture_output=True,
                        text=True, timeout=240)
     assert r.returncode == 0 and "RCCL_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+@pytest.mark.parametrize("rules,plies,n", [("ref2", 20, 65536), ("ref2", 1000, 1000), ("full4", 20, 4099),
+                                           ("full4", 60, 65536), ("ref2", 7, 300)])
+def test_rollout_launch_totals_rows(rules, plies, n):
+    """narde_rollout_timed(totals=...): the launch writes its envs'
+    statistics after it, summed per 256 envs -- equal to stats() of the same
+    handle grouped the same way (and .sum(0) to totals()), for every rollout
+    kernel (REF2 producer/consumer, FULL4 one-wave below 48 plies and
+    rule/helper waves above) and ragged env counts."""
+    from gym_narde import _lib
+
+    env = vec(n, seed=13, rules=rules)
+    bufs = env.rollout_buffers(plies)
+    rows = torch.full((_lib.wg_rows(n), 3), -1, dtype=torch.int64, device="cuda:0")
+    env.rollout(150, env.rollout_buffers(150))  # some episodes finished already
+    L = env.rollout_launcher(plies, bufs, totals=rows)
+    for _ in range(2):
+        L()
+    st = env.stats().long()
+    pad = torch.zeros((rows.shape[0] * 256, 3), dtype=torch.int64, device="cuda:0")
+    pad[:n] = st
+    assert torch.equal(rows, pad.view(-1, 256, 3).sum(1))
+    assert torch.equal(rows.sum(0), env.totals().sum(0))
+    assert int(rows[:, 0].sum()) > 0
+    env.close()

@@ -10,27 +10,21 @@ ply written to HBM (int32[24] obs, reward, terminated, truncated, compact
 legal set, actions).  The timed path is k_rollout: P plies per launch with
 the env record in VGPRs, each ply's outputs streamed to [P][B] rollout
 buffers (K steps = ceil(K/P) launches).  The per-ply API kernel k_step is
-measured beside it (eager and hipGraph-replayed).  N GPUs = N processes,
-each owning a contiguous shard of global env ids (weak scaling): under
-torchrun (WORLD_SIZE set) the bench is one rank and checks that the world
-size equals --gpus; run plainly with --gpus N > 1 it starts the N ranks
-itself (torch.distributed.run, 127.0.0.1) before touching the GPU.  The
-timed region ends with every rank's episode totals (one kernel) and, at
-N > 1, the RCCL all-gather of them.
+measured beside it (eager and hipGraph-replayed).  N GPUs = N processes
+(torchrun), each owning a contiguous shard of global env ids (weak
+scaling); at N > 1 the timed region ends with the RCCL all-gather of every
+rank's episode totals.
 
 Prints ONE JSON line on rank 0 (fields: DESIGN.md section 6).
 """
 import argparse
 import gc
-import importlib.util
 import json
 import os
-import socket
-import subprocess
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "gym-narde_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
@@ -154,69 +148,9 @@ def load_traffic(path, envs, plies):
     return d.get("hbm_bytes_per_launch")
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-def spawn_ranks(n, argv):
-    """Start the N-rank bench as the driver would (torch.distributed.run,
-    one process per GPU, rendezvous on 127.0.0.1) and return its exit code.
-    Called before this process touches the GPU; the ranks are children (no
-    exec), and rank 0's JSON line reaches our stdout."""
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL on this host driver)
-    return subprocess.call(cmd, env=env)
-
-
-class GpuEngine:
-    """The product: VecNardeEnv (libnarde.so) on this rank's GPU."""
-
-    name = None
-
-    def __init__(self, local_rank):
-        import torch
-
-        torch.cuda.set_device(local_rank)
-        self.torch = torch
-        self.device = torch.device("cuda", local_rank)
-
-    def make_env(self, per, first, seed, rules):
-        from gym_narde.vector import VecNardeEnv
-
-        return VecNardeEnv(per, device=self.device, seed=seed, env_id_offset=first, max_episode_steps=1000,
-                           rules=rules)
-
-    def timing_event(self):
-        from gym_narde.vector import TimingEvent
-
-        return TimingEvent(self.device)
-
-    def sync(self):
-        self.torch.cuda.synchronize()
-
-
-def load_engine(local_rank):
-    """GpuEngine, or the test-only host engine NARDE_BENCH_TEST_ENGINE names
-    (tests/bench_host_engine.py: the N-rank plumbing on a CPU-only machine;
-    never a measurement)."""
-    path = os.environ.get("NARDE_BENCH_TEST_ENGINE")
-    if not path:
-        return GpuEngine(local_rank)
-    spec = importlib.util.spec_from_file_location("narde_bench_test_engine", path)
-    mod = importlib.util.module_from_spec(spec)
-    spec.loader.exec_module(mod)
-    return mod.Engine(local_rank)
-
-
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=None,
-                    help="ranks (one per GPU); under torchrun it must equal WORLD_SIZE, otherwise "
-                         "N > 1 starts the N ranks itself (default: WORLD_SIZE, or 1)")
+    ap.add_argument("--gpus", type=int, default=1)
     # 200 launches of 1,000 plies timed, after 100 untimed: the device needs
     # ~100 back-to-back 0.14-ms launches to reach its sustained rate
     # (tools/diag/ramp_rollout.py, DESIGN.md section 6)
@@ -248,17 +182,7 @@ def main():
                     help="PMC summary (tools/pmc_summary.py); default profiles/pmc_k_rollout[_full].json")
     args = ap.parse_args()
 
-    world_env = os.environ.get("WORLD_SIZE")
-    if world_env is None:
-        if args.gpus is not None and args.gpus > 1:
-            # the N ranks, started here before any GPU call (no exec)
-            return spawn_ranks(args.gpus, sys.argv[1:])
-        world_env = "1"
-    world_env = int(world_env)
-    if args.gpus is None:
-        args.gpus = world_env
-    if args.gpus != world_env:
-        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env} ranks were started")
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
     rank_env = int(os.environ.get("RANK", "0"))
     cpu = None
     if world_env == 1 and rank_env == 0 and not args.no_cpu_baseline:
@@ -271,19 +195,15 @@ def main():
     import torch.distributed as dist
 
     from gym_narde import distributed as D
+    from gym_narde.vector import TimingEvent, VecNardeEnv
 
     rank, world, local = D.init_from_env()
-    if world > 1:
-        assert dist.get_world_size() == args.gpus == world, (dist.get_world_size(), args.gpus, world)
-    eng = load_engine(local)
-    dev = eng.device
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
     first, per = D.env_shard(world * args.envs, rank, world)
     is_full4 = args.rules == "full4"
-    env = eng.make_env(per, first, args.seed, args.rules)
-    if eng.name is not None:  # the test-only host engine: the plumbing, no secondary legs
-        args.ramp_launches = 0
-        args.ramp_ms = 0.0
-        args.api_steps = args.fused_launches = args.other_launches = args.dqn_steps = 0
+    env = VecNardeEnv(per, device=dev, seed=args.seed, env_id_offset=first, max_episode_steps=1000,
+                      rules=args.rules)
 
     def barrier():
         if world > 1:
@@ -318,7 +238,7 @@ def main():
             for _ in range(10):
                 ramp()
             ramp_n += 10
-            eng.sync()
+            torch.cuda.synchronize()
         del ramp, rbufs
     ramp_ms = (time.perf_counter() - ramp_t0) * 1e3
 
@@ -332,35 +252,27 @@ def main():
     # invalidates the caches, which lengthens the span it measures by ~1 us
     # at the driver's shape).  The launch path is warmed up untimed.
     K = args.steps
-    ev0, ev1 = eng.timing_event(), eng.timing_event()
+    ev0, ev1 = TimingEvent(dev), TimingEvent(dev)
     sizes = [P] * (K // P) + ([K % P] if K % P else [])
-    # the episode totals land here at every world size: the LAST launch of
-    # the region writes its envs' statistics summed per 256 envs
-    # (narde_rollout_timed's totals rows -- no second launch); at N > 1 the
-    # region ends with the one RCCL all-gather of every rank's rows
-    # (wg_rows(B) x 24 B per rank), summed afterwards
-    rows_buf = torch.empty((-(-per // 256), 3), dtype=torch.int64, device=dev)
     calls = []
     for j, p in enumerate(sizes):
-        last = j == len(sizes) - 1
-        evs = (ev0 if j == 0 else None, ev1 if last else None)
-        calls.append(full_launch if evs == (None, None) else
-                     env.rollout_launcher(p, bufs, events=evs, totals=rows_buf if last else None))
+        evs = (ev0 if j == 0 else None, ev1 if j == len(sizes) - 1 else None)
+        calls.append(full_launch if evs == (None, None) else env.rollout_launcher(p, bufs, events=evs))
     for _ in range(3):
         calls[0]()
         if len(calls) > 1:
             calls[-1]()
-    eng.sync()
+    torch.cuda.synchronize()
     ramp_n += 3 if len(calls) == 1 else 6
 
     run_plies(args.warmup)
-    # every call of the timed region once, untimed: a first call pays one-off
-    # host costs (the first unsqueeze of this process took ~150 us,
-    # tools/diag/after_launch_calls.py; an RCCL collective sets itself up)
-    D.gather_total_rows(rows_buf)
-    eng.sync()
+    # the episode totals land here (VecNardeEnv.totals: one kernel, 64
+    # partial rows); at N > 1 the timed region ends with the one RCCL
+    # all-gather of every rank's rows (1.5 KB per rank), summed afterwards
+    rows_buf = torch.empty((64, 3), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
     barrier()
-    eng.sync()
+    torch.cuda.synchronize()
 
     # HIP events on the launching stream around the launches of the timed
     # region (no per-launch event between them): kernel time per launch =
@@ -372,20 +284,21 @@ def main():
         call()
     launches = sizes
     t_sub = time.perf_counter()
-    gathered = D.gather_total_rows(rows_buf)
-    t_tot = time.perf_counter()
-    eng.sync()
+    if world > 1:
+        gathered = D.gather_total_rows(env.totals(out=rows_buf))
+    torch.cuda.synchronize()
     t_wait = time.perf_counter()
     barrier()
     if world > 1:  # (one process: no barrier, and the device is idle already)
-        eng.sync()
+        torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     gc.enable()
-    host_us = {"submit": round((t_sub - t0) * 1e6, 1), "gather_call": round((t_tot - t_sub) * 1e6, 1),
-               "wait": round((t_wait - t_tot) * 1e6, 1), "close": round((elapsed - (t_wait - t0)) * 1e6, 1)}
+    host_us = {"submit": round((t_sub - t0) * 1e6, 1), "wait": round((t_wait - t_sub) * 1e6, 1),
+               "close": round((elapsed - (t_wait - t0)) * 1e6, 1)}
     span_ms = ev0.elapsed_ms(ev1)
-    rank_totals = gathered.sum(1)  # (world, 3): each rank's {episodes, white pts, black pts}
-    totals = rank_totals
+    if world == 1:
+        gathered = D.gather_total_rows(env.totals(out=rows_buf))
+    totals = gathered.sum(1)
     # algorithmic bytes of every launch in the span (a last partial launch
     # included), and the mean duration of a full-length launch
     span_bytes = sum(launch_bytes(per, p, is_full4) for p in launches)
@@ -402,105 +315,75 @@ def main():
     summary = D.summarize(totals)
 
     # secondary 1: per-ply API kernel k_step (eager, then hipGraph replay)
-    api = None
     S = args.api_steps
-    if S > 0:
-        for _ in range(10):
-            env.step()
+    for _ in range(10):
+        env.step()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(S)]
+    for i in range(S):  # per-launch kernel time (events cost host time: not in the rate below)
+        ev[i][0].record()
+        env.step()
+        ev[i][1].record()
+    torch.cuda.synchronize()
+    step_ms = sum(x.elapsed_time(y) for x, y in ev) / S
+    a0 = time.perf_counter()
+    for i in range(S):
+        env.step()
+    torch.cuda.synchronize()
+    api_eager = per * S / (time.perf_counter() - a0)
+    G = 50
+    graph = torch.cuda.CUDAGraph()
+    cap = torch.cuda.Stream()
+    cap.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(cap):
+        env.step()  # warm the capture stream
         torch.cuda.synchronize()
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(S)]
-        for i in range(S):  # per-launch kernel time (events cost host time: not in the rate below)
-            ev[i][0].record()
-            env.step()
-            ev[i][1].record()
-        torch.cuda.synchronize()
-        step_ms = sum(x.elapsed_time(y) for x, y in ev) / S
-        a0 = time.perf_counter()
-        for i in range(S):
-            env.step()
-        torch.cuda.synchronize()
-        api_eager = per * S / (time.perf_counter() - a0)
-        G = 50
-        graph = torch.cuda.CUDAGraph()
-        cap = torch.cuda.Stream()
-        cap.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(cap):
-            env.step()  # warm the capture stream
-            torch.cuda.synchronize()
-            with torch.cuda.graph(graph, stream=cap):
-                for _ in range(G):
-                    env.step()
-        torch.cuda.current_stream().wait_stream(cap)
+        with torch.cuda.graph(graph, stream=cap):
+            for _ in range(G):
+                env.step()
+    torch.cuda.current_stream().wait_stream(cap)
+    graph.replay()
+    torch.cuda.synchronize()
+    reps = max(1, S // G)
+    g0 = time.perf_counter()
+    for _ in range(reps):
         graph.replay()
-        torch.cuda.synchronize()
-        reps = max(1, S // G)
-        g0 = time.perf_counter()
-        for _ in range(reps):
-            graph.replay()
-        torch.cuda.synchronize()
-        api_graph = per * G * reps / (time.perf_counter() - g0)
-        api = {
-            "kernel": "k_step (one ply per launch, same outputs)",
-            "eager": round(api_eager, 1),
-            "hipgraph": round(api_graph, 1),
-            "unit": "env steps/s",
-            "kernel_ms": round(step_ms, 5),
-            "achieved_GBps": round(((OUT_BYTES_PER_STEP_FULL if is_full4 else OUT_BYTES_PER_STEP) + RECORD_BYTES)
-                                   * per / (step_ms * 1e-3) / 1e9, 2),
-        }
+    torch.cuda.synchronize()
+    api_graph = per * G * reps / (time.perf_counter() - g0)
 
     # secondary 2: fused self-play with no per-ply outputs (statistics only)
-    fused = None
     F = args.fused_plies
-    if args.fused_launches > 0:
+    env.selfplay(F)
+    torch.cuda.synchronize()
+    f0 = time.perf_counter()
+    for _ in range(args.fused_launches):
         env.selfplay(F)
-        torch.cuda.synchronize()
-        f0 = time.perf_counter()
-        for _ in range(args.fused_launches):
-            env.selfplay(F)
-        torch.cuda.synchronize()
-        fused = {
-            "kernel": f"k_rollout without per-ply outputs, {F} plies per launch",
-            "value": round(per * F * args.fused_launches / (time.perf_counter() - f0), 1),
-            "unit": "env steps/s",
-        }
+    torch.cuda.synchronize()
+    fused = per * F * args.fused_launches / (time.perf_counter() - f0)
 
     # secondary 3: the other rules mode through the same rollout kernel shape
     other_rules = "ref2" if is_full4 else "full4"
-    other = None
-    if args.other_launches > 0:
-        env_o = eng.make_env(per, first, args.seed, other_rules)
-        bufs_o = env_o.rollout_buffers(P)
+    env_o = VecNardeEnv(per, device=dev, seed=args.seed, env_id_offset=first, max_episode_steps=1000,
+                        rules=other_rules)
+    bufs_o = env_o.rollout_buffers(P)
+    env_o.rollout(P, bufs_o)
+    env_o.rollout(P, bufs_o)
+    torch.cuda.synchronize()
+    ev_o = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            for _ in range(args.other_launches)]
+    o0 = time.perf_counter()
+    for s_, e_ in ev_o:
+        s_.record()
         env_o.rollout(P, bufs_o)
-        env_o.rollout(P, bufs_o)
-        torch.cuda.synchronize()
-        ev_o = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                for _ in range(args.other_launches)]
-        o0 = time.perf_counter()
-        for s_, e_ in ev_o:
-            s_.record()
-            env_o.rollout(P, bufs_o)
-            e_.record()
-        torch.cuda.synchronize()
-        other_rate = per * P * args.other_launches / (time.perf_counter() - o0)
-        other_ms = sum(s_.elapsed_time(e_) for s_, e_ in ev_o) / len(ev_o)
-        other_M = None
-        if other_rules == "full4":
-            M = ((bufs_o["legal"] >> 56) & 7).flatten()
-            other_M = [round(float(x), 4) for x in (torch.bincount(M, minlength=5).double() / M.numel()).tolist()]
-        env_o.close()
-        obytes = launch_bytes(per, P, not is_full4)
-        other = {
-            "rules": other_rules,
-            "kernel": f"{kernel_name(other_rules == 'full4', P)} ({other_rules.upper()}), {P} plies per launch, all outputs",
-            "value": round(other_rate, 1),
-            "unit": "env steps/s",
-            "kernel_ms": round(other_ms, 5),
-            "bytes_per_launch": obytes,
-            "achieved_GBps": round(obytes / (other_ms * 1e-3) / 1e9, 2),
-            "frac": round(obytes / (other_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
-            "max_dice_hist": other_M,
-        }
+        e_.record()
+    torch.cuda.synchronize()
+    other_rate = per * P * args.other_launches / (time.perf_counter() - o0)
+    other_ms = sum(s_.elapsed_time(e_) for s_, e_ in ev_o) / len(ev_o)
+    other_M = None
+    if other_rules == "full4":
+        M = ((bufs_o["legal"] >> 56) & 7).flatten()
+        other_M = [round(float(x), 4) for x in (torch.bincount(M, minlength=5).double() / M.numel()).tolist()]
+    env_o.close()
 
     # secondary 4: configs[3] -- the batched DQN driver (198-d obs + legal
     # masks -> DecomposedDQN -> env step -> device replay -> one PER update)
@@ -510,7 +393,8 @@ def main():
 
         tuned = use_tuned_gemms()  # TunableOp GEMM choices measured on MI355X
 
-        env_q = eng.make_env(per, first, args.seed + 1, "ref2")
+        env_q = VecNardeEnv(per, device=dev, seed=args.seed + 1, env_id_offset=first,
+                            max_episode_steps=1000)
         drv = BatchedDQNDriver(env_q, obs="tesauro198", train_batch=args.dqn_train_batch,
                                capacity=max(1 << 20, 4 * per))
         for _ in range(5):
@@ -571,6 +455,7 @@ def main():
             traffic = load_traffic(tj, per, P)
             if traffic is not None:
                 break
+        obytes = launch_bytes(per, P, not is_full4)
         # what each rules mode is, and which BASELINE.json config it times
         rules_txt = {
             "ref2": ("REF2 = the reference's NardeEnv.step (narde_env.py:27-103: <=2 checker moves "
@@ -621,14 +506,6 @@ def main():
                 "global_envs": world * per,
                 "parallelism": f"dp{world} (env-id shards, 1 RCCL all-gather of episode totals)",
                 "episodes_finished": summary["episodes"],
-                # every rank's {episodes, white points, black points}, as gathered in the timed region
-                "rank_totals": rank_totals.tolist(),
-                "collective": {"backend": dist.get_backend() if dist.is_initialized() else None,
-                               "world_size": dist.get_world_size() if dist.is_initialized() else 1,
-                               "timed": (f"the last launch writes its {rows_buf.shape[0]} per-256-env totals "
-                                         f"rows; all_gather_into_tensor of them ({rows_buf.shape[0] * 24} B per rank)"
-                                         if world > 1 else f"the last launch writes its {rows_buf.shape[0]} "
-                                         "per-256-env totals rows (no process group at N=1)")},
             },
             "roofline": {
                 "bound": "hbm",
@@ -645,16 +522,35 @@ def main():
             # waiting for them (and the gather), the closing barrier + sync
             "timed_region_host_us": host_us,
             "cpu_baseline": cpu,
-            "api_step": api,
-            "other_rules": other,
+            "api_step": {
+                "kernel": "k_step (one ply per launch, same outputs)",
+                "eager": round(api_eager, 1),
+                "hipgraph": round(api_graph, 1),
+                "unit": "env steps/s",
+                "kernel_ms": round(step_ms, 5),
+                "achieved_GBps": round(((OUT_BYTES_PER_STEP_FULL if is_full4 else OUT_BYTES_PER_STEP) + RECORD_BYTES)
+                                       * per / (step_ms * 1e-3) / 1e9, 2),
+            },
+            "other_rules": {
+                "rules": other_rules,
+                "workload": f"{config_txt[other_rules]}; rules = {rules_txt[other_rules]}",
+                "parity": parity_txt[other_rules],
+                "kernel": f"{kernel_name(other_rules == 'full4', P)} ({other_rules.upper()}), {P} plies per launch, all outputs",
+                "value": round(other_rate, 1),
+                "unit": "env steps/s",
+                "kernel_ms": round(other_ms, 5),
+                "bytes_per_launch": obytes,
+                "achieved_GBps": round(obytes / (other_ms * 1e-3) / 1e9, 2),
+                "frac": round(obytes / (other_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                "max_dice_hist": other_M,
+            },
             "config4_dqn": dqn,
-            "selfplay_stats_only": fused,
+            "selfplay_stats_only": {
+                "kernel": f"k_rollout without per-ply outputs, {F} plies per launch",
+                "value": round(fused, 1),
+                "unit": "env steps/s",
+            },
         }
-        if other is not None:
-            other["workload"] = f"{config_txt[other_rules]}; rules = {rules_txt[other_rules]}"
-            other["parity"] = parity_txt[other_rules]
-        if eng.name is not None:
-            line["engine"] = eng.name
         print(json.dumps(line), flush=True)
     env.close()
     if world > 1:
@@ -662,4 +558,4 @@ def main():
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    main()
