@@ -354,10 +354,25 @@ def main():
     ramp_n += 3 if len(calls) == 1 else 6
 
     run_plies(args.warmup)
+    # the rows' all-gather at N > 1: RCCL's own ncclAllGather on the
+    # launching stream (D.RcclGather, one library call) -- ProcessGroupNCCL's
+    # all_gather_into_tensor costs ~80 us of host time after a marked launch
+    # (tools/diag/launch_after_marker.py); the process group's collective if
+    # RCCL's C API cannot be set up
+    rows_view = D.gather_total_rows(rows_buf)  # one rank: the (1, R, 3) view, no collective
+    gather, gather_impl = (lambda: rows_view), "none (one rank)"
+    if world > 1:
+        gather = lambda: D.gather_total_rows(rows_buf)  # noqa: E731
+        gather_impl = "ProcessGroup all_gather_into_tensor"
+        if dist.get_backend() == "nccl":
+            try:
+                gather, gather_impl = D.RcclGather(rows_buf), "ncclAllGather (RCCL C API, launching stream)"
+            except (OSError, RuntimeError, AttributeError) as exc:
+                gather_impl += f" (RCCL C API unavailable: {exc})"
     # every call of the timed region once, untimed: a first call pays one-off
     # host costs (the first unsqueeze of this process took ~150 us,
     # tools/diag/after_launch_calls.py; an RCCL collective sets itself up)
-    D.gather_total_rows(rows_buf)
+    gather()
     eng.sync()
     barrier()
     eng.sync()
@@ -372,19 +387,24 @@ def main():
         call()
     launches = sizes
     t_sub = time.perf_counter()
-    gathered = D.gather_total_rows(rows_buf)
+    gathered = gather()
     t_tot = time.perf_counter()
     eng.sync()
-    t_wait = time.perf_counter()
+    # the region ends when this rank's stream has run its launches and the
+    # all-gather -- which completes only once EVERY rank's rows are in, so
+    # no rank stops its clock before the slowest rank's last launch is done;
+    # the closing barrier follows, and the max over ranks is taken
+    elapsed = time.perf_counter() - t0
     barrier()
     if world > 1:  # (one process: no barrier, and the device is idle already)
         eng.sync()
-    elapsed = time.perf_counter() - t0
+    t_close = time.perf_counter() - t0
     gc.enable()
     host_us = {"submit": round((t_sub - t0) * 1e6, 1), "gather_call": round((t_tot - t_sub) * 1e6, 1),
-               "wait": round((t_wait - t_tot) * 1e6, 1), "close": round((elapsed - (t_wait - t0)) * 1e6, 1)}
+               "wait": round((elapsed - (t_tot - t0)) * 1e6, 1),
+               "closing_barrier_untimed": round((t_close - elapsed) * 1e6, 1)}
     span_ms = ev0.elapsed_ms(ev1)
-    rank_totals = gathered.sum(1)  # (world, 3): each rank's {episodes, white pts, black pts}
+    rank_totals = gathered.sum(1).cpu()  # (world, 3): each rank's {episodes, white pts, black pts}
     totals = rank_totals
     # algorithmic bytes of every launch in the span (a last partial launch
     # included), and the mean duration of a full-length launch
@@ -626,9 +646,13 @@ def main():
                 "collective": {"backend": dist.get_backend() if dist.is_initialized() else None,
                                "world_size": dist.get_world_size() if dist.is_initialized() else 1,
                                "timed": (f"the last launch writes its {rows_buf.shape[0]} per-256-env totals "
-                                         f"rows; all_gather_into_tensor of them ({rows_buf.shape[0] * 24} B per rank)"
+                                         f"rows; one all-gather of them ({rows_buf.shape[0] * 24} B per rank)"
                                          if world > 1 else f"the last launch writes its {rows_buf.shape[0]} "
-                                         "per-256-env totals rows (no process group at N=1)")},
+                                         "per-256-env totals rows (no process group at N=1)"),
+                               "impl": gather_impl,
+                               "region_end": "this rank's synchronize after the all-gather (complete only once "
+                                             "every rank's rows are in); the closing barrier is untimed; max over "
+                                             "ranks"},
             },
             "roofline": {
                 "bound": "hbm",

@@ -7,6 +7,7 @@ bit for bit.  The only collective is one all_gather_into_tensor of the
 per-env statistics {episodes, white points, black points} at the end of a
 run (backend "nccl" = RCCL over xGMI on ROCm; "gloo" on CPU for tests).
 """
+import ctypes
 import os
 
 import torch
@@ -99,3 +100,74 @@ def summarize(stats):
     """{episodes, white_points, black_points} of a (B, 3) statistics tensor."""
     s = stats.to(torch.int64).sum(0).tolist()
     return {"episodes": int(s[0]), "white_points": int(s[1]), "black_points": int(s[2])}
+
+
+# ---------------------------------------------------------------- RCCL, direct
+_NCCL_INT64 = 4  # ncclDataType_t ncclInt64 (rccl.h)
+
+
+class _NcclUniqueId(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]  # NCCL_UNIQUE_ID_BYTES
+
+
+def _rccl():
+    """The RCCL library torch's ProcessGroupNCCL already uses (torch/lib)."""
+    path = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    lib = ctypes.CDLL(path if os.path.exists(path) else "librccl.so.1")
+    lib.ncclGetUniqueId.argtypes = [ctypes.POINTER(_NcclUniqueId)]
+    lib.ncclCommInitRank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, _NcclUniqueId, ctypes.c_int]
+    lib.ncclAllGather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p,
+                                  ctypes.c_void_p]
+    lib.ncclCommDestroy.argtypes = [ctypes.c_void_p]
+    lib.ncclGetErrorString.argtypes = [ctypes.c_int]
+    lib.ncclGetErrorString.restype = ctypes.c_char_p
+    return lib
+
+
+class RcclGather:
+    """gather_total_rows through RCCL's own C API: one ncclAllGather on the
+    caller's stream (ring / direct xGMI transfers of every rank's rows into
+    every rank's (world, R, 3) buffer) -- one library call in the timed
+    region, where ProcessGroupNCCL's all_gather_into_tensor adds its stream
+    and event bookkeeping on the host (~20 us after a bare launch, ~80 us
+    after a launch bracketed by timing markers: tools/diag/launch_after_marker.py).
+    Built collectively from an initialised process group (the unique id is
+    broadcast through it); the same bytes as gather_total_rows."""
+
+    def __init__(self, rows):
+        self.lib = _rccl()
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        uid = _NcclUniqueId()
+        if self.rank == 0:
+            self._check(self.lib.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
+        dev = rows.device
+        idb = ctypes.string_at(ctypes.addressof(uid), 128)  # (c_char arrays stop at a NUL)
+        raw = torch.tensor(list(idb), dtype=torch.uint8, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.broadcast(raw, 0)
+        uid = _NcclUniqueId()
+        ctypes.memmove(ctypes.addressof(uid), bytes(raw.cpu().tolist()), 128)
+        self.comm = ctypes.c_void_p()
+        self._check(self.lib.ncclCommInitRank(ctypes.byref(self.comm), self.world, uid, self.rank),
+                    "ncclCommInitRank")
+        self.src = rows
+        self.out = torch.empty((self.world,) + tuple(rows.shape), dtype=rows.dtype, device=dev)
+        self.count = rows.numel()
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed ({rc}): {self.lib.ncclGetErrorString(rc).decode()}")
+
+    def __call__(self, stream=None):
+        """All-gather the rows tensor given at construction (its current
+        contents) on `stream` (default: torch's current stream of its
+        device); returns the (world, R, 3) output."""
+        st = stream if stream is not None else torch.cuda.current_stream(self.src.device).cuda_stream
+        self._check(self.lib.ncclAllGather(ctypes.c_void_p(self.src.data_ptr()), ctypes.c_void_p(self.out.data_ptr()),
+                                           self.count, _NCCL_INT64, self.comm, ctypes.c_void_p(st)),
+                    "ncclAllGather")
+        return self.out
+
+    def close(self):
+        if self.comm:
+            self.lib.ncclCommDestroy(self.comm)
+            self.comm = ctypes.c_void_p()

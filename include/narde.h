@@ -77,8 +77,11 @@ int64_t narde_num_envs(const narde_env *env);
  * Philox4x32-10(ctr = {t, global_env_id, 0, 0}, key = seed).  Because t lives
  * in device state, narde_step / narde_rollout launches can be captured in a
  * hipGraph and replayed.  get_ply reads env 0's counter and set_ply sets
- * every env's counter; both synchronise the whole device first, so work
- * queued on any stream is ordered before them. */
+ * every env's counter; both synchronise the whole device first
+ * (hipDeviceSynchronize), so work queued on any stream is ordered before
+ * them -- a device-wide barrier: they also wait for every other stream of
+ * the process on that device, unrelated work (training, other handles)
+ * included.  Neither belongs in a hot loop. */
 int narde_get_ply(const narde_env *env, uint32_t *t);
 int narde_set_ply(narde_env *env, uint32_t t);
 

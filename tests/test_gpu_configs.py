@@ -318,6 +318,21 @@ assert tot.is_cuda and tot.shape == (1, 3) and torch.equal(tot[0], st.to(torch.i
 rows = D.gather_total_rows(env.totals())  # the bench's timed-region gather: one kernel + one all-gather
 torch.cuda.synchronize()
 assert rows.is_cuda and rows.shape == (1, 64, 3) and torch.equal(rows.sum(1), tot)
+# the bench's timed-region gather at N > 1: the last launch's per-256-env
+# totals rows through RCCL's own ncclAllGather (D.RcclGather)
+from gym_narde import _lib
+wrows = torch.empty((_lib.wg_rows(8192), 3), dtype=torch.int64, device="cuda:0")
+L = env.rollout_launcher(20, env.rollout_buffers(20), totals=wrows)
+L()
+G = D.RcclGather(wrows)
+out = G()
+torch.cuda.synchronize()
+assert out.shape == (1,) + tuple(wrows.shape) and torch.equal(out[0], wrows)
+L()
+out = G()  # the rows of the next launch, same buffers
+torch.cuda.synchronize()
+assert torch.equal(out[0], wrows) and torch.equal(wrows.sum(0), env.stats().long().sum(0))
+G.close()
 t = torch.tensor([1.5, 2.5], dtype=torch.float64, device="cuda:0")
 dist.all_reduce(t, op=dist.ReduceOp.MAX)  # the bench's max-over-ranks timing
 dist.barrier()

@@ -6,7 +6,8 @@ totals call (tools/diag/gpu_benchcmp2.sh).  For each case: the host time of
 the second call (first occurrence after a fresh handle, then the median of
 20 repeats), and the whole region (launch + second call + synchronize).
 Second calls: the totals kernel (pre-bound), a torch op on the same stream,
-an RCCL all-gather on a world-1 process group.  argv: plies (20)."""
+an RCCL all-gather on a world-1 process group (ProcessGroupNCCL, and
+RCCL's own ncclAllGather through gym_narde.distributed.RcclGather).  argv: plies (20)."""
 import json
 import os
 import sys
@@ -37,8 +38,12 @@ def main():
     rows = torch.empty((64, 3), dtype=torch.int64, device="cuda:0")
     gat = torch.empty((1, 64, 3), dtype=torch.int64, device="cuda:0")
     x = torch.zeros(16, device="cuda:0")
+    from gym_narde.distributed import RcclGather
+
+    G = RcclGather(rows)
     seconds = {"totals": env.totals_launcher(rows), "torch_add": lambda: x.add_(1.0),
-               "allgather": lambda: dist.all_gather_into_tensor(gat, rows.unsqueeze(0))}
+               "allgather": lambda: dist.all_gather_into_tensor(gat, rows.unsqueeze(0)),
+               "rccl_direct": G}
     for f in seconds.values():  # every path once
         f()
     torch.cuda.synchronize()
