@@ -260,6 +260,12 @@ def main():
     if args.gpus != world_env:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env} ranks were started")
     rank_env = int(os.environ.get("RANK", "0"))
+    if rank_env != 0:
+        # ONE JSON line on stdout, from rank 0: the other ranks' stdout (RCCL /
+        # gloo print banners there at init) goes to /dev/null, fd level
+        devnull = os.open(os.devnull, os.O_WRONLY)
+        os.dup2(devnull, 1)
+        os.close(devnull)
     cpu = None
     if world_env == 1 and rank_env == 0 and not args.no_cpu_baseline:
         cores, how = available_cores()
@@ -679,7 +685,9 @@ def main():
             other["parity"] = parity_txt[other_rules]
         if eng.name is not None:
             line["engine"] = eng.name
-        print(json.dumps(line), flush=True)
+        # (a fresh line: a library banner on stdout may lack its newline)
+        sys.stdout.write("\n" + json.dumps(line) + "\n")
+        sys.stdout.flush()
     env.close()
     if world > 1:
         dist.destroy_process_group()
