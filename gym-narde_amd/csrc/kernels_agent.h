@@ -351,6 +351,27 @@ __global__ void __launch_bounds__(kBlock) k_play_set(Planes pl, int n, Rng g, co
   count[i] = play_walk(s, d0, d1, kind, l, [&](int k, int p, int, uint32_t w, bool) { row[k * 24 + p] = w; });
 }
 
+// act()'s greedy candidate masks per env (narde_rules.h act_masks): move1
+// NULL -- the move-1 codes of list #1; else the move-2 codes act() offers
+// after each env's move1[i] (pre-move lists).  u64[n][9].
+__global__ void __launch_bounds__(kBlock) k_act_masks(Planes pl, int n, Rng g, const uint8_t* __restrict__ dice,
+                                                      const int64_t* __restrict__ move1, int64_t ld_move1,
+                                                      uint64_t* __restrict__ mask) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const Side s = side_from_record(pl.p0[i], pl.p1[i]);
+  uint64_t m[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int d0, d1;
+  if (play_dice(s, g, i, dice, d0, d1)) {
+    Legal l;
+    legal2(s, d0, d1, l);
+    const int64_t c = move1 ? move1[(size_t)i * (size_t)ld_move1] : -1;
+    act_masks(s, d0, d1, l, c < 0 ? -1 : (c > 575 ? 576 : (int)c), m);
+  }
+#pragma unroll
+  for (int q = 0; q < 9; ++q) mask[(size_t)i * 9 + q] = m[q];
+}
+
 // The batched driver's exploration (train_deepq_pytorch.py:514-515:
 // np.random.rand() <= epsilon, then random.choice(valid_move_combinations)):
 // the rows whose shared explore draw (Philox4x32-10({tag, row, 0, 5}, seed)

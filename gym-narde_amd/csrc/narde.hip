@@ -517,6 +517,16 @@ int narde_play_set(narde_env* e, const uint8_t* dice, int kind, uint64_t* legal,
   return check_launch("k_play_set");
 }
 
+int narde_act_masks(narde_env* e, const uint8_t* dice, const int64_t* move1, int64_t ld_move1, uint64_t* mask,
+                    void* stream) {
+  if (!e || !mask) return fail(NARDE_EINVAL, "NULL argument");
+  if (move1 && ld_move1 < 1) return fail(NARDE_EINVAL, "bad move1 stride");
+  DeviceGuard dg(e->device);
+  k_act_masks<<<grid(e->n), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n, rng_of(e), dice, move1, ld_move1,
+                                                              mask);
+  return check_launch("k_act_masks");
+}
+
 int narde_explore_plays(narde_env* e, const uint8_t* dice, const float* epsilon, uint64_t seed, const int64_t* tag,
                         int64_t* out, int64_t ld_out, void* stream) {
   if (!e || !epsilon || !tag || !out) return fail(NARDE_EINVAL, "NULL argument");

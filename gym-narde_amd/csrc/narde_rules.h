@@ -618,6 +618,32 @@ NARDE_FN void play_codes_act(const Side& s, int d0, int d1, const Legal& l, int 
   });
 }
 
+// DQNAgent.act's greedy candidate sets (train_deepq_pytorch.py:520-560) as
+// 576-bit masks m[9]: move1 < 0 -- the codes of list #1's entries
+// (valid_first_moves' keys, :526); else valid_first_moves[move1]: the move-2
+// codes act() listed for the LAST list-#1 entry coded move1 (the dict entry
+// is reset at every occurrence, :474), {0} when that list is empty, nothing
+// when no entry has that code.
+NARDE_FN void act_masks(const Side& s, int d0, int d1, const Legal& l, int move1, uint64_t m[9]) {
+  for (int q = 0; q < 9; ++q) m[q] = 0ull;
+  uint32_t last = 0u;
+  play_walk(s, d0, d1, kPlayAct, l, [&](int, int p, int die, uint32_t word, bool) {
+    const int c = encode_move(p, p < die ? OFF : p - die);
+    if (move1 < 0) m[c >> 6] |= 1ull << (c & 63);
+    else if (c == move1) last = word;
+  });
+  if (move1 < 0 || !last) return;
+  uint32_t src = last & 0xFFFFFFu;
+  const int rem = (int)((last >> 24) & 7u);
+  if (!src) m[0] |= 1ull;  // (move 1, 0)
+  while (src) {
+    const int q = __builtin_ctz(src);
+    src &= src - 1u;
+    const int c = encode_move(q, q < rem ? OFF : q - rem);
+    m[c >> 6] |= 1ull << (c & 63);
+  }
+}
+
 // ============================================================ FULL4 turns
 // Build extension: one
 // step = the mover's WHOLE turn -- four sub-moves on doubles, the

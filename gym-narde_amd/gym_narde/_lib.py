@@ -60,6 +60,7 @@ SIGNATURES = {
     "narde_legal_mask576": (_i32, [_vp, _vp, _vp]),
     "narde_legal_mask576_move2": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "narde_play_set": (_i32, [_vp, _vp, _i32, _vp, _vp, _vp, _vp]),
+    "narde_act_masks": (_i32, [_vp, _vp, _vp, _i64, _vp, _vp]),
     "narde_explore_plays": (_i32, [_vp, _vp, _vp, _u64, _vp, _vp, _i64, _vp]),
     "narde_policy_masked_argmax576": (_i32, [_i32, _vp, _i64, _vp, _i64, ctypes.c_float, _u64, _u32,
                                              _i32, _vp, _vp]),

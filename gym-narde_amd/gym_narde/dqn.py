@@ -16,11 +16,14 @@ without leaving the GPU:
   move-2 mask   VecNardeEnv.legal_mask_move2()  (k_mask576_move2: the codes
                 step accepts after the chosen move 1 -- the reference's act()
                 guesses them from the pre-move board, :452-503)
+                (greedy="reference": act()'s own candidate sets instead,
+                VecNardeEnv.act_masks, k_act_masks)
   Q-values      DecomposedDQN, the reference's architecture and parameter
                 names (:184-277), so its checkpoints load; move-2 Q-values
                 use the column-gather identity below instead of a one-hot
                 concat GEMM
-  policy        masked epsilon-greedy (explore: uniform over legal codes)
+  policy        masked epsilon-greedy; explore="plays": random.choice over
+                act()'s (move1, move2) combinations (k_explore_plays, :514-515)
   env step      VecNardeEnv.step(actions)  (k_step, auto-reset)
   replay        DeviceReplay: prioritized replay with the reference's
                 alpha/beta/epsilon rules on device tensors (:279-342)
@@ -583,7 +586,7 @@ class BatchedDQNDriver:
                  learning_rate=1e-4, gamma=0.99, epsilon=1.0, epsilon_min=0.01,
                  epsilon_decay=0.995, target_update=10, updates_per_step=1, shaping=True,
                  seed=0, fused=True, fused_heads=True, gathered_heads=True, fused_features=True,
-                 explore="plays"):
+                 explore="plays", greedy="accepted"):
         if env.full:
             raise ValueError("the DQN driver plays the reference's (move1, move2) actions: rules='ref2'")
         if explore not in ("plays", "codes"):
@@ -593,6 +596,13 @@ class BatchedDQNDriver:
         # moves listed on the pre-move board), k_explore_plays; "codes" = each
         # head uniform over its own legal codes (the policy kernels alone)
         self.explore = explore
+        if greedy not in ("accepted", "reference"):
+            raise ValueError("greedy must be 'accepted' or 'reference'")
+        # the greedy branch's candidate sets: "accepted" = the codes the step
+        # executes (move 1 it accepts, move 2 it accepts after that move 1,
+        # post-move); "reference" = act()'s own (valid_first_moves' keys,
+        # then valid_first_moves[move1]: pre-move lists, :520-560)
+        self.greedy = greedy
         self.env, self.dev = env, env.device
         self.obs_kind = obs
         self.state_size = 198 if obs == "tesauro198" else 24
@@ -674,9 +684,12 @@ class BatchedDQNDriver:
     def act(self, x):
         """Masked epsilon-greedy (move1, move2) codes for the next step: the
         env's exact legal masks and the fused policy kernel (epsilon and the
-        step tag read from device memory).  Greedy: move 1 = the masked
-        argmax over the move-1 codes the step accepts, move 2 = the masked
-        argmax over the codes the step accepts after it (post-move).
+        step tag read from device memory).  Greedy (greedy="accepted"):
+        move 1 = the masked argmax over the move-1 codes the step accepts,
+        move 2 = the masked argmax over the codes the step accepts after it
+        (post-move); greedy="reference": over act()'s own candidate sets
+        (narde_act_masks: list #1's codes, then the pre-move second list of
+        that move 1, :520-560).
         Exploring rows (one shared draw per row and step): explore="plays"
         draws one of act()'s (move1, move2) combinations uniformly
         (k_explore_plays), as random.choice(valid_move_combinations)."""
@@ -689,17 +702,19 @@ class BatchedDQNDriver:
             h1, h2 = self.model.move1_head, self.model.move2_head
             acts = torch.empty((x.shape[0], 2), dtype=torch.int64, device=self.dev)
             m1 = torch.empty(x.shape[0], dtype=torch.int16, device=self.dev)
-            head_policy_576(f, h1.weight, h1.bias, self.env.legal_mask(), self.eps_t, self.seed, self.tag_t, 0,
-                            out=acts[:, 0], out16=m1)
-            m2 = self.env.legal_mask_move2(m1)
+            ref = self.greedy == "reference"
+            head_policy_576(f, h1.weight, h1.bias, self.env.act_masks() if ref else self.env.legal_mask(),
+                            self.eps_t, self.seed, self.tag_t, 0, out=acts[:, 0], out16=m1)
+            m2 = self.env.act_masks(move1=acts[:, 0]) if ref else self.env.legal_mask_move2(m1)
             head_policy_576(f, h2.weight, h2.bias, m2, self.eps_t, self.seed, self.tag_t, 1, out=acts[:, 1],
                             move1=acts[:, 0])
             if self.explore == "plays":
                 self.env.explore_plays(acts, self.eps_t, self.seed, self.tag_t)
             return acts
-        a1 = policy_576(self.model.move1_head(f), self.env.legal_mask(), self.eps_t, self.seed,
-                        self.tag_t, 0)
-        m2 = self.env.legal_mask_move2(a1.to(torch.int16))
+        ref = self.greedy == "reference"
+        a1 = policy_576(self.model.move1_head(f), self.env.act_masks() if ref else self.env.legal_mask(), self.eps_t,
+                        self.seed, self.tag_t, 0)
+        m2 = self.env.act_masks(move1=a1) if ref else self.env.legal_mask_move2(a1.to(torch.int16))
         # move-2 Q = (f @ Wf^T + b) + Wm[:, move1]: the column add is fused
         # into the policy kernel (rows of Wm^T, a 1.3 MB transpose per step)
         w = self.model.move2_head.weight

@@ -293,6 +293,24 @@ class VecNardeEnv:
         self._keep = (d,)
         return legal, words, count
 
+    def act_masks(self, move1=None, dice=None, out=None):
+        """DQNAgent.act's greedy candidate sets (narde_act_masks) as (B,9)
+        int64 576-bit masks: move1 None -- the move-1 codes of list #1
+        (valid_first_moves' keys); move1 (B,) int64 (any positive stride)
+        -- the move-2 codes act() offers after it (the pre-move second list
+        of the last list-#1 entry with that code; code 0 alone if empty)."""
+        B, t = self.num_envs, self.torch
+        d = None if dice is None else self._dev(dice, t.uint8, (B, 2))
+        if move1 is not None and (move1.dtype != t.int64 or move1.dim() != 1 or move1.shape[0] != B
+                                  or move1.device != self.device or move1.stride(0) < 1):
+            raise ValueError(f"move1 must be ({B},) int64 on the env's device")
+        if out is None:
+            out = t.empty((B, 9), dtype=t.int64, device=self.device)
+        self.handle.call("narde_act_masks", _lib.ptr(d), _lib.ptr(move1),
+                         move1.stride(0) if move1 is not None else 1, _lib.ptr(out), self._s())
+        self._keep = (d, move1)
+        return out
+
     def explore_plays(self, actions, epsilon, seed, tag, dice=None):
         """The DQN driver's exploration (narde_explore_plays): rows whose
         explore draw ({tag, row, 0, 5}, seed) is below epsilon get a play

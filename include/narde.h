@@ -260,6 +260,17 @@ int narde_legal_mask576_move2(narde_env *env, const int16_t *move1, const uint8_
 int narde_play_set(narde_env *env, const uint8_t *dice, int kind, uint64_t *legal, uint32_t *table,
                    int32_t *count, void *stream);
 
+/* DQNAgent.act's greedy candidate sets (train_deepq_pytorch.py:520-560) as
+ * 576-bit masks u64[B][9], for dice u8[B][2] in roll order (NULL = the next
+ * step's device dice).  move1 NULL: bit c set iff c is the code act() gives
+ * some list-#1 entry (valid_first_moves' keys).  move1 int64 (element i at
+ * move1[i * ld_move1]): the move-2 codes act() offers after move 1 --
+ * valid_first_moves[move1]: the pre-move second list of the LAST list-#1
+ * entry with that code, bit 0 alone if that list is empty, no bit if no
+ * entry has that code. */
+int narde_act_masks(narde_env *env, const uint8_t *dice, const int64_t *move1, int64_t ld_move1,
+                    uint64_t *mask, void *stream);
+
 /* The DQN driver's exploration (train_deepq_pytorch.py:514-515): for the
  * rows whose explore draw Philox4x32-10({*tag, row, 0, 5}, seed) r0 <
  * *epsilon * 2^32 (the policy kernels' shared decision), writes play

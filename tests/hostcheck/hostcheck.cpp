@@ -123,6 +123,17 @@ int hc_play_codes_act(const int8_t* board, const uint8_t* off, const uint8_t* ft
   return cnt;
 }
 
+// k_act_masks' per-lane body; move1 < 0 = the move-1 mask
+void hc_act_masks(int64_t n, const int8_t* board, const uint8_t* off, const uint8_t* ft, const int8_t* player,
+                  const uint8_t* dice, const int16_t* move1, uint64_t* mask) {
+  for (int64_t i = 0; i < n; ++i) {
+    const Side s = load(board + i * 24, off + 2 * i, ft + 2 * i, player[i], 0);
+    Legal l;
+    legal2(s, dice[2 * i], dice[2 * i + 1], l);
+    act_masks(s, dice[2 * i], dice[2 * i + 1], l, move1 ? move1[i] : -1, mask + 9 * i);
+  }
+}
+
 void hc_reset_batch(int64_t n, int64_t env0, uint64_t seed, uint32_t epoch, int8_t* board,
                     uint8_t* off, uint8_t* ft, int8_t* player, uint16_t* elapsed) {
   for (int64_t i = 0; i < n; ++i) {

@@ -180,3 +180,56 @@ def test_driver_explores_over_act_combinations():
     assert bool((ok | quirk).all())
     assert float(ok.float().mean()) > 0.8
     env.close()
+
+
+def test_act_masks_reproduce_reference_greedy_act():
+    """k_act_masks (VecNardeEnv.act_masks) + the policy kernel on the
+    Q-values the reference's DQNAgent.act was given
+    (tests/golden/act_greedy.npz, tools/capture_act_greedy.py): the same
+    greedy (move1, move2) as the reference on 2,500 trainer steps."""
+    from gym_narde.dqn import policy_576
+
+    t = golden("trainer.npz")
+    a = golden("act_greedy.npz")
+    rows = a["step"]
+    env = _env_at(t["pre_board"][rows], t["pre_off"][rows], t["pre_ft"][rows], t["player"][rows])
+    tab = np.random.default_rng(int(a["meta"][2])).standard_normal((576, 576)).astype(np.float32)
+    q1 = np.stack([np.random.default_rng(int(a["meta"][0]) + int(i)).standard_normal(576).astype(np.float32)
+                   for i in rows])
+    b2 = np.stack([np.random.default_rng(int(a["meta"][1]) + int(i)).standard_normal(576).astype(np.float32)
+                   for i in rows])
+    dice = torch.as_tensor(t["dice"][rows], device="cuda:0")
+    m1 = env.act_masks(dice=dice)
+    a1 = policy_576(torch.as_tensor(q1, device="cuda:0"), m1, 0.0, seed=0, tag=0, head=0)
+    assert np.array_equal(a1.cpu().numpy(), a["action"][:, 0])
+    m2 = env.act_masks(move1=a1, dice=dice)
+    q2 = torch.as_tensor(b2 + tab[a1.cpu().numpy()], device="cuda:0")
+    a2 = policy_576(q2, m2, 0.0, seed=0, tag=0, head=1)
+    assert np.array_equal(a2.cpu().numpy(), a["action"][:, 1])
+    env.close()
+
+
+def test_driver_reference_greedy_uses_act_sets():
+    """BatchedDQNDriver(greedy="reference") at epsilon 0: move 1 is the
+    fused heads' argmax over act()'s move-1 codes, move 2 over act()'s
+    move-2 codes for it (pre-move lists)."""
+    from gym_narde.dqn import BatchedDQNDriver, expand_mask
+    from gym_narde.vector import VecNardeEnv
+
+    env = VecNardeEnv(4096, device="cuda:0", seed=27)
+    drv = BatchedDQNDriver(env, capacity=1 << 14, train_batch=256, epsilon=0.0, greedy="reference")
+    env.selfplay(45)
+    drv.resync()
+    a = drv.act(drv.state)
+    m1 = expand_mask(env.act_masks())
+    rows = torch.arange(env.num_envs, device="cuda:0")
+    has1 = m1.any(1)
+    assert bool(m1[rows, a[:, 0]][has1].all()) and bool((a[:, 0][~has1] == 0).all())
+    m2 = expand_mask(env.act_masks(move1=a[:, 0].contiguous()))
+    assert bool(m2[rows, a[:, 1]][has1].all())
+    with torch.no_grad():
+        q1 = drv.model(drv.state)
+    best = q1.masked_fill(~m1, -np.inf).max(1).values
+    got = q1.gather(1, a[:, :1]).squeeze(1)
+    assert bool((got >= best - 1e-5 * (1 + best.abs()))[has1].all())
+    env.close()

@@ -194,3 +194,43 @@ def test_in_act_plays_helper(hostcheck):
     bad[sel, 1] = (bad[sel, 1] + 1) % 576  # a neighbouring code is (almost always) not a member
     member = [any(tuple(r) == tuple(bad[i]) for r in t["combos"][starts[i]:starts[i + 1]]) for i in sel]
     assert np.array_equal(in_act_plays(*args, torch.from_numpy(bad)).numpy()[sel], np.array(member))
+
+
+def _act_masks(hc, t, rows, move1=None):
+    n = len(rows)
+    c = lambda a, dt: np.ascontiguousarray(a, dtype=dt)  # noqa: E731
+    b, o, f, p, d = (c(t["pre_board"][rows], np.int8), c(t["pre_off"][rows], np.uint8),
+                     c(t["pre_ft"][rows], np.uint8), c(t["player"][rows], np.int8), c(t["dice"][rows], np.uint8))
+    m = np.zeros((n, 9), np.uint64)
+    mv = None if move1 is None else c(move1, np.int16)
+    hc.hc_act_masks(ctypes.c_int64(n), P(b), P(o), P(f), P(p), P(d), None if mv is None else P(mv), P(m))
+    return m
+
+
+def _expand(m):
+    return np.unpackbits(m.view(np.uint8).reshape(m.shape[0], 72), axis=1, bitorder="little")[:, :576].astype(bool)
+
+
+def test_act_greedy_masks_reproduce_reference_act(hostcheck):
+    """narde_rules.h act_masks (k_act_masks' per-lane body): with the Q-values
+    the reference's DQNAgent.act was given (tests/golden/act_greedy.npz,
+    tools/capture_act_greedy.py), the masked argmax over act_masks' move-1
+    codes, then over its move-2 codes for that move 1, picks exactly the
+    reference's greedy (move1, move2) -- act()'s candidate sets
+    (valid_first_moves' keys; valid_first_moves[move1], pre-move lists)."""
+    t = golden("trainer.npz")
+    a = golden("act_greedy.npz")
+    rows = a["step"]
+    tab = np.random.default_rng(int(a["meta"][2])).standard_normal((576, 576)).astype(np.float32)
+    q1 = np.stack([np.random.default_rng(int(a["meta"][0]) + int(i)).standard_normal(576).astype(np.float32)
+                   for i in rows])
+    b2 = np.stack([np.random.default_rng(int(a["meta"][1]) + int(i)).standard_normal(576).astype(np.float32)
+                   for i in rows])
+    m1 = _expand(_act_masks(hostcheck, t, rows))
+    pick1 = np.where(m1, q1, -np.inf).argmax(1)
+    assert np.array_equal(pick1, a["action"][:, 0])
+    m2 = _expand(_act_masks(hostcheck, t, rows, move1=pick1))
+    q2 = b2 + tab[pick1]
+    pick2 = np.where(m2, q2, -np.inf).argmax(1)
+    assert np.array_equal(pick2, a["action"][:, 1])
+    assert m2.any(1).all()  # act() always offers a move 2 (code 0 when none)
