@@ -30,7 +30,14 @@ def main():
     assert lib.narde_diag_f4(c.ctypes.data_as(ctypes.c_void_p)) == 0
     c = c[:1024].astype(np.float64)
     passes, waits, lanes, parks = c[:, 0], c[:, 1], c[:, 2], c[:, 3]
-    out = {"plies": P,
+    h = np.zeros((4096, 4), np.uint64)
+    assert lib.narde_diag_f4h(h.ctypes.data_as(ctypes.c_void_p)) == 0
+    h = h[:1024].astype(np.float64)
+    helper = {"helper_passes_per_ply": round(float(h[:, 0].mean() / P), 4),
+              "lanes_per_helper_pass": round(float(h[:, 1].sum() / max(1.0, h[:, 0].sum())), 2),
+              "helper_busy_frac_of_rule_loop": round(float(h[:, 2].sum() / h[:, 3].sum()), 4),
+              "rule_loop_us_per_ply": round(float(h[:, 3].mean() / P / 100.0), 4)}  # wall_clock64: 100 MHz
+    out = {"plies": P, **helper,
            "passes_per_ply": [round(float(x), 4) for x in np.percentile(passes / P, [0, 50, 100])],
            "wait_passes_per_ply": round(float(waits.mean() / P), 4),
            "lanes_per_pass": round(float(lanes.sum() / passes.sum()), 2),
