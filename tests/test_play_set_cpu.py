@@ -234,3 +234,49 @@ def test_act_greedy_masks_reproduce_reference_act(hostcheck):
     pick2 = np.where(m2, q2, -np.inf).argmax(1)
     assert np.array_equal(pick2, a["action"][:, 1])
     assert m2.any(1).all()  # act() always offers a move 2 (code 0 when none)
+
+
+def _act_combos_oracle(board, off, ft, player, dice):
+    """DQNAgent.act's valid_move_combinations (train_deepq_pytorch.py:430-507)
+    restated over the C oracle's get_valid_moves."""
+    roll = np.array([[dice[0], dice[1], 0, 0]], np.uint8)
+    mv, cnt = O.legal_moves(board[None], ft[None], np.array([player], np.int8), roll, np.array([2], np.uint8))
+    combos = []
+    for r in mv[0, :cnt[0]]:
+        f1, t1 = int(r[0]), int(r[1])
+        c1 = f1 * 24 + (0 if t1 == 24 else t1)
+        temp = [int(dice[0]), int(dice[1])]
+        if t1 == 24:
+            match = next((d for d in temp if d >= f1 + 1), None)
+            if match is None:
+                match = max(temp)
+        else:
+            match = next((d for d in temp if d == f1 - t1), temp[0])
+        temp.remove(match)
+        mv2, c2 = O.legal_moves(board[None], ft[None], np.array([player], np.int8),
+                                np.array([[temp[0], 0, 0, 0]], np.uint8), np.array([1], np.uint8))
+        if c2[0] == 0:
+            combos.append((c1, 0))
+        for q in mv2[0, :c2[0]]:
+            combos.append((c1, int(q[0]) * 24 + (0 if int(q[1]) == 24 else int(q[1]))))
+    return combos
+
+
+def test_play_sets_on_random_positions(hostcheck):
+    """Both kinds on 3,000 random run-heavy and bear-off positions (random
+    mover, first-turn flags, two-dice rolls including doubles) against
+    restatements over the C oracle: act()'s list element for element, the
+    step's set as a set."""
+    from fuzz_positions import random_positions
+
+    board, off, ft, player, rng = random_positions(3000, 11)
+    dice = rng.integers(1, 7, size=(3000, 2)).astype(np.uint8)
+    la, wa, ca = _play_set(hostcheck, board, off, ft, player, dice, 0)
+    ls, ws, cs = _play_set(hostcheck, board, off, ft, player, dice, 1)
+    for i in range(3000):
+        want = _act_combos_oracle(board[i], off[i], ft[i], int(player[i]), dice[i])
+        assert _decode(la[i], wa[i], "act") == want, f"act {i}"
+        assert ca[i] == len(want)
+        want_s = _step_plays_oracle(board[i], off[i], ft[i], int(player[i]), dice[i])
+        assert _decode(ls[i], ws[i], "step") == want_s, f"step {i}"
+        assert cs[i] == len(want_s)
