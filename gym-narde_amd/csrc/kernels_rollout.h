@@ -305,12 +305,16 @@ __global__ void __launch_bounds__(kBlock, 1) k_rollout_wave(Planes pl, int n, Rn
 // the parked lanes' latency, not the helper's issue, bounds the wave.)
 // Drift bound, measured (sustained 1,000-ply launches, one box): every ply
 // waiting for the parked envs 0.513 ms per 100 plies (the general turn's
-// latency stalls the wave); 2 / 4 / 8 / 12 / 16 / unbounded: 0.412 / 0.395 /
-// 0.374 / 0.372 / 0.409 / 0.465 -- past ~12 plies the lanes' rows scatter
-// over more lines than the caches merge.  Staging the rows in an LDS ring
-// and storing whole rows (as k_rollout_pc does) kept the stores coalesced
-// at any drift but cost ~120 VALU + 20 LDS instructions per ply more than
-// storing from registers: 0.404.
+// latency stalls the wave); with every output stored straight from the
+// lanes, 2 / 4 / 8 / 12 / 16 / unbounded: 0.412 / 0.395 / 0.374 / 0.372 /
+// 0.409 / 0.465 -- past ~12 plies the lanes' narrow rows scattered over more
+// lines than the caches merge.  Staging the whole rows in an LDS ring (obs
+// too, expanded by the helper) kept every store coalesced but cost ~120 VALU
+// + 20 LDS instructions per ply: 0.404.  Kept (round 3): only the narrow
+// outputs through a 16-slot ring (FxRing, fx_flush), the obs rows from the
+// lanes' registers, drift 16: 0.3700-0.3711 against 0.3723-0.3725 at drift
+// 10 without the ring (drift 13: 0.3704-0.3707), PMC 1.07 x the algorithmic
+// bytes against 1.45 x (profiles/r03/full4_ring/).
 // The two waves of a pair meet only through per-lane LDS words: rule lane l
 // counts its parks and stores the count to post[l] after filling its
 // mailbox; helper lane l plays the turn when post[l] moves past the count it
@@ -326,7 +330,7 @@ __global__ void __launch_bounds__(kBlock, 1) k_rollout_wave(Planes pl, int n, Rn
 constexpr int kFxGroups = 4;                 // rule waves per workgroup (one per SIMD)
 constexpr int kFxEnvs = 64 * kFxGroups;      // envs per workgroup
 constexpr int kFxThreads = 2 * kFxEnvs;      // + one helper wave per rule wave
-constexpr int kFxDrift = 10;                 // lanes stay within kFxDrift plies of the slowest
+constexpr int kFxDrift = 16;                 // lanes stay within kFxDrift plies of the slowest
 // launches shorter than this take k_rollout_wave (sustained, ms per 100
 // plies, k_rollout_wave / k_rollout_full: 20 plies 0.540 / 0.602, 50 plies
 // 0.477 / 0.471, 100 plies 0.447 / 0.420, 200 plies 0.429 / 0.397)
@@ -341,6 +345,47 @@ struct FxLds {  // the mailboxes of one rule/helper pair
   uint32_t post[64], back[64];   // park counts: posted by the rule lane, answered by the helper lane
   uint32_t fin;                  // the rule wave has finished
 };
+
+// The narrow per-ply outputs of one rule/helper pair (reward | term << 8 |
+// trunc << 16, the legal word, the played word of each lane's turn), staged
+// in LDS slot ply & 15 (a lane plays at most kFxDrift - 1 plies past the
+// slowest).  A lane's turn writes its slot (the rule lane, or the helper
+// lane for a parked turn before it hands the env back); the rule wave stores
+// the whole 64-env rows of a ply once its slowest lane has passed it
+// (fx_flush).  Written straight from each lane, the rows of drifted lanes
+// went out at different times in pieces of 1-8 B, and the L2 wrote each
+// piece back on its own: PMC WRITE_SIZE 1.45 x the algorithmic bytes, 1.07 x
+// through the ring (at drift 16).  The obs rows (96 B a lane, whole 32-B sectors) still go
+// straight out of the lanes' registers.
+constexpr int kFxSlots = 16;
+static_assert(kFxSlots >= kFxDrift && (kFxSlots & (kFxSlots - 1)) == 0, "ring slots");
+struct FxRing {
+  uint4 lp[kFxSlots][64];     // legal word, played word
+  uint32_t rf[kFxSlots][64];  // reward | term << 8 | trunc << 16
+};
+
+__device__ __forceinline__ void fx_put(FxRing& R, int l, int p, const TurnOut& o, int term, int trunc) {
+  const int k = p & (kFxSlots - 1);
+  R.lp[k][l] = make_uint4((uint32_t)o.legal, (uint32_t)(o.legal >> 32), (uint32_t)o.played,
+                          (uint32_t)(o.played >> 32));
+  R.rf[k][l] = (uint32_t)o.reward | ((uint32_t)term << 8) | ((uint32_t)trunc << 16);
+}
+
+// the rows of ply q (every valid lane has played it): coalesced 64-env stores
+__device__ __forceinline__ void fx_flush(const FxRing& R, const Outs& out, int l, int q, int n, int i,
+                                         bool valid) {
+  const int k = q & (kFxSlots - 1);
+  const uint4 lp = R.lp[k][l];
+  const uint32_t rf = R.rf[k][l];
+  if (valid) {
+    const size_t ix = (size_t)q * n + i;
+    if (out.reward) st_out(out.reward + ix, (int32_t)(rf & 0xFFu));
+    if (out.term) st_out(out.term + ix, (uint8_t)((rf >> 8) & 1u));
+    if (out.trunc) st_out(out.trunc + ix, (uint8_t)((rf >> 16) & 1u));
+    if (out.legal) st_out(out.legal + ix, (uint64_t)lp.x | ((uint64_t)lp.y << 32));
+    if (out.played) st_out(out.played + ix, (uint64_t)lp.z | ((uint64_t)lp.w << 32));
+  }
+}
 
 __device__ __forceinline__ void mail_put(FxLds& M, int l, const Side& s) {
   const uint32_t misc = s.off_own | (s.off_opp << 4) | (s.ft_own << 8) | (s.ft_opp << 9) | (s.black << 10) |
@@ -381,9 +426,11 @@ template <bool kOut>
 __global__ void __launch_bounds__(kFxThreads) k_rollout_full(Planes pl, int n, Rng g, int plies,
                                                              int max_steps, Outs out) {
   __shared__ FxLds fx[kFxGroups];
+  __shared__ FxRing fring[kOut ? kFxGroups : 1];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int grp = wave % kFxGroups;
   FxLds& M = fx[grp];
+  FxRing& RG = fring[kOut ? grp : 0];
   const int i = blockIdx.x * kFxEnvs + grp * 64 + lane;
   const bool valid = i < n;
   int4 cum = make_int4(0, 0, 0, 0);  // the env's statistics after the launch (wg_totals)
@@ -404,6 +451,7 @@ __global__ void __launch_bounds__(kFxThreads) k_rollout_full(Planes pl, int n, R
     uint32_t seq = 0u;   // parks of this lane
     int p = 0;           // this env's next ply of the launch
     int lo = 0;          // the slowest lane's next ply (wave-uniform)
+    int fl = 0;          // plies whose narrow rows are stored (wave-uniform)
     for (;;) {
       if (__ballot(parked) != 0ull) {  // wave-uniform: take the envs handed back
         if (parked && lds_acquire(&M.back[lane]) == seq) {
@@ -417,6 +465,9 @@ __global__ void __launch_bounds__(kFxThreads) k_rollout_full(Planes pl, int n, R
         }
       }
       while (lo < plies && __ballot(valid && p <= lo) == 0ull) ++lo;
+      // before any turn below reuses a slot: every ply below lo is complete
+      if (kOut)
+        for (; fl < lo; ++fl) fx_flush(RG, out, lane, fl, n, i, valid);
       const bool act = valid && !parked && p < plies && p < lo + kFxDrift;
       if (__ballot(act) == 0ull) {
         if (__ballot(parked) == 0ull) break;  // every ply played
@@ -455,7 +506,10 @@ __global__ void __launch_bounds__(kFxThreads) k_rollout_full(Planes pl, int n, R
         turn_free(s, dh, dl, w, o);
         int term, trunc;
         ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, true, term, trunc);
-        if (kOut) store_outs(out, (size_t)p * n + i, s, o, term, trunc, nullptr, false);
+        if (kOut) {
+          if (out.obs) store_obs(out.obs, (size_t)p * n + i, s);
+          fx_put(RG, lane, p, o, term, trunc);
+        }
         ++p;
       }
     }
@@ -501,7 +555,10 @@ __global__ void __launch_bounds__(kFxThreads) k_rollout_full(Planes pl, int n, R
         int term, trunc;
         ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, true, term, trunc);
         if (mine) {
-          if (kOut) store_outs(out, (size_t)p * n + i, s, o, term, trunc, nullptr, false);
+          if (kOut) {
+            if (out.obs) store_obs(out.obs, (size_t)p * n + i, s);
+            fx_put(RG, lane, p, o, term, trunc);
+          }
           mail_put(M, lane, s);
           M.ret[lane] = (uint32_t)st.x | ((uint32_t)st.y << 4) | ((uint32_t)st.z << 8);
           done = want;
