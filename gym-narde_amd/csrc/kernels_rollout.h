@@ -310,11 +310,14 @@ __global__ void __launch_bounds__(kBlock, 1) k_rollout_wave(Planes pl, int n, Rn
 // 0.409 / 0.465 -- past ~12 plies the lanes' narrow rows scattered over more
 // lines than the caches merge.  Staging the whole rows in an LDS ring (obs
 // too, expanded by the helper) kept every store coalesced but cost ~120 VALU
-// + 20 LDS instructions per ply: 0.404.  Kept (round 3): only the narrow
-// outputs through a 16-slot ring (FxRing, fx_flush), the obs rows from the
-// lanes' registers, drift 16: 0.3700-0.3711 against 0.3723-0.3725 at drift
-// 10 without the ring (drift 13: 0.3704-0.3707), PMC 1.07 x the algorithmic
-// bytes against 1.45 x (profiles/r03/full4_ring/).
+// + 20 LDS instructions per ply: 0.404.  Round 3 (profiles/r03/full4_ring/):
+// the narrow outputs through a 16-slot ring (FxRing, fx_flush), the obs rows
+// from the lanes' registers, drift 16: 0.3700-0.3711 against 0.3723-0.3725
+// at drift 10 without the ring (drift 13: 0.3704-0.3707), PMC 1.07 x the
+// algorithmic bytes against 1.45 x; every obs row through the ring as well
+// (12 or 8 slots): PMC 1.002 x but 0.400 / 0.408.  Kept: the narrow ring
+// plus each row pair's shared 64-B granule at the flush (fx_obs_own), drift
+// 16: PMC 1.026 x, 0.3743-0.3753 (1.1 % behind the narrow ring alone).
 // The two waves of a pair meet only through per-lane LDS words: rule lane l
 // counts its parks and stores the count to post[l] after filling its
 // mailbox; helper lane l plays the turn when post[l] moves past the count it
@@ -346,43 +349,77 @@ struct FxLds {  // the mailboxes of one rule/helper pair
   uint32_t fin;                  // the rule wave has finished
 };
 
-// The narrow per-ply outputs of one rule/helper pair (reward | term << 8 |
-// trunc << 16, the legal word, the played word of each lane's turn), staged
-// in LDS slot ply & 15 (a lane plays at most kFxDrift - 1 plies past the
-// slowest).  A lane's turn writes its slot (the rule lane, or the helper
-// lane for a parked turn before it hands the env back); the rule wave stores
-// the whole 64-env rows of a ply once its slowest lane has passed it
-// (fx_flush).  Written straight from each lane, the rows of drifted lanes
-// went out at different times in pieces of 1-8 B, and the L2 wrote each
-// piece back on its own: PMC WRITE_SIZE 1.45 x the algorithmic bytes, 1.07 x
-// through the ring (at drift 16).  The obs rows (96 B a lane, whole 32-B sectors) still go
-// straight out of the lanes' registers.
+// The narrow per-ply outputs of one rule/helper pair (the legal word with
+// reward, term and trunc in its top 4 bits, the played word), staged in LDS
+// slot ply & 15 (a lane plays at most kFxDrift - 1 plies past the slowest),
+// with 32 B of each obs row (fx_obs_own).  A lane's turn writes its slot (the
+// rule lane, or the helper lane for a parked turn before it hands the env
+// back); the rule wave stores the whole 64-env rows of a ply once its
+// slowest lane has passed it (fx_flush).  Written straight from each lane,
+// the rows of drifted lanes went out at different times in pieces of 1-8 B,
+// and the L2 wrote each piece back on its own: PMC WRITE_SIZE 1.45 x the
+// algorithmic bytes; 1.07 x with the narrow outputs through the ring; 1.026 x
+// with the obs rows' shared granules too.
 constexpr int kFxSlots = 16;
 static_assert(kFxSlots >= kFxDrift && (kFxSlots & (kFxSlots - 1)) == 0, "ring slots");
 struct FxRing {
-  uint4 lp[kFxSlots][64];     // legal word, played word
-  uint32_t rf[kFxSlots][64];  // reward | term << 8 | trunc << 16
+  uint4 lp[kFxSlots][64];    // legal word | reward << 60 | term << 62 | trunc << 63, played word
+  uint2 half[kFxSlots][64];  // the own / opp nibble word of the row's shared 32 B (fx_put)
 };
 
-__device__ __forceinline__ void fx_put(FxRing& R, int l, int p, const TurnOut& o, int term, int trunc) {
-  const int k = p & (kFxSlots - 1);
-  R.lp[k][l] = make_uint4((uint32_t)o.legal, (uint32_t)(o.legal >> 32), (uint32_t)o.played,
-                          (uint32_t)(o.played >> 32));
-  R.rf[k][l] = (uint32_t)o.reward | ((uint32_t)term << 8) | ((uint32_t)trunc << 16);
+// Lanes 2j and 2j + 1 hold adjacent 96-B obs rows: 192 B = three 64-B
+// granules, of which the middle one holds 32 B of each row (points 16..23
+// of the even lane's env, points 0..7 of the odd lane's).  A lane stores its
+// own whole granule from its registers at its turn (fx_obs_own) and leaves
+// its share of the middle one in the ring, stored with the pair's other
+// half at the flush.
+__device__ __forceinline__ void fx_obs_own(int32_t* __restrict__ obs, size_t ix, const Side& s, bool odd) {
+  // even: points 0..15 (nibble words 0, 1); odd: points 8..23 (words 1, 2)
+  const uint32_t o0 = odd ? s.own.w[1] : s.own.w[0], o1 = odd ? s.own.w[2] : s.own.w[1];
+  const uint32_t q0 = odd ? s.opp.w[1] : s.opp.w[0], q1 = odd ? s.opp.w[2] : s.opp.w[1];
+  int4* dst = reinterpret_cast<int4*>(obs + ix * 24 + (odd ? 8 : 0));
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const uint32_t ow = (c < 2 ? o0 : o1) >> (16 * (c & 1)), pw = (c < 2 ? q0 : q1) >> (16 * (c & 1));
+    st_out(dst + c, make_int4((int)(ow & 15u) - (int)(pw & 15u), (int)((ow >> 4) & 15u) - (int)((pw >> 4) & 15u),
+                              (int)((ow >> 8) & 15u) - (int)((pw >> 8) & 15u),
+                              (int)((ow >> 12) & 15u) - (int)((pw >> 12) & 15u)));
+  }
 }
 
-// the rows of ply q (every valid lane has played it): coalesced 64-env stores
+__device__ __forceinline__ void fx_put(FxRing& R, int l, int p, const Side& s, const TurnOut& o, int term,
+                                       int trunc) {
+  const int k = p & (kFxSlots - 1);
+  const uint64_t lg = o.legal | ((uint64_t)o.reward << 60) | ((uint64_t)term << 62) | ((uint64_t)trunc << 63);
+  R.lp[k][l] = make_uint4((uint32_t)lg, (uint32_t)(lg >> 32), (uint32_t)o.played, (uint32_t)(o.played >> 32));
+  const bool odd = l & 1;
+  R.half[k][l] = make_uint2(odd ? s.own.w[0] : s.own.w[2], odd ? s.opp.w[0] : s.opp.w[2]);
+}
+
+// the rows of ply q (every valid lane has played it): the narrow outputs as
+// coalesced 64-env stores, and each lane's 32 B of its pair's middle granule
 __device__ __forceinline__ void fx_flush(const FxRing& R, const Outs& out, int l, int q, int n, int i,
                                          bool valid) {
   const int k = q & (kFxSlots - 1);
   const uint4 lp = R.lp[k][l];
-  const uint32_t rf = R.rf[k][l];
+  const uint2 h = R.half[k][l];
   if (valid) {
     const size_t ix = (size_t)q * n + i;
-    if (out.reward) st_out(out.reward + ix, (int32_t)(rf & 0xFFu));
-    if (out.term) st_out(out.term + ix, (uint8_t)((rf >> 8) & 1u));
-    if (out.trunc) st_out(out.trunc + ix, (uint8_t)((rf >> 16) & 1u));
-    if (out.legal) st_out(out.legal + ix, (uint64_t)lp.x | ((uint64_t)lp.y << 32));
+    if (out.obs) {
+      int4* dst = reinterpret_cast<int4*>(out.obs + ix * 24 + ((l & 1) ? 0 : 16));
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const uint32_t ow = h.x >> (16 * c), pw = h.y >> (16 * c);
+        st_out(dst + c, make_int4((int)(ow & 15u) - (int)(pw & 15u), (int)((ow >> 4) & 15u) - (int)((pw >> 4) & 15u),
+                                  (int)((ow >> 8) & 15u) - (int)((pw >> 8) & 15u),
+                                  (int)((ow >> 12) & 15u) - (int)((pw >> 12) & 15u)));
+      }
+    }
+    const uint32_t hi = lp.y;
+    if (out.reward) st_out(out.reward + ix, (int32_t)((hi >> 28) & 3u));
+    if (out.term) st_out(out.term + ix, (uint8_t)((hi >> 30) & 1u));
+    if (out.trunc) st_out(out.trunc + ix, (uint8_t)(hi >> 31));
+    if (out.legal) st_out(out.legal + ix, (uint64_t)lp.x | ((uint64_t)(hi & 0x0FFFFFFFu) << 32));
     if (out.played) st_out(out.played + ix, (uint64_t)lp.z | ((uint64_t)lp.w << 32));
   }
 }
@@ -507,8 +544,8 @@ __global__ void __launch_bounds__(kFxThreads) k_rollout_full(Planes pl, int n, R
         int term, trunc;
         ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, true, term, trunc);
         if (kOut) {
-          if (out.obs) store_obs(out.obs, (size_t)p * n + i, s);
-          fx_put(RG, lane, p, o, term, trunc);
+          if (out.obs) fx_obs_own(out.obs, (size_t)p * n + i, s, lane & 1);
+          fx_put(RG, lane, p, s, o, term, trunc);
         }
         ++p;
       }
@@ -556,8 +593,8 @@ __global__ void __launch_bounds__(kFxThreads) k_rollout_full(Planes pl, int n, R
         ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, true, term, trunc);
         if (mine) {
           if (kOut) {
-            if (out.obs) store_obs(out.obs, (size_t)p * n + i, s);
-            fx_put(RG, lane, p, o, term, trunc);
+            if (out.obs) fx_obs_own(out.obs, (size_t)p * n + i, s, lane & 1);
+            fx_put(RG, lane, p, s, o, term, trunc);
           }
           mail_put(M, lane, s);
           M.ret[lane] = (uint32_t)st.x | ((uint32_t)st.y << 4) | ((uint32_t)st.z << 8);
