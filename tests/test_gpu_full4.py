@@ -124,14 +124,17 @@ def test_full4_selfplay_trajectory_vs_oracle(dice_mode, max_steps):
     assert np.array_equal(np_(env.stats()), ref.stats)
 
 
-def test_full4_rollout_equals_steps():
+@pytest.mark.parametrize("max_steps", [1000, 30])
+def test_full4_rollout_equals_steps(max_steps):
     """narde_rollout_full over launch boundaries == per-ply k_step<full>: 1 and
     29 plies take k_rollout_wave, 70 and 100 k_rollout_full (rule + helper
-    waves, lanes drifting up to 10 plies), ragged n (the last workgroup
-    partly empty)."""
+    waves, lanes drifting up to 16 plies, the per-ply rows through the LDS
+    ring), ragged odd n (the last workgroup partly empty, odd plies' rows not
+    64-B aligned); with TimeLimit 30 every env truncates several times
+    inside the launches (the truncated flag through the ring)."""
     n, seed = 2048 + 77, 31337
-    a = vec(n, seed=seed)
-    b = vec(n, seed=seed)
+    a = vec(n, seed=seed, max_episode_steps=max_steps)
+    b = vec(n, seed=seed, max_episode_steps=max_steps)
     bufs = a.rollout_buffers(100)
     got = {k: [] for k in bufs}
     for plies in (1, 29, 70, 100):
@@ -148,6 +151,8 @@ def test_full4_rollout_equals_steps():
         assert np.array_equal(got["legal"][p], np_(info["legal"])), p
         assert np.array_equal(got["actions"][p], np_(info["played"])), p
     assert np.array_equal(np_(a.stats()), np_(b.stats()))
+    if max_steps == 30:
+        assert got["truncated"].sum() > n  # truncations inside the rollout launches
 
 
 @pytest.mark.parametrize("plies", [120, 20])
