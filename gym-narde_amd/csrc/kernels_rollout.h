@@ -38,20 +38,10 @@ __device__ __forceinline__ void st_out(T* p, T v) {
   *p = v;
 }
 
-// non-temporal form (global_store ... nt) for the plies at the end of a
-// rollout launch (k_rollout_pc, kPcNtTail)
-template <bool kNt, class T>
-__device__ __forceinline__ void st_out_p(T* p, T v) {
-  if constexpr (!kNt) {
-    *p = v;
-  } else if constexpr (sizeof(T) == 16) {
-    typedef int v4i __attribute__((ext_vector_type(4)));
-    v4i x;
-    __builtin_memcpy(&x, &v, 16);
-    __builtin_nontemporal_store(x, reinterpret_cast<v4i*>(p));
-  } else {
-    __builtin_nontemporal_store(v, p);
-  }
+// the nibble of x at bit `off` (a multiple of 4, below 32) as one v_bfe_u32:
+// with a per-lane offset the compiler emits a shift and a mask (two VALU)
+__device__ __forceinline__ int nib_at(uint32_t x, int off) {
+  return (int)__builtin_amdgcn_ubfe(x, (uint32_t)off, 4u);
 }
 
 __device__ __forceinline__ int4 obs_quad(const Side& s, int q) {
@@ -678,47 +668,123 @@ __device__ __forceinline__ void pc_put(PcLds& L, int slot, int k, int le, const 
                                  (uint32_t)o.reward | ((uint32_t)term << 8) | ((uint32_t)trunc << 16));
 }
 
+// obs quad qq (points 4qq .. 4qq + 3) of workgroup-local env le from the ply
+// results in LDS: only the two words it needs -- own word wi is dword wi of
+// nib0, opponent word wi is dword 3 of nib0 or wi - 1 of nib1
+__device__ __forceinline__ int4 pc_obs_quad(const PcLds& L, int slot, int k, int le, int qq) {
+  const int wi = qq >> 1, sh = (qq & 1) * 16;
+  const uint32_t* n0w = reinterpret_cast<const uint32_t*>(&L.nib0[slot][k][le]);
+  const uint32_t* n1w = reinterpret_cast<const uint32_t*>(&L.nib1[slot][k][le]);
+  const uint32_t own = n0w[wi];
+  const uint32_t opp = wi == 0 ? n0w[3] : n1w[wi - 1];
+  int4 v;
+  v.x = nib_at(own, sh) - nib_at(opp, sh);
+  v.y = nib_at(own, sh + 4) - nib_at(opp, sh + 4);
+  v.z = nib_at(own, sh + 8) - nib_at(opp, sh + 8);
+  v.w = nib_at(own, sh + 12) - nib_at(opp, sh + 12);
+  return v;
+}
+
+// Non-temporal raw buffer stores for the consumers of short launches: a
+// scalar resource (base, extent) per output and ply, built by SALU, and a
+// 32-bit per-lane byte offset -- the 64-bit address arithmetic of global
+// stores (two VALU per store and ply) leaves the VALU that the SIMD's rule
+// and consumer waves share.  aux 2 = the non-temporal policy
+// (buffer_store ... nt).  Dword 3 = 0x00020000, the
+// gfx9 raw-buffer word (/opt/rocm/include/ck/ck.hpp).
+typedef int pc_v4i __attribute__((ext_vector_type(4)));
+typedef unsigned pc_v2u __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pc_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ void pc_st16(__amdgpu_buffer_rsrc_t r, uint32_t off, int4 v) {
+  const pc_v4i x = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)off, 0, 2);
+}
+__device__ __forceinline__ void pc_st8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint64_t v) {
+  const pc_v2u x = {(unsigned)v, (unsigned)(v >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b64(x, r, (int)off, 0, 2);
+}
+__device__ __forceinline__ void pc_st4(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, 2);
+}
+__device__ __forceinline__ void pc_st1(__amdgpu_buffer_rsrc_t r, uint32_t off, uint8_t v) {
+  __builtin_amdgcn_raw_buffer_store_b8(v, r, (int)off, 0, 2);
+}
+
 // consumer: outputs of ply p (block slot `slot`, index k) for the 64 envs of
-// consumer wave cw
+// consumer wave cw.  Two forms, chosen with the store policy (kNt, by launch
+// length), each the faster of the two on its launches (tools/diag/
+// gpu_ab_multi.sh, one box; ms per 100 plies, base = round 2's consumer):
+//   short launches (non-temporal): raw buffer stores with a wave-uniform
+//     resource per output, no per-lane bounds branch (the resource's extent
+//     drops the stores past n): 20 plies 0.1697 -> 0.1613 sustained, one
+//     launch 34.7 -> 32.7 us back to back;
+//   long launches (plain stores): global stores with the bounds branches --
+//     the branch-free buffer form ran 0.1366 against 0.1276 at 1,000 plies,
+//     this one 0.1258.
 template <bool kNt>
 __device__ __forceinline__ void pc_emit_ply(const PcLds& L, int slot, int k, int p, int n, int wg_env0, int cw,
                                             int lane, const Outs& out) {
-  const int e0 = cw * 64;          // first env of this wave, workgroup-local
-  const int g0 = wg_env0 + e0;     // ... global (handle) index
-  const size_t row0 = (size_t)p * n + g0;
-  if (out.obs) {
-    // the wave's 64 obs rows are 384 contiguous int4 quads: lane takes
-    // quads lane + 64 q, so every store instruction covers 1 KiB
-    int4* dst = reinterpret_cast<int4*>(out.obs + row0 * 24);
+  const int e0 = cw * 64;  // first env of this wave, workgroup-local (LDS index)
+  if constexpr (kNt) {
+    const int g0 = wg_env0 + __builtin_amdgcn_readfirstlane(cw) * 64;  // global, wave-uniform
+    const size_t row0 = (size_t)p * n + g0;                              // wave-uniform
+    const uint32_t nw = (uint32_t)max(0, min(64, n - g0));              // envs of this wave
+    if (out.obs) {
+      // the wave's 64 obs rows are 384 contiguous int4 quads: lane takes
+      // quads lane + 64 q, so every store instruction covers 1 KiB
+      const __amdgpu_buffer_rsrc_t r = pc_rsrc(out.obs + row0 * 24, nw * 96u);
 #pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      const int j = lane + 64 * q;
-      const int el = j / 6, qq = j - 6 * el;
-      if (g0 + el >= n) continue;
-      const int wi = qq >> 1, sh = (qq & 1) * 16;
-      // read only the two words this quad needs: own word wi is dword wi
-      // of nib0, opponent word wi is dword 3 of nib0 or wi - 1 of nib1
-      const uint32_t* n0w = reinterpret_cast<const uint32_t*>(&L.nib0[slot][k][e0 + el]);
-      const uint32_t* n1w = reinterpret_cast<const uint32_t*>(&L.nib1[slot][k][e0 + el]);
-      const uint32_t own = n0w[wi];
-      const uint32_t opp = wi == 0 ? n0w[3] : n1w[wi - 1];
-      int4 v;
-      v.x = (int)((own >> sh) & 15u) - (int)((opp >> sh) & 15u);
-      v.y = (int)((own >> (sh + 4)) & 15u) - (int)((opp >> (sh + 4)) & 15u);
-      v.z = (int)((own >> (sh + 8)) & 15u) - (int)((opp >> (sh + 8)) & 15u);
-      v.w = (int)((own >> (sh + 12)) & 15u) - (int)((opp >> (sh + 12)) & 15u);
-      st_out_p<kNt>(dst + j, v);
+      for (int q = 0; q < 6; ++q) {
+        const int j = lane + 64 * q;
+        const int el = j / 6, qq = j - 6 * el;
+        pc_st16(r, (uint32_t)j * 16u, pc_obs_quad(L, slot, k, e0 + el, qq));
+      }
     }
-  }
-  if (g0 + lane < n) {
     const uint2 lg = L.legal[slot][k][e0 + lane];
     const uint2 c = L.cf[slot][k][e0 + lane];
-    const size_t ix = row0 + lane;
-    if (out.reward) st_out_p<kNt>(out.reward + ix, (int32_t)(c.y & 0xFFu));
-    if (out.term) st_out_p<kNt>(out.term + ix, (uint8_t)((c.y >> 8) & 1u));
-    if (out.trunc) st_out_p<kNt>(out.trunc + ix, (uint8_t)((c.y >> 16) & 1u));
-    if (out.legal) st_out_p<kNt>(out.legal + ix, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
-    if (out.act_out) st_out_p<kNt>(reinterpret_cast<uint32_t*>(out.act_out) + ix, c.x);
+    const uint32_t l = (uint32_t)lane;
+    if (out.reward) pc_st4(pc_rsrc(out.reward + row0, nw * 4u), 4u * l, c.y & 0xFFu);
+    if (out.term) pc_st1(pc_rsrc(out.term + row0, nw), l, (uint8_t)((c.y >> 8) & 1u));
+    if (out.trunc) pc_st1(pc_rsrc(out.trunc + row0, nw), l, (uint8_t)((c.y >> 16) & 1u));
+    if (out.legal) pc_st8(pc_rsrc(out.legal + row0, nw * 8u), 8u * l, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
+    if (out.act_out) pc_st4(pc_rsrc(reinterpret_cast<uint32_t*>(out.act_out) + row0, nw * 4u), 4u * l, c.x);
+  } else {
+    const int g0 = wg_env0 + e0;
+    const size_t row0 = (size_t)p * n + g0;
+    if (out.obs) {
+      int4* dst = reinterpret_cast<int4*>(out.obs + row0 * 24);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const int j = lane + 64 * q;
+        const int el = j / 6, qq = j - 6 * el;
+        if (g0 + el >= n) continue;
+        const int wi = qq >> 1, sh = (qq & 1) * 16;
+        // read only the two words this quad needs: own word wi is dword wi
+        // of nib0, opponent word wi is dword 3 of nib0 or wi - 1 of nib1
+        const uint32_t* n0w = reinterpret_cast<const uint32_t*>(&L.nib0[slot][k][e0 + el]);
+        const uint32_t* n1w = reinterpret_cast<const uint32_t*>(&L.nib1[slot][k][e0 + el]);
+        const uint32_t own = n0w[wi];
+        const uint32_t opp = wi == 0 ? n0w[3] : n1w[wi - 1];
+        int4 v;
+        v.x = nib_at(own, sh) - nib_at(opp, sh);
+        v.y = nib_at(own, sh + 4) - nib_at(opp, sh + 4);
+        v.z = nib_at(own, sh + 8) - nib_at(opp, sh + 8);
+        v.w = nib_at(own, sh + 12) - nib_at(opp, sh + 12);
+        st_out(dst + j, v);
+      }
+    }
+    if (g0 + lane < n) {
+      const uint2 lg = L.legal[slot][k][e0 + lane];
+      const uint2 c = L.cf[slot][k][e0 + lane];
+      const size_t ix = row0 + lane;
+      if (out.reward) st_out(out.reward + ix, (int32_t)(c.y & 0xFFu));
+      if (out.term) st_out(out.term + ix, (uint8_t)((c.y >> 8) & 1u));
+      if (out.trunc) st_out(out.trunc + ix, (uint8_t)((c.y >> 16) & 1u));
+      if (out.legal) st_out(out.legal + ix, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
+      if (out.act_out) st_out(reinterpret_cast<uint32_t*>(out.act_out) + ix, c.x);
+    }
   }
 }
 
