@@ -184,6 +184,40 @@ def test_rollout_vs_oracle_and_step(n):
     assert env.ply == 320
 
 
+@pytest.mark.parametrize("rules", ["ref2", "full4"])
+@pytest.mark.parametrize("n", [37, 130, 4097])
+def test_rollout_writes_only_its_buffers(rules, n):
+    """Every output of a rollout launch lands inside its [plies][n] buffer and
+    nowhere else, for batches that end inside a wave and inside a workgroup,
+    at both REF2 store forms (<= 32 plies: raw buffer stores whose extents
+    drop the rows past n; longer: global stores behind bounds checks) and the
+    FULL4 kernels: each buffer is a view into a larger sentinel-filled
+    tensor, with guard regions before and after it, and the guards must come
+    back untouched while the buffer itself matches a plain rollout."""
+    G = 4096  # guard elements on each side
+    fills = {torch.uint8: 0x5A, torch.int16: -0x2B2B, torch.int32: -0x2B2B2B2B, torch.int64: -0x2B2B2B2B2B}
+    for plies in (20, 33):
+        ref = vec(n, seed=5, rules=rules, max_episode_steps=60)
+        env = vec(n, seed=5, rules=rules, max_episode_steps=60)
+        want = ref.rollout(plies)
+        bufs, bigs = {}, {}
+        for k, v in env.rollout_buffers(plies).items():
+            if v is None:
+                bufs[k] = None
+                continue
+            flat = v.numel()
+            big = torch.full((flat + 2 * G,), fills[v.dtype], dtype=v.dtype, device=v.device)
+            bigs[k] = big
+            bufs[k] = big[G:G + flat].view(v.shape)
+        env.rollout(plies, bufs)
+        for k, big in bigs.items():
+            b = np_(big)
+            assert (b[:G] == fills[big.dtype]).all() and (b[-G:] == fills[big.dtype]).all(), (k, plies)
+            assert np.array_equal(np_(bufs[k]), np_(want[k])), (k, plies)
+        env.close()
+        ref.close()
+
+
 def test_step_graph_replay_vs_oracle():
     """k_step captured in a hipGraph and replayed advances each env's own RNG
     counter, so replays reproduce consecutive plies exactly."""

@@ -85,7 +85,7 @@ __device__ __forceinline__ uint32_t tbs_bf(uint32_t O, uint32_t S1, uint32_t P, 
 """
 
 
-def build(tag, force_full, drift=None, cut=None, wave=None):
+def build(tag, force_full, drift=None, cut=None, wave=None, prio=None):
     tmp = tempfile.mkdtemp()
     shutil.copytree(os.path.join(ROOT, "gym-narde_amd"), os.path.join(tmp, "gym-narde_amd"))
     shutil.copytree(os.path.join(ROOT, "include"), os.path.join(tmp, "include"))
@@ -136,6 +136,12 @@ def build(tag, force_full, drift=None, cut=None, wave=None):
         body = body.replace("    ply_close(", "    o.played ^= (uint64_t)bs;\n    ply_close(")
         s = sub(s, WAVE_PLY, body)
         s = sub(s, "// k_rollout_wave: the FULL4 rollout", PROBE_FNS + "// k_rollout_wave: the FULL4 rollout")
+    if prio is not None:  # the helper's turn at a raised wave priority (s_setprio)
+        s = sub(s, "        coop_turn_full<true>(s, d0, d1, false, ~0ull, w, o, lane, bs);",
+                f"        __builtin_amdgcn_s_setprio({prio});\n"
+                "        coop_turn_full<true>(s, d0, d1, false, ~0ull, w, o, lane, bs);")
+        s = sub(s, "          lds_publish(&M.back[lane], want);\n        }\n",
+                "          lds_publish(&M.back[lane], want);\n        }\n        __builtin_amdgcn_s_setprio(0);\n")
     if force_full:
         s = sub(s, "constexpr int kFxMinPlies = 48;", "constexpr int kFxMinPlies = 1;")
     if drift is not None:
@@ -165,6 +171,10 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "wave":  # build_wave_clock.py wave free allfree
         for v in sys.argv[2:]:
             build(f"wclock_{v}", False, wave=v)
+    elif len(sys.argv) > 1 and sys.argv[1] == "prio":  # build_wave_clock.py prio 1 3
+        for q in sys.argv[2:]:
+            build(f"wclock_full_p{q}", True, prio=int(q))
+            build(f"wclock_full_d4p{q}", True, drift=4, prio=int(q))
     elif len(sys.argv) > 1 and sys.argv[1] == "cut":  # build_wave_clock.py cut 1 3
         for c in sys.argv[2:]:
             build(f"wclock_cut{c}", False, cut=int(c))
