@@ -132,6 +132,11 @@ __device__ __forceinline__ void turn_play(Side& s, int dh, int dl, uint32_t Ch, 
       hl -= p == 23 ? 1 : 0;
     }
   }
+  // unrolled: with the general turn's cooperative check inside `later` the
+  // compiler keeps a rolled loop, whose per-iteration control cost a short
+  // FULL4 launch (k_rollout_wave, 20 plies) 6 % (0.519 -> 0.487 ms per 100
+  // plies, profiles/r03/session3/wave_clock/wc9)
+#pragma unroll
   for (int k = 1; k < 4; ++k) {
     const bool act = go && k < M;
     if (__ballot(act) == 0ull) break;  // wave-uniform: no lane has sub-move k

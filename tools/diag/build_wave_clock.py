@@ -119,6 +119,30 @@ def build(tag, force_full, drift=None, cut=None, wave=None, prio=None):
         s = sub(s, WAVE_PLY, WAVE_FAST % "__ballot(bs != 0u) == 0ull")
     elif wave == "allfree":
         s = sub(s, WAVE_PLY, WAVE_FAST % "true || bs == 0u")
+    elif wave == "unroll":  # turn_play's later sub-moves unrolled (product semantics)
+        q = os.path.join(csrc, "kernels_full4.h")
+        t = open(q).read()
+        t = sub(t, "  for (int k = 1; k < 4; ++k) {\n    const bool act = go && k < M;",
+                "#pragma unroll\n  for (int k = 1; k < 4; ++k) {\n    const bool act = go && k < M;")
+        open(q, "w").write(t)
+    elif wave in ("nc_nofilt0", "nc_nolater", "nc_nosure", "nc_min"):
+        # on top of "nocoop" (timing only): no root block filter ("nc_nofilt0"),
+        # no block filter in the later sub-moves ("nc_nolater"), no sure-move
+        # masks ("nc_nosure"), none of the three ("nc_min")
+        q = os.path.join(csrc, "kernels_full4.h")
+        t = open(q).read()
+        t = sub(t, "fast = dbl && !bf && f4_safe_bound(s, dh, hl0, ws) >= 4;", "fast = dbl && !bf;")
+        if wave in ("nc_nosure", "nc_min"):
+            t = sub(t, "sh = nbf2 ? f4_sure_pair(s.O, s.P, dl, Lh, hs) : 0u;", "sh = nbf2 ? Lh : 0u;")
+            t = sub(t, "sl = nbf2 ? f4_sure_pair(s.O, s.P, dh, Ll, hs) : 0u;", "sl = nbf2 ? Ll : 0u;")
+        else:
+            t = sub(t, "sh = nbf2 ? f4_sure_pair(s.O, s.P, dl, Lh, hs) : 0u;", "sh = nbf2 ? (Lh | f4_sure_pair(s.O, s.P, dl, Lh, hs)) : 0u;")
+            t = sub(t, "sl = nbf2 ? f4_sure_pair(s.O, s.P, dh, Ll, hs) : 0u;", "sl = nbf2 ? (Ll | f4_sure_pair(s.O, s.P, dh, Ll, hs)) : 0u;")
+        if wave in ("nc_nofilt0", "nc_min"):
+            t = sub(t, "  if (!bf) {\n    const Blocks bl = block_info_low(s.O, low);", "  if (false) {\n    const Blocks bl = block_info_low(s.O, low);")
+        if wave in ("nc_nolater", "nc_min"):
+            t = sub(t, "if (act && !bf) Lk = die_filter(s.O, s.S1o, block_info_low(s.O, low), Lk, dk);", "")
+        open(q, "w").write(t)
     elif wave in ("nodsearch", "notask", "nocoop"):
         # timing only (wrong results): block-bound doubles never search
         # ("nodsearch"), block-bound two-dice first moves all sure ("notask"), both ("nocoop")
