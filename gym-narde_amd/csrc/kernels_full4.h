@@ -172,15 +172,16 @@ __device__ __forceinline__ void turn_play(Side& s, int dh, int dl, uint32_t Ch, 
 // env_turn_full with the per-source checks done cooperatively (see above).
 // kBound: every lane that has a turn is block-bound, with turn_block_set =
 // bs_given (the rollout's helper wave: its rule wave ran the test); the
-// block-free code is compiled out.
-template <bool kBound = false>
+// block-free code is compiled out.  kGiven: bs_given is every lane's
+// turn_block_set, computed by the caller (k_rollout_wave).
+template <bool kBound = false, bool kGiven = false>
 __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, const uint32_t w[4],
                                TurnOut& o, int lane, uint32_t bs_given = 0u) {
   const uint32_t low = block_lowmask(s.P);
   const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
   const bool dbl = dh == dl;
   // one block test for both kinds of turn (turn_block_set)
-  const uint32_t bs = kBound ? bs_given : turn_block_set(s.O, s.S1o, s.P, low, dh, dl);
+  const uint32_t bs = (kBound || kGiven) ? bs_given : turn_block_set(s.O, s.S1o, s.P, low, dh, dl);
   const bool bf = kBound ? false : bs == 0u;
   const uint32_t hs = dbl ? 0u : bs, ws = dbl ? bs : 0u;
   // first sub-move: the lists, the shortcuts, then every lane's checks at once

@@ -246,11 +246,25 @@ __global__ void __launch_bounds__(kBlock, 1) k_rollout_wave(Planes pl, int n, Rn
   Side s = valid ? side_from_record(pl.p0[i], pl.p1[i]) : side_start(0u);
   int4 st = make_int4(0, 0, 0, 0);
   uint32_t R[4];  // the Philox block of the current ply pair
+  const int lane = (int)(threadIdx.x & 63);
   for (int p = 0; p < plies; ++p) {
+    // ply() with the block test first: a wave with no block-bound lane
+    // plays turn_free (no cooperative pass, no block filter), else the
+    // cooperative turn with the test's result
+    uint32_t r[4];
+    ply_draw_cached(g, s.t, (uint32_t)i, R, p == 0, r);
+    int d0, d1;
+    dice_from(r[0], g.dice_mode, d0, d1);
+    const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
+    const uint32_t bs = turn_block_set(s.O, s.S1o, s.P, block_lowmask(s.P), dh, dl);
+    uint32_t w[4];
+    turn_words(r, w);
+    const uint32_t mover_black = s.black;
     TurnOut o;
+    if (__ballot(bs != 0u) == 0ull) turn_free(s, dh, dl, w, o);
+    else coop_turn_full<false, true>(s, d0, d1, false, ~0ull, w, o, lane, bs);
     int term, trunc;
-    ply(s, st, g, (uint32_t)i, valid, (const int8_t*)nullptr, nullptr, max_steps, true, o, term, trunc, R,
-        p == 0);
+    ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, true, term, trunc);
     if (kOut && valid) store_outs(out, (size_t)p * n + i, s, o, term, trunc, nullptr, false);
   }
   int4 cum = make_int4(0, 0, 0, 0);
