@@ -272,16 +272,35 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
 // f4_open_moves) with every C_k = L_k.  No cross-lane operation but the
 // sub-move loop's early exit, so it may run with lanes masked off.  The
 // random-legal policy only (the rollout).
-__device__ __forceinline__ void turn_free(Side& s, int dh, int dl, const uint32_t w[4], TurnOut& o) {
+// kBound2: lanes with bs != 0 (turn_block_set's holes) are block-bound
+// TWO-dice turns (the caller sends waves with a block-bound doubles lane to
+// coop_turn_full): their lists block-filtered, their first moves kept from
+// the sure-move masks (f4_sure_pair) and, for the rest, the per-source pair
+// check (f4_keep_pair: a per-lane loop, usually empty) -- env_turn_full's
+// two-dice branch inline, with no cooperative pass.
+template <bool kBound2 = false>
+__device__ __forceinline__ void turn_free(Side& s, int dh, int dl, const uint32_t w[4], TurnOut& o,
+                                          uint32_t bs = 0u) {
   const bool dbl = dh == dl;
-  const uint32_t Lh = die_candidates(s.O, s.P, dh);
-  const uint32_t Ll = dbl ? 0u : die_candidates(s.O, s.P, dl);
+  uint32_t Lh = die_candidates(s.O, s.P, dh);
+  uint32_t Ll = dbl ? 0u : die_candidates(s.O, s.P, dl);
   const int hl0 = (dbl && s.ft_own && (dh == 3 || dh == 4 || dh == 6)) ? 2 : 1;
+  const bool b2 = kBound2 && bs != 0u;
+  const uint32_t low = kBound2 ? block_lowmask(s.P) : 0u;
   uint32_t Ch, Cl;
   int M;
   if (!dbl) {
-    Ch = f4_keep_pair_bf(s.O, s.S1o, s.P, dh, dl, Lh);
-    Cl = f4_keep_pair_bf(s.O, s.S1o, s.P, dl, dh, Ll);
+    if (b2) {
+      const Blocks bl = block_info_low(s.O, low);
+      Lh = die_filter(s.O, s.S1o, bl, Lh, dh);
+      Ll = die_filter(s.O, s.S1o, bl, Ll, dl);
+      const uint32_t sh = f4_sure_pair(s.O, s.P, dl, Lh, bs), sl = f4_sure_pair(s.O, s.P, dh, Ll, bs);
+      Ch = sh | f4_keep_pair(s, low, dh, dl, Lh & ~sh, false);
+      Cl = sl | f4_keep_pair(s, low, dl, dh, Ll & ~sl, false);
+    } else {
+      Ch = f4_keep_pair_bf(s.O, s.S1o, s.P, dh, dl, Lh);
+      Cl = f4_keep_pair_bf(s.O, s.S1o, s.P, dl, dh, Ll);
+    }
     if (Ch | Cl) {
       M = 2;
     } else {
@@ -297,8 +316,9 @@ __device__ __forceinline__ void turn_free(Side& s, int dh, int dl, const uint32_
     M = Lh ? Mx : 0;
   }
   turn_play(s, dh, dl, Ch, Cl, M, hl0, false, ~0ull, w, o,
-            [](int k, int dk, int need, bool act, int hl, uint32_t Lk) -> uint32_t {
-              (void)k; (void)dk; (void)need; (void)act;
+            [&](int k, int dk, int need, bool act, int hl, uint32_t Lk) -> uint32_t {
+              (void)k; (void)need;
+              if (kBound2 && b2 && act) Lk = die_filter(s.O, s.S1o, block_info_low(s.O, low), Lk, dk);
               return hl <= 0 ? (Lk & ~HEAD) : Lk;
             });
 }

@@ -249,8 +249,10 @@ __global__ void __launch_bounds__(kBlock, 1) k_rollout_wave(Planes pl, int n, Rn
   const int lane = (int)(threadIdx.x & 63);
   for (int p = 0; p < plies; ++p) {
     // ply() with the block test first: a wave with no block-bound lane
-    // plays turn_free (no cooperative pass, no block filter), else the
-    // cooperative turn with the test's result
+    // plays turn_free (no cooperative pass, no block filter), a wave whose
+    // block-bound lanes all roll two different dice turn_free<true> (their
+    // general two-dice turn inline), else the cooperative turn with the
+    // test's result
     uint32_t r[4];
     ply_draw_cached(g, s.t, (uint32_t)i, R, p == 0, r);
     int d0, d1;
@@ -262,6 +264,7 @@ __global__ void __launch_bounds__(kBlock, 1) k_rollout_wave(Planes pl, int n, Rn
     const uint32_t mover_black = s.black;
     TurnOut o;
     if (__ballot(bs != 0u) == 0ull) turn_free(s, dh, dl, w, o);
+    else if (__ballot(bs != 0u && dh == dl) == 0ull) turn_free<true>(s, dh, dl, w, o, bs);
     else coop_turn_full<false, true>(s, d0, d1, false, ~0ull, w, o, lane, bs);
     int term, trunc;
     ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, true, term, trunc);
