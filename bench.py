@@ -212,6 +212,31 @@ def load_engine(local_rank):
     return mod.Engine(local_rank)
 
 
+def aligned_start(world, dev):
+    """After the barrier + synchronize: every rank starts its clock at the
+    same instant of the node's monotonic clock (CLOCK_MONOTONIC is one clock
+    for every process of a node) -- a little after the slowest rank has left
+    the barrier (one MAX all-reduce of each rank's exit time).  Ranks leave
+    a barrier at different times (host wake-up jitter), and with the max
+    over ranks of per-rank spans that jitter would be timed as work.
+    Returns this rank's barrier-exit lag behind the slowest rank (us)."""
+    if world == 1:
+        return 0.0
+    import torch
+    import torch.distributed as dist
+
+    mine = time.monotonic()
+    t = torch.tensor([mine], dtype=torch.float64)
+    if dist.get_backend() != "gloo":
+        t = t.to(dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    latest = float(t.cpu()[0])
+    go = latest + 0.002  # after the all-reduce has returned on every rank
+    while time.monotonic() < go:
+        pass
+    return round((latest - mine) * 1e6, 1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -382,6 +407,7 @@ def main():
     eng.sync()
     barrier()
     eng.sync()
+    start_skew_us = aligned_start(world, dev)
 
     # HIP events on the launching stream around the launches of the timed
     # region (no per-launch event between them): kernel time per launch =
@@ -406,7 +432,8 @@ def main():
         eng.sync()
     t_close = time.perf_counter() - t0
     gc.enable()
-    host_us = {"submit": round((t_sub - t0) * 1e6, 1), "gather_call": round((t_tot - t_sub) * 1e6, 1),
+    host_us = {"start_skew_removed": start_skew_us,
+               "submit": round((t_sub - t0) * 1e6, 1), "gather_call": round((t_tot - t_sub) * 1e6, 1),
                "wait": round((elapsed - (t_tot - t0)) * 1e6, 1),
                "closing_barrier_untimed": round((t_close - elapsed) * 1e6, 1)}
     span_ms = ev0.elapsed_ms(ev1)
