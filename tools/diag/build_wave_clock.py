@@ -115,6 +115,22 @@ def build(tag, force_full, drift=None, cut=None, wave=None, prio=None):
     s = sub(s, "    lds_publish(&M.fin, 1u);\n", "    lds_publish(&M.fin, 1u);\n    if (lane == 0) TS[1] = wall_clock64();\n")
     s = sub(s, "      __builtin_amdgcn_s_sleep(24);\n    }\n",
             "      __builtin_amdgcn_s_sleep(24);\n    }\n    if (lane == 0) TS[1] = wall_clock64();\n")
+    if wave == "passes":  # count the cooperative passes (owners > 0) per wave, by mode
+        q = os.path.join(csrc, "kernels_full4.h")
+        t = open(q).read()
+        t = sub(t, "__device__ void coop_run(", "__device__ unsigned g_passes[4096 * 2];\n__device__ void coop_run(")
+        t = sub(t, "  const int which = lane >> 5, p = lane & 31;\n  while (owners) {",
+                "  const int which = lane >> 5, p = lane & 31;\n"
+                "  if (owners != 0ull && lane == 0)\n"
+                "    atomicAdd(&g_passes[((blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 2 + (mode ? 1 : 0)],\n"
+                "              (unsigned)__builtin_popcountll(owners));\n"
+                "  while (owners) {")
+        open(q, "w").write(t)
+        s2 = open(os.path.join(csrc, "narde.hip")).read()
+        s2 += ('\nextern "C" int narde_diag_passes(unsigned* host, int zero) {\n'
+               '  if (zero) { static unsigned z[4096 * 2]; return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_passes), z, sizeof(z)); }\n'
+               '  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_passes), sizeof(g_passes));\n}\n')
+        open(os.path.join(csrc, "narde.hip"), "w").write(s2)
     if wave == "free":
         s = sub(s, WAVE_PLY, WAVE_FAST % "__ballot(bs != 0u) == 0ull")
     elif wave == "allfree":

@@ -31,9 +31,13 @@ def main():
     torch.cuda.synchronize()
     full = "full" in tag
     nw = 2048 if full else 1024
+    passes = hasattr(lib, "narde_diag_passes")
     for trial in range(6):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         env.rollout(P, b)
+        torch.cuda.synchronize()
+        if passes:
+            assert lib.narde_diag_passes(None, 1) == 0
         e0.record()
         env.rollout(P, b)
         e1.record()
@@ -54,6 +58,17 @@ def main():
                "life_mean_us": round(float(life.mean()), 2)}
         if full:
             out["helper_end_max_us"] = q(rel[~rule, 1], 100)
+        if passes:  # owner-passes per wave (depth / pair) against the wave's end
+            pc = np.zeros((4096, 2), dtype=np.uint32)
+            assert lib.narde_diag_passes(pc.ctypes.data_as(ctypes.c_void_p), 0) == 0
+            pc = pc[:nw].astype(np.float64)
+            ends = rel[:, 1]
+            X = np.column_stack([np.ones(nw), pc[:, 0], pc[:, 1]])
+            coef, *_ = np.linalg.lstsq(X, ends, rcond=None)
+            out["passes"] = {"depth_mean": round(float(pc[:, 0].mean()), 2), "depth_max": int(pc[:, 0].max()),
+                             "pair_mean": round(float(pc[:, 1].mean()), 2), "pair_max": int(pc[:, 1].max()),
+                             "fit_us": [round(float(c), 3) for c in coef],
+                             "slowest_wave_passes": pc[int(np.argmax(ends))].astype(int).tolist()}
         # which workgroups hold the slowest waves (per-CU placement is not known)
         out["slowest_waves"] = [int(x) for x in np.argsort(-rel[:, 1])[:5]]
         print(json.dumps(out), flush=True)
