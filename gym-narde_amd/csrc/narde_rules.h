@@ -927,26 +927,44 @@ NARDE_FN bool f4_bearoff_fixed(const Side& s, int rem = 4) {
   return (int)(15u - s.off_own - home) >= rem;
 }
 
-// f4_lower_bound for a block-bound doubles turn, from ws = dbl_block_windows
+// f4_chain_bound for a block-bound doubles turn, from ws = dbl_block_windows
 // (its failing windows: no other window can ever fill this turn).  Only
-// sources whose landing cannot fill a failing window count: not a hole of
+// steps whose landing cannot fill a failing window count: not a hole of
 // one, not a window point some sub-move may vacate (a source now, or a
-// bear-off source once bear-off opens, if it can this turn).  Such moves
-// are never rejected, in any order, and any sub-move lowers the count by at
-// most one (the window set stays that of the root) -- so, as for the
-// block-free bound, >= 4 at the root gives M = 4 and every C_k = L_k.
-// ws = 0 (block-free) gives f4_lower_bound itself.  Settles ~1/4 of the
-// block-bound doubles turns of random self-play.
+// bear-off source once bear-off opens, if it can this turn).  Such steps are
+// never rejected, in any order; a checker walks on over them (its chain).
+// The count (min(count, 2) checkers per point) is at most E = the sum over
+// checkers of their chain lengths, a legal sub-move lowers E by at most one
+// (the mover keeps the rest of its chain, the others theirs; the window set
+// stays that of the root), and min(4, E) sub-moves stay playable -- so, as
+// for the block-free bounds, >= 4 at the root gives M = 4 and every C_k = L_k.
+// ws = 0 (block-free) gives f4_chain_bound itself.  Settles 38 % of the
+// block-bound doubles turns of random self-play (the single steps alone,
+// the first form: 23 %); every legal path of each settled turn checked in
+// tools/diag/safe_chain_check.cpp.
 NARDE_FN int f4_safe_bound(const Side& s, int d, int hl, uint32_t ws) {
   if (ws == ~0u) return 0;
-  const uint32_t C = die_candidates(s.O, s.P, d);
+  const uint32_t O = s.O, P = s.P;
+  const uint32_t C = die_candidates(O, P, d);
   const uint32_t opens = f4_bearoff_fixed(s) ? 0u : ((1u << d) - 1u);
-  const uint32_t bad = ws & (~s.O | C | opens);
-  uint32_t L = C & ~(bad << d);
-  if (hl <= 0) L &= ~HEAD;
-  const uint32_t body = L & ~HEAD;
-  const int head = (L & HEAD) ? ((hl >= 2 && !(s.S1o & HEAD)) ? 2 : 1) : 0;
-  return __builtin_popcount(body) + __builtin_popcount(body & ~s.S1o) + head;
+  const uint32_t bad = ws & (~O | C | opens);
+  const uint32_t gn = (~(P | bad) << d) & (MASK24 << d) & MASK24;  // y: y - d free, safe
+  const uint32_t go = ((O >> 6) == 0u) ? ((1u << d) - 1u) : 0u;    // y: bears off
+  const uint32_t a = gn | go;
+  const uint32_t keep = hl > 0 ? O : (O & ~HEAD);
+  const uint32_t g1 = gn & (gn << d), g2 = g1 & (gn << (2 * d));
+  const uint32_t c1 = keep & a;
+  const uint32_t c2 = keep & gn & (a << d);
+  const uint32_t c3 = keep & g1 & (a << (2 * d));
+  const uint32_t c4 = keep & g2 & (a << (3 * d));
+  const uint32_t multi = ~s.S1o & ~HEAD;
+  const int hm = (hl >= 2 && !(s.S1o & HEAD)) ? 2 : 1;
+  int lb = __builtin_popcount(c1 & ~HEAD) + __builtin_popcount(c2 & ~HEAD) +
+           __builtin_popcount(c3 & ~HEAD) + __builtin_popcount(c4 & ~HEAD) +
+           __builtin_popcount(c1 & multi) + __builtin_popcount(c2 & multi) +
+           __builtin_popcount(c3 & multi) + __builtin_popcount(c4 & multi);
+  lb += hm * (int)(((c1 >> 23) & 1u) + ((c2 >> 23) & 1u) + ((c3 >> 23) & 1u) + ((c4 >> 23) & 1u));
+  return lb;
 }
 
 // Exact sub-move count of a block-free doubles turn whose bear-off status

@@ -58,7 +58,7 @@ int main() {
     S[e] = side_start(e & 1);
     ST[e] = make_int4(0, 0, 0, 0);
   }
-  long turns = 0, searched = 0, unsound = 0, later_need = 0, later_bf = 0;
+  long turns = 0, searched = 0, unsound = 0, later_need = 0, later_bf = 0, later_safe = 0, later_either = 0, later_root = 0, need2 = 0, later_root2 = 0;
   std::vector<long> maxn, maxp, sumn, sump;
   for (int p = 0; p < plies; ++p)
     for (int e = 0; e < n; ++e) {
@@ -120,7 +120,19 @@ int main() {
                 const int need = M - k - 1;
                 if (need > 0) {
                   ++later_need;
-                  if (dbl_block_free(u.O, u.S1o, u.P, low, d, M - k)) ++later_bf;
+                  const bool bfk = dbl_block_free(u.O, u.S1o, u.P, low, d, M - k);
+                  const bool sfk = f4_safe_bound(u, d, hl, dbl_block_windows(u.O, u.S1o, u.P, low, d, M - k)) >= M - k;
+                  later_bf += bfk;
+                  later_safe += sfk;
+                  later_either += bfk || sfk;
+                  // the same with the root's failing windows (no window test at the node)
+                  const bool srk = f4_safe_bound(u, d, hl, bs) >= M - k;
+                  later_root += srk;
+                  if (srk && f4_keep_rt(u, low, d, hl, Lk, need, false) != Lk) ++unsound;
+                  need2 += need == 2;
+                  later_root2 += srk && need == 2;
+                  // the safe bound settles the node: every source keeps M - k - 1
+                  if (sfk && f4_keep_rt(u, low, d, hl, Lk, need, false) != Lk) ++unsound;
                 }
                 C = need > 0 ? f4_keep_rt(u, low, d, hl, Lk, need, false) : Lk;
               }
@@ -143,7 +155,9 @@ int main() {
   printf("max nodes per turn (slowest source): mean %.1f p50 %ld p90 %ld p99 %ld max %ld\n", mean(maxn), pct(maxn, .5), pct(maxn, .9), pct(maxn, .99), pct(maxn, 1.0));
   printf("  with the relaxed bound:             mean %.1f p50 %ld p90 %ld p99 %ld max %ld\n", mean(maxp), pct(maxp, .5), pct(maxp, .9), pct(maxp, .99), pct(maxp, 1.0));
   printf("total nodes per turn: mean %.1f -> %.1f\n", mean(sumn), mean(sump));
-  printf("later sub-moves that search: %ld, settled by the block-free shortcut: %ld\n", later_need, later_bf);
+  printf("later sub-moves that search: %ld, settled by the block-free shortcut: %ld, by f4_safe_bound: %ld, by either: %ld\n",
+         later_need, later_bf, later_safe, later_either);
+  printf("  by f4_safe_bound with the root's windows: %ld (need 2: %ld of %ld)\n", later_root, later_root2, need2);
   printf("unsound prunes (depth differs): %ld\n", unsound);
   return unsound != 0;
 }

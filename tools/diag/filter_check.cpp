@@ -1,5 +1,7 @@
-// DIAGNOSTIC (host): the loop-free block filter (narde_rules.h die_filter, round 3)
-// against the per-candidate loop it replaced (restated here as
+// DIAGNOSTIC (host): narde_rules.h's die_filter and a loop-free form of it
+// (die_filter_x below: measured slower on both rules, also when used only
+// in block-bound turns -- DESIGN.md 10) against the per-candidate loop
+// (restated here as
 // filter_loop: every single-checker source whose move may complete a
 // window tested by runs6 of its child board), for every die, on FULL4
 // self-play positions and on random positions rich in 6-runs.  Must print 0
@@ -46,6 +48,32 @@ static uint32_t filter_loop(uint32_t O, uint32_t S1, uint32_t low, uint32_t C, i
   return L;
 }
 
+// After a single-checker source p moves to q = p - d, an allowed window
+// violates iff it does not hold p and is either already full (a bit of F
+// outside [p-5, p]) or completed by q with its other five points own --
+// window [q-a, q-a+5] misses p iff a >= 6 - d.
+static uint32_t die_filter_x(uint32_t O, uint32_t S1, uint32_t low, uint32_t C, int d) {
+  const uint32_t r2 = O & (O >> 1);
+  const uint32_t r3 = r2 & (O >> 2);
+  const uint32_t r4 = r2 & (r2 >> 2);
+  const uint32_t r5 = r4 & (O >> 4);
+  const uint32_t F = r4 & (r2 >> 4) & low;
+  const uint32_t lp = low + 1u;
+  const uint32_t t0 = (r5 >> 1) & low;
+  const uint32_t t1 = (O << 1) & (r4 >> 1) & ((lp << 1) - 1u);
+  const uint32_t t2 = (r2 << 2) & (r3 >> 1) & ((lp << 2) - 1u);
+  const uint32_t t3 = (r3 << 3) & (r2 >> 1) & ((lp << 3) - 1u);
+  const uint32_t t4 = (r4 << 4) & (O >> 1) & ((lp << 4) - 1u);
+  const uint32_t t5 = (r5 << 5) & ((lp << 5) - 1u);
+  const uint32_t Q = (t0 | t1 | t2 | t3 | t4 | t5) & ~O & MASK24;
+  const uint32_t Qd = (t5 | (d >= 2 ? t4 : 0u) | (d >= 3 ? t3 : 0u) | (d >= 4 ? t2 : 0u) | (d >= 5 ? t1 : 0u) |
+                       (d >= 6 ? t0 : 0u)) & ~O & MASK24;
+  const int fmin = __builtin_ctz(F | (1u << 31)), fmax = 31 - __builtin_clz(F | 1u);
+  const uint32_t v1 = F ? ((~0u << (fmin + 6)) | ((1u << fmax) - 1u)) : 0u;
+  const uint32_t hit = F ? MASK24 : (Q << d);
+  return C & ~(hit & ~S1) & ~(S1 & (v1 | (Qd << d)));
+}
+
 static long checked = 0, bad = 0, differs = 0;
 
 static void check(uint32_t O, uint32_t S1, uint32_t P) {
@@ -54,9 +82,11 @@ static void check(uint32_t O, uint32_t S1, uint32_t P) {
   for (int d = 1; d <= 6; ++d) {
     const uint32_t C = die_candidates(O, P, d);
     const uint32_t a = filter_loop(O, S1, low, C, d), b = die_filter(O, S1, bl, C, d);
+    const uint32_t x = die_filter_x(O, S1, low, C, d);
     ++checked;
     differs += a != C;
-    if (a != b) {
+    if (a != b || a != x) {
+      if (bad < 10) printf("  loop-free %06x\n", x);
       if (bad < 10) printf("O %06x S1 %06x P %06x d %d: loop %06x new %06x\n", O, S1, P, d, a, b);
       ++bad;
     }
