@@ -154,22 +154,72 @@ def load_traffic(path, envs, plies):
     return d.get("hbm_bytes_per_launch")
 
 
+# SURVEY.md 8(d)'s secondary figure: VALU wave-instructions per launch (a
+# committed SQ-counter summary at the launch shape, tools/sq_summary.py)
+# against the chip's integer VALU issue peak -- one VALU wave-instruction per
+# 4 cycles per SIMD (tools/sq_summary.py's docstring)
+ISSUE_PEAK = 1024 * 2.4e9 / 4
+
+
+def load_issue(full4, envs, plies, kernel_ms):
+    """The issue roofline of a launch of this shape: profiles/sq_k_rollout
+    [_full]_p<plies>.json's VALU wave-instructions per launch over the
+    launch's live duration (kernel_ms), or None if no summary was measured
+    at this shape."""
+    path = os.path.join(ROOT, "profiles", f"sq_k_rollout{'_full' if full4 else ''}_p{plies}.json")
+    try:
+        d = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if d.get("envs") != envs or d.get("plies") != plies or not d.get("valu_per_launch") or not kernel_ms:
+        return None
+    achieved = d["valu_per_launch"] / (kernel_ms * 1e-3)
+    return {
+        "bound": "valu-issue",
+        "valu_per_launch": d["valu_per_launch"],
+        "salu_per_launch": d.get("salu_per_launch"),
+        "valu_per_wave_ply": d.get("valu_per_env_ply"),
+        "achieved": round(achieved / 1e9, 2),
+        "peak": round(ISSUE_PEAK / 1e9, 2),
+        "unit": "G VALU wave-instructions/s",
+        "frac": round(achieved / ISSUE_PEAK, 4),
+        "valu_busy_of_wave_cycles": d.get("valu_busy_of_wave_cycles"),
+        "source": os.path.relpath(path, ROOT),
+    }
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
 
 
-def spawn_ranks(n, argv):
+# the launching process's CPU baseline, handed to rank 0 (spawn_ranks)
+CPU_BASELINE_ENV = "NARDE_BENCH_CPU_BASELINE"
+
+
+def spawn_ranks(n, argv, cpu=None):
     """Start the N-rank bench as the driver would (torch.distributed.run,
     one process per GPU, rendezvous on 127.0.0.1) and return its exit code.
     Called before this process touches the GPU; the ranks are children (no
-    exec), and rank 0's JSON line reaches our stdout."""
+    exec), and rank 0's JSON line reaches our stdout.  `cpu`: the CPU
+    baseline this process measured before starting them (rank 0 reports it
+    instead of measuring it again)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL on this host driver)
+    if cpu is not None:
+        env[CPU_BASELINE_ENV] = json.dumps(cpu)
     return subprocess.call(cmd, env=env)
+
+
+def measure_cpu_baseline(args):
+    """The CPU baseline leg (before any GPU call: the pool forks)."""
+    cores, how = available_cores()
+    if args.cpu_cores > 0:
+        cores, how = args.cpu_cores, f"--cpu-cores {args.cpu_cores}"
+    return cpu_baseline(args.cpu_seconds, cores, how)
 
 
 class GpuEngine:
@@ -212,6 +262,11 @@ def load_engine(local_rank):
     return mod.Engine(local_rank)
 
 
+def single_node(world):
+    """Every rank on this node (torchrun's LOCAL_WORLD_SIZE == WORLD_SIZE)."""
+    return int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world
+
+
 def aligned_start(world, dev):
     """After the barrier + synchronize: every rank starts its clock at the
     same instant of the node's monotonic clock (CLOCK_MONOTONIC is one clock
@@ -219,9 +274,13 @@ def aligned_start(world, dev):
     the barrier (one MAX all-reduce of each rank's exit time).  Ranks leave
     a barrier at different times (host wake-up jitter), and with the max
     over ranks of per-rank spans that jitter would be timed as work.
-    Returns this rank's barrier-exit lag behind the slowest rank (us)."""
+    Returns this rank's barrier-exit lag behind the slowest rank (us), or
+    None where the clocks are not one clock (ranks on several nodes: the
+    plain barrier stands)."""
     if world == 1:
         return 0.0
+    if not single_node(world):
+        return None
     import torch
     import torch.distributed as dist
 
@@ -276,8 +335,11 @@ def main():
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None:
         if args.gpus is not None and args.gpus > 1:
-            # the N ranks, started here before any GPU call (no exec)
-            return spawn_ranks(args.gpus, sys.argv[1:])
+            # the N ranks, started here before any GPU call (no exec); the CPU
+            # baseline first, on this launching process, so the N-GPU line
+            # carries it too
+            cpu = None if args.no_cpu_baseline else measure_cpu_baseline(args)
+            return spawn_ranks(args.gpus, sys.argv[1:], cpu)
         world_env = "1"
     world_env = int(world_env)
     if args.gpus is None:
@@ -291,12 +353,13 @@ def main():
         devnull = os.open(os.devnull, os.O_WRONLY)
         os.dup2(devnull, 1)
         os.close(devnull)
+    # the CPU baseline on rank 0 at every world size, before any GPU call:
+    # the launching process's (spawn_ranks), else measured here (under an
+    # outside launcher the other ranks wait in the rendezvous meanwhile)
     cpu = None
-    if world_env == 1 and rank_env == 0 and not args.no_cpu_baseline:
-        cores, how = available_cores()
-        if args.cpu_cores > 0:
-            cores, how = args.cpu_cores, f"--cpu-cores {args.cpu_cores}"
-        cpu = cpu_baseline(args.cpu_seconds, cores, how)
+    if rank_env == 0 and not args.no_cpu_baseline:
+        handed = os.environ.get(CPU_BASELINE_ENV)
+        cpu = json.loads(handed) if handed else measure_cpu_baseline(args)
 
     import torch
     import torch.distributed as dist
@@ -392,13 +455,17 @@ def main():
     # RCCL's C API cannot be set up
     rows_view = D.gather_total_rows(rows_buf)  # one rank: the (1, R, 3) view, no collective
     gather, gather_impl = (lambda: rows_view), "none (one rank)"
+    rccl = None
     if world > 1:
         gather = lambda: D.gather_total_rows(rows_buf)  # noqa: E731
         gather_impl = "ProcessGroup all_gather_into_tensor"
         if dist.get_backend() == "nccl":
+            # RcclGather agrees across ranks at every stage: it either builds
+            # on every rank or raises on every rank, so the fallback is common
             try:
-                gather, gather_impl = D.RcclGather(rows_buf), "ncclAllGather (RCCL C API, launching stream)"
-            except (OSError, RuntimeError, AttributeError) as exc:
+                rccl = D.RcclGather(rows_buf)
+                gather, gather_impl = rccl, "ncclAllGather (RCCL C API, launching stream)"
+            except RuntimeError as exc:
                 gather_impl += f" (RCCL C API unavailable: {exc})"
     # every call of the timed region once, untimed: a first call pays one-off
     # host costs (the first unsqueeze of this process took ~150 us,
@@ -408,6 +475,8 @@ def main():
     barrier()
     eng.sync()
     start_skew_us = aligned_start(world, dev)
+    if start_skew_us is None:  # several nodes: no shared clock, the barrier stands
+        start_skew_us = "n/a (ranks on several nodes: plain barrier)"
 
     # HIP events on the launching stream around the launches of the timed
     # region (no per-launch event between them): kernel time per launch =
@@ -552,6 +621,7 @@ def main():
             "bytes_per_launch": obytes,
             "achieved_GBps": round(obytes / (other_ms * 1e-3) / 1e9, 2),
             "frac": round(obytes / (other_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+            "issue": load_issue(other_rules == "full4", per, P, other_ms),
             "max_dice_hist": other_M,
         }
 
@@ -641,6 +711,14 @@ def main():
             "full4": ("configs[2] as written: 65536 envs/GPU, full rules incl. 4-move doubles "
                       "(FULL4); the REF2 leg is other_rules"),
         }
+        if world > 1:
+            # configs[4]: 524,288 envs sharded over 8 GPUs (its N = 2 / 4
+            # points: the same 65,536-env shards on fewer GPUs)
+            c4 = ("configs[4]: batch=524288 sharded 8 x MI355X (8 x 65536 contiguous global env ids), "
+                  "one RCCL all-gather of the episode totals" if world * per == 524288 else
+                  f"configs[4]'s layout at {world} GPUs: {world} x {per} = {world * per} envs, contiguous "
+                  f"global env-id shards, one RCCL all-gather of the episode totals")
+            config_txt = {k: f"{c4}; per GPU {v}" for k, v in config_txt.items()}
         parity_txt = {
             "ref2": ("bit-exact vs the reference's golden vectors and the CPU oracle; unpinned: "
                      "TimeLimit truncation (gymnasium semantics, gymnasium absent) and the device "
@@ -697,6 +775,8 @@ def main():
                 "traffic": traffic,
                 "bytes_per_launch": nbytes,
                 "kernel_ms": round(kern_ms, 5),
+                # the same launch against the integer VALU issue peak
+                "issue": load_issue(is_full4, per, P, kern_ms),
             },
             # rank 0's wall split of the timed region: launches submitted,
             # waiting for them (and the gather), the closing barrier + sync
@@ -716,6 +796,9 @@ def main():
         sys.stdout.write("\n" + json.dumps(line) + "\n")
         sys.stdout.flush()
     env.close()
+    if rccl is not None:  # its communicator before the process group's
+        eng.sync()
+        rccl.close()
     if world > 1:
         dist.destroy_process_group()
 

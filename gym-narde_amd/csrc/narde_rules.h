@@ -392,7 +392,7 @@ NARDE_FN void legal2_entry(const Legal& l, int i, int& f, int& t) {
   t = f - d < 0 ? OFF : f - d;
 }
 
-// `move in valid_moves` (narde_env.py:255/281 analogue) in O(n)
+// `move in valid_moves` (narde_env.py:63 for move 1, :89 for move 2) in O(n)
 NARDE_FN bool legal_contains(const Legal& l, int f, int t) {
   if (f < 0 || f > 23) return false;
   const uint32_t bf = 1u << f;
@@ -404,7 +404,7 @@ NARDE_FN bool legal_contains(const Legal& l, int f, int t) {
 
 NARDE_FN int encode_move(int f, int t) { return f * 24 + (t == OFF ? 0 : t); }
 
-// narde_env.py:238-254 action decode (the 'off' quirk: to==0 & from<=5)
+// narde_env.py:45-62 action decode (the 'off' quirk: to==0 & from<=5)
 NARDE_FN void decode_action(int code, int& f, int& t) {
   if (code < 0 || code >= 576) { f = -1; t = -1; return; }
   f = code / 24;

@@ -124,6 +124,18 @@ def _rccl():
     return lib
 
 
+def agree(ok, device=None):
+    """True on every rank iff `ok` is true on every rank: one MIN all-reduce
+    (a device tensor on the nccl backend, a host one on gloo).  Without a
+    process group: `ok` itself."""
+    if not dist.is_initialized():
+        return bool(ok)
+    dev = device if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return bool(int(t.cpu()[0]))
+
+
 class RcclGather:
     """gather_total_rows through RCCL's own C API: one ncclAllGather on the
     caller's stream (ring / direct xGMI transfers of every rank's rows into
@@ -132,30 +144,57 @@ class RcclGather:
     and event bookkeeping on the host (~20 us after a bare launch, ~80 us
     after a launch bracketed by timing markers: tools/diag/launch_after_marker.py).
     Built collectively from an initialised process group (the unique id is
-    broadcast through it); the same bytes as gather_total_rows."""
+    broadcast through it); the same bytes as gather_total_rows.
+
+    Every stage ends with the ranks agreeing (`agree`, or rank 0's status
+    byte riding with the unique id), so either every rank gets a
+    communicator or every rank raises RuntimeError -- a caller that falls
+    back to the process group's collective on that error falls back on every
+    rank alike (a rank deciding alone would leave the others in
+    a broadcast, or in a different collective, forever)."""
 
     def __init__(self, rows):
-        self.lib = _rccl()
+        self.comm = ctypes.c_void_p()
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
-        uid = _NcclUniqueId()
-        if self.rank == 0:
-            self._check(self.lib.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
         dev = rows.device
-        idb = ctypes.string_at(ctypes.addressof(uid), 128)  # (c_char arrays stop at a NUL)
+        err = None
+        try:
+            self.lib = _rccl()
+        except (OSError, AttributeError) as exc:
+            self.lib, err = None, f"librccl: {exc}"
+        if not agree(err is None, dev):
+            raise RuntimeError(err or "RCCL C API unavailable on another rank")
+        # rank 0's unique id, with its status in byte 128 (one broadcast)
+        uid = _NcclUniqueId()
+        ok0 = 1
+        if self.rank == 0:
+            rc = self.lib.ncclGetUniqueId(ctypes.byref(uid))
+            if rc != 0:
+                ok0, err = 0, self._msg(rc, "ncclGetUniqueId")
+        idb = ctypes.string_at(ctypes.addressof(uid), 128) + bytes([ok0])  # (c_char arrays stop at a NUL)
         raw = torch.tensor(list(idb), dtype=torch.uint8, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.broadcast(raw, 0)
+        host = raw.cpu().tolist()
+        if host[128] != 1:
+            raise RuntimeError(err or "ncclGetUniqueId failed on rank 0")
         uid = _NcclUniqueId()
-        ctypes.memmove(ctypes.addressof(uid), bytes(raw.cpu().tolist()), 128)
-        self.comm = ctypes.c_void_p()
-        self._check(self.lib.ncclCommInitRank(ctypes.byref(self.comm), self.world, uid, self.rank),
-                    "ncclCommInitRank")
+        ctypes.memmove(ctypes.addressof(uid), bytes(host[:128]), 128)
+        rc = self.lib.ncclCommInitRank(ctypes.byref(self.comm), self.world, uid, self.rank)
+        if rc != 0:
+            self.comm, err = ctypes.c_void_p(), self._msg(rc, "ncclCommInitRank")
+        if not agree(rc == 0, dev):
+            self.close()
+            raise RuntimeError(err or "ncclCommInitRank failed on another rank")
         self.src = rows
         self.out = torch.empty((self.world,) + tuple(rows.shape), dtype=rows.dtype, device=dev)
         self.count = rows.numel()
 
+    def _msg(self, rc, what):
+        return f"{what} failed ({rc}): {self.lib.ncclGetErrorString(rc).decode()}"
+
     def _check(self, rc, what):
         if rc != 0:
-            raise RuntimeError(f"{what} failed ({rc}): {self.lib.ncclGetErrorString(rc).decode()}")
+            raise RuntimeError(self._msg(rc, what))
 
     def __call__(self, stream=None):
         """All-gather the rows tensor given at construction (its current
@@ -168,6 +207,6 @@ class RcclGather:
         return self.out
 
     def close(self):
-        if self.comm:
+        if self.comm and self.lib is not None:
             self.lib.ncclCommDestroy(self.comm)
             self.comm = ctypes.c_void_p()

@@ -91,3 +91,40 @@ def test_bench_gpus4_rank_totals(hostcheck, world):
     assert line["n_gpus"] == world and line["config"]["global_envs"] == world * 1024
     want = _oracle_rank_totals(1024, world, 3 * 10 + 10, seed=0)
     assert np.array_equal(np.array(line["config"]["rank_totals"], np.int64), want)
+
+
+def test_bench_gpus8_scale_line(hostcheck):
+    """the N = 8 line the driver's SCALE run prints --
+    8 ranks, configs[4] named at 8 x 65,536 global envs, a CPU baseline
+    measured by the launching process before the ranks start, and every
+    rank's totals equal to the oracle on the same global env ids."""
+    steps, ppl = 4, 4
+    quiet = [a for a in QUIET if a != "--no-cpu-baseline"]
+    p = _run(["--gpus", "8", "--steps", str(steps), "--warmup", "0", "--plies-per-launch", str(ppl),
+              "--envs", "65536", "--cpu-seconds", "0.3", "--cpu-cores", "2", *quiet], timeout=600)
+    line = _line(p)
+    assert line["n_gpus"] == 8
+    cfg = line["config"]
+    assert cfg["envs_per_gpu"] == 65536 and cfg["global_envs"] == 524288
+    assert cfg["workload"].startswith("configs[4]: batch=524288 sharded 8 x MI355X")
+    cpu = line["cpu_baseline"]
+    assert cpu is not None and cpu["value"] > 0 and cpu["cores"] == 2 and cpu["kind"] == "port"
+    assert isinstance(line["timed_region_host_us"]["start_skew_removed"], float)
+    want = _oracle_rank_totals(65536, 8, 3 * 2 * ppl + steps, seed=0)
+    assert np.array_equal(np.array(cfg["rank_totals"], np.int64), want)
+
+
+def test_aligned_start_only_on_one_node(monkeypatch):
+    """time.monotonic() is one clock only within a node; with
+    ranks on several nodes the aligned start is skipped (plain barrier)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("narde_bench", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert bench.single_node(8) and not bench.single_node(16)
+    assert bench.aligned_start(16, None) is None  # returns before any collective
+    assert bench.aligned_start(1, None) == 0.0
+    monkeypatch.delenv("LOCAL_WORLD_SIZE")
+    assert bench.single_node(4)

@@ -129,3 +129,77 @@ def test_gather_total_rows_without_process_group():
     rows = torch.arange(12, dtype=torch.int64).reshape(4, 3)
     out = gather_total_rows(rows)
     assert out.shape == (1, 4, 3) and torch.equal(out[0], rows)
+
+
+class _FakeRccl:
+    """Stands in for librccl in RcclGather's set-up: status
+    codes per entry point, no device work."""
+
+    def __init__(self, uid_rc=0, init_rc=0):
+        self.uid_rc, self.init_rc, self.destroyed = uid_rc, init_rc, 0
+
+    def ncclGetUniqueId(self, p):
+        return self.uid_rc
+
+    def ncclCommInitRank(self, comm, world, uid, rank):
+        if self.init_rc == 0:
+            ctypes.cast(comm, ctypes.POINTER(ctypes.c_void_p))[0] = 0x1234
+        return self.init_rc
+
+    def ncclCommDestroy(self, comm):
+        self.destroyed += 1
+        return 0
+
+    def ncclGetErrorString(self, rc):
+        return b"injected"
+
+
+def _rccl_agree_main(rank, world, port, case, out_path):
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "gym-narde_amd")]
+    import torch.distributed as dist
+
+    from gym_narde import distributed as D
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    D.init_from_env(backend="gloo")
+    fake = _FakeRccl()
+    if case == "load" and rank == 1:
+        def _fail():
+            raise OSError("injected: no librccl")
+        D._rccl = _fail
+    else:
+        if case == "uid" and rank == 0:
+            fake.uid_rc = 3
+        if case == "init" and rank == world - 1:
+            fake.init_rc = 2
+        D._rccl = lambda: fake
+    try:
+        g = D.RcclGather(torch.zeros((4, 3), dtype=torch.int64))
+        outcome = "built"
+        g.close()
+    except RuntimeError:
+        outcome = "raised"
+    # every rank reaches this barrier: no rank is left inside a collective
+    dist.barrier()
+    with open(f"{out_path}.{rank}", "w") as f:
+        f.write(f"{outcome} {fake.destroyed}")
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", ["load", "uid", "init", "ok"])
+def test_rccl_gather_setup_agrees_across_ranks(tmp_path, case):
+    """A failure at any set-up stage on any one rank makes every rank raise
+    (so bench.py falls back to the process group's collective on every rank
+    alike); with no failure every rank builds its communicator."""
+    world = 3
+    out = str(tmp_path / "outcome")
+    mp.spawn(_rccl_agree_main, args=(world, _free_port(), case, out), nprocs=world, join=True)
+    got = [open(f"{out}.{r}").read().split() for r in range(world)]
+    want = "built" if case == "ok" else "raised"
+    assert [g[0] for g in got] == [want] * world, got
+    if case == "init":  # the ranks whose init succeeded destroyed their communicator
+        assert [int(g[1]) for g in got] == [1] * (world - 1) + [0]
