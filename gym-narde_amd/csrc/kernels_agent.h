@@ -5,11 +5,18 @@
 
 namespace {
 
-// obs i32[n][24] (get_perspective_board of the mover), one env per thread
+// obs i32[n][24] (get_perspective_board of the mover), one env per thread;
+// a whole wave stages its 64 rows in LDS and stores them as contiguous
+// 1-KiB pieces (store_obs_wave; a partial wave stores per lane)
 __global__ void __launch_bounds__(kBlock) k_observe(Planes pl, int n, int32_t* __restrict__ obs) {
+  OBS_LDS_DECL
   const int i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  store_obs(obs, i, side_from_record(pl.p0[i], pl.p1[i]));
+  const int w0 = i - (int)(threadIdx.x & 63);
+  if (w0 + 64 <= n) {  // wave-uniform
+    store_obs_wave(obs, (size_t)i, side_from_record(pl.p0[i], pl.p1[i]), wave_lds);
+  } else if (i < n) {
+    store_obs(obs, (size_t)i, side_from_record(pl.p0[i], pl.p1[i]));
+  }
 }
 
 // One DQN transition for every env, fused (config 4, gym_narde/dqn.py
@@ -71,33 +78,75 @@ __device__ __forceinline__ float tes_value(uint4 a, uint4 b, int col) {
   return col >= 196 ? player : pv;
 }
 
-// The 198-float Tesauro observation f32[n][198] (README.md:42-102 layout,
-// absolute points: [white 24 x 4, bar, off, black 24 x 4, bar, off, player
-// one-hot]) with coalesced stores: each thread owns 4 consecutive floats of
-// the flat array (16 B, so every wave-wide store is one contiguous 1 KiB),
-// computed from the env record(s) they fall in (tes_value).  (One thread per
-// env writing its 792-B row, 8 B at a time, ran at 2.4 TB/s.)
-__global__ void __launch_bounds__(kBlock) k_tesauro198(Planes pl, int n, float* __restrict__ tes) {
-  const uint32_t total = (uint32_t)n * 198u;  // < 2^31 (checked on the host)
-  const uint32_t e0 = 4u * (blockIdx.x * kBlock + threadIdx.x);
-  if (e0 >= total) return;
-  const int i0 = (int)(e0 / 198u);
-  const int c0 = (int)(e0 - (uint32_t)i0 * 198u);
-  const uint4 a0 = pl.p0[i0], b0 = pl.p1[i0];
-  const bool split = c0 > 194 && i0 + 1 < n;  // the 4 floats reach into row i0 + 1
-  uint4 a1 = a0, b1 = b0;
-  if (split) { a1 = pl.p0[i0 + 1]; b1 = pl.p1[i0 + 1]; }
-  float nv[4];
+// The 198-float observation, a wave per 16 envs: lane l computes a quarter
+// of env (l & 15)'s row -- quarter q = l >> 4: white points 0-11 (columns
+// 0-47), white points 12-23 + bar + off (48-97), black points 0-11
+// (98-145), black points 12-23 + bar + off + player one-hot (146-197) --
+// from the record's nibbles with one bit-field extract per point (v, then
+// the four floats [v >= 1, v >= 2, v >= 3, (v - 3) / 2 if v >= 3]: the
+// values of tes_value, bit for bit), stages it in LDS, and the wave stores
+// its 16 contiguous rows (12,672 B) as 1-KiB pieces.  Layout (README.md:42-102,
+// absolute points): [white 24 x 4, bar, off, black 24 x 4, bar, off, player
+// one-hot].  (Round 3's kernel -- one thread per 4 output floats, each float
+// evaluated generically by tes_value, ~25 VALU per float -- was issue-bound:
+// 19.3 us for 54 MB.)
+constexpr int kTesEnvs = 16;                       // envs per wave
+constexpr int kTesRowB = 198 * 4;                  // bytes per row
+constexpr int kTesWaveB = kTesEnvs * kTesRowB;     // 12,672 B per wave
+static_assert(kTesWaveB % 16 == 0, "16-B pieces");
+
+__device__ __forceinline__ void tes_point4(uint32_t v, float* f) {
+  f[0] = v >= 1u ? 1.0f : 0.0f;
+  f[1] = v >= 2u ? 1.0f : 0.0f;
+  f[2] = v >= 3u ? 1.0f : 0.0f;
+  f[3] = v >= 3u ? (float)(v - 3u) / 2.0f : 0.0f;
+}
+
+__global__ void __launch_bounds__(kBlock) k_tesauro198_rows(Planes pl, int n, float* __restrict__ tes) {
+  __shared__ __attribute__((aligned(16))) float rows[kBlock / 64][kTesEnvs * 198];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int e0 = (blockIdx.x * (kBlock / 64) + wave) * kTesEnvs;  // first env of the wave
+  const int le = lane & 15, q = lane >> 4;
+  const int i = e0 + le;
+  float* row = rows[wave] + le * 198;
+  if (i < n) {
+    const uint4 a = pl.p0[i], b = pl.p1[i];
+    const int side = q >> 1, upper = q & 1;
+    const uint32_t w0 = side ? a.z : a.x, w1 = side ? a.w : a.y, w2 = side ? b.y : b.x;
+    // points 12q' .. 12q' + 11 of the side: 8 nibbles in X, 4 in Y
+    const uint32_t X = upper ? ((w1 >> 16) | (w2 << 16)) : w0;
+    const uint32_t Y = upper ? (w2 >> 16) : (w1 & 0xFFFFu);
+    float f[52];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int c = c0 + q;
-    const bool nx = c >= 198;  // the record first, then one evaluation (not both)
-    nv[q] = tes_value(nx ? a1 : a0, nx ? b1 : b0, nx ? c - 198 : c);
+    for (int k = 0; k < 8; ++k) tes_point4(__builtin_amdgcn_ubfe(X, 4u * k, 4u), f + 4 * k);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tes_point4(__builtin_amdgcn_ubfe(Y, 4u * k, 4u), f + 32 + 4 * k);
+    const uint32_t misc = b.z;
+    const float offv = (float)(side ? ((misc >> 4) & 15u) : (misc & 15u)) / 15.0f;
+    const bool black = (misc >> 10) & 1u;
+    f[48] = 0.0f;   // bar (always empty in Narde)
+    f[49] = offv;
+    f[50] = black ? 0.0f : 1.0f;  // player one-hot (quarter 3 only)
+    f[51] = black ? 1.0f : 0.0f;
+    // columns of the quarter: 0, 48, 98, 146 (8-B aligned: ds_write_b64)
+    const int c0 = q == 0 ? 0 : (q == 1 ? 48 : (q == 2 ? 98 : 146));
+    const int nf = q == 0 || q == 2 ? 48 : (q == 1 ? 50 : 52);
+#pragma unroll
+    for (int k = 0; k < 26; ++k)
+      if (2 * k < nf) *reinterpret_cast<float2*>(row + c0 + 2 * k) = make_float2(f[2 * k], f[2 * k + 1]);
   }
-  if (e0 + 4u <= total) {
-    *reinterpret_cast<float4*>(tes + e0) = make_float4(nv[0], nv[1], nv[2], nv[3]);
-  } else {
-    for (int q = 0; q < 4 && e0 + (uint32_t)q < total; ++q) tes[e0 + q] = nv[q];
+  __builtin_amdgcn_wave_barrier();  // the wave reads only its own rows: LDS ops of one wave retire in issue order
+  // the wave's rows: [e0, min(e0 + 16, n)) -> 16-B pieces, lane-major
+  const int rows_here = max(0, min(kTesEnvs, n - e0));
+  const uint32_t bytes = (uint32_t)rows_here * kTesRowB;
+  const float4* src = reinterpret_cast<const float4*>(rows[wave]);
+  float4* dst = reinterpret_cast<float4*>(tes + (size_t)e0 * 198);
+  for (uint32_t k = (uint32_t)lane; 16u * k < bytes; k += 64u) {
+    if (16u * k + 16u <= bytes) {
+      dst[k] = src[k];
+    } else {  // the row set ends inside this piece (an odd number of rows): its 8-B half
+      *reinterpret_cast<float2*>(reinterpret_cast<float*>(dst + k)) = *reinterpret_cast<const float2*>(src + k);
+    }
   }
 }
 

@@ -133,29 +133,69 @@ __device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t i,
           autoreset, o, term, trunc);
 }
 
-// one FULL4 ply of the random-legal policy with device dice, the block test
-// first: a wave with no block-bound lane plays turn_free (no cooperative
-// pass, no block filter), a wave whose block-bound lanes all roll two
-// different dice turn_free<true> (their general two-dice turn inline), else
-// the cooperative turn with the test's result.  Every lane of the wave must
-// call it.  (The cooperative turn for every wave: 0.522 against 0.469 ms per
-// 100 plies of 20-ply k_rollout_wave launches)
+// the words of ply p of a launch (env counter t): the Philox block on the
+// launch's first ply and on every even t.  par >= 0: every lane's counter
+// had parity par at ply 0 (every env's t advances by one per ply), so the
+// test is a scalar branch; par < 0: per lane
+__device__ __forceinline__ void ply_draw_wave(const Rng& g, uint32_t t, uint32_t i, uint32_t R[4], int p, int par,
+                                              uint32_t r[4]) {
+  if (par >= 0) {
+    if (p == 0 || ((par + p) & 1) == 0) ply_block(t, g.env0 + i, g.k0, g.k1, R);
+  } else if (p == 0 || (t & 1u) == 0u) {
+    ply_block(t, g.env0 + i, g.k0, g.k1, R);
+  }
+  ply_words_of(R, t, g.dice_mode, r);
+}
+
+// the wave's counter parity for ply_draw_wave (0 / 1, or -1 if mixed)
+__device__ __forceinline__ int wave_parity(bool valid, uint32_t t) {
+  const uint64_t odd = __ballot(valid && (t & 1u)), vm = __ballot(valid);
+  return odd == 0ull ? 0 : (odd == vm ? 1 : -1);
+}
+
+// one FULL4 ply of the random-legal policy with device dice (ply p of the
+// launch), the block test first.  A wave with no block-bound doubles lane
+// plays every lane's turn straight-line (narde_rules.h turn_c0_free +
+// turn_moves_sl: no branch whose condition differs between lanes), its
+// block-bound two-dice lanes taking env_turn_full's bound branch for C_0
+// (turn_c0_pair_bound) and block-filtered lists; a wave with a block-bound
+// doubles lane plays the cooperative turn with the test's result.  Every
+// lane of the wave must call it.  (Round 3 -- turn_free / turn_free<true>
+// with per-lane branches: 0.460 ms per 100 plies of 20-ply k_rollout_wave
+// launches)
+template <bool kFilt>
+__device__ __forceinline__ void ply_free_turn(Side& s, int dh, int dl, uint32_t low, uint32_t bs, const uint32_t w[4],
+                                              bool flip_always, TurnOut& o) {
+  uint32_t Lh, Ll, Ch, Cl;
+  int M, hl0;
+  turn_c0_free(s, dh, dl, Lh, Ll, Ch, Cl, M, hl0);
+  const bool b2 = kFilt && bs != 0u;
+  if (kFilt && b2) turn_c0_pair_bound(s, low, dh, dl, bs, Lh, Ll, Ch, Cl, M);
+  turn_moves_sl(s, dh, dl, Ch, Cl, M, hl0, w, b2, low, flip_always, o);
+}
+
 __device__ __forceinline__ void ply_policy_full(Side& s, int4& st, const Rng& g, uint32_t i, int max_steps,
                                                 bool autoreset, TurnOut& o, int& term, int& trunc,
-                                                uint32_t R[4], bool first) {
+                                                uint32_t R[4], int p, int par) {
   uint32_t r[4];
-  ply_draw_cached(g, s.t, i, R, first, r);
+  ply_draw_wave(g, s.t, i, R, p, par, r);
   int d0, d1;
   dice_from(r[0], g.dice_mode, d0, d1);
   const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
-  const uint32_t bs = turn_block_set(s.O, s.S1o, s.P, block_lowmask(s.P), dh, dl);
+  const uint32_t low = block_lowmask(s.P);
+  const uint32_t bs = turn_block_set_sl(s.O, s.S1o, s.P, low, dh, dl);
   uint32_t w[4];
   turn_words(r, w);
   const uint32_t mover_black = s.black;
-  if (__ballot(bs != 0u) == 0ull) turn_free(s, dh, dl, w, o);
-  else if (__ballot(bs != 0u && dh == dl) == 0ull) turn_free<true>(s, dh, dl, w, o, bs);
-  else coop_turn_full<false, true>(s, d0, d1, false, ~0ull, w, o, (int)(threadIdx.x & 63), bs);
-  ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, autoreset, term, trunc);
+  if (__ballot(bs != 0u && dh == dl) == 0ull) {
+    if (__ballot(bs != 0u) == 0ull) ply_free_turn<false>(s, dh, dl, low, bs, w, autoreset, o);
+    else ply_free_turn<true>(s, dh, dl, low, bs, w, autoreset, o);
+  } else {
+    coop_turn_full<false, true>(s, d0, d1, false, ~0ull, w, o, (int)(threadIdx.x & 63), bs);
+    // (coop_turn_full flips only a live game; ply_close_sl resets a finished one)
+  }
+  if (autoreset) ply_close_sl(s, st, o.term, o.reward, mover_black, r[3], max_steps, term, trunc);
+  else ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, false, term, trunc);
 }
 
 // one FULL4 ply (a whole turn per step), the turn
@@ -166,7 +206,7 @@ __device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t i,
                                     bool autoreset, TurnOut& o, int& term, int& trunc, uint32_t R[4],
                                     bool first) {
   if (!play && !dice) {  // kernel arguments: a wave-uniform branch
-    ply_policy_full(s, st, g, i, max_steps, autoreset, o, term, trunc, R, first);
+    ply_policy_full(s, st, g, i, max_steps, autoreset, o, term, trunc, R, 0, 0);
     return;
   }
   uint32_t r[4];
@@ -275,10 +315,11 @@ __global__ void __launch_bounds__(kBlock, 1) k_rollout_wave(Planes pl, int n, Rn
   Side s = valid ? side_from_record(pl.p0[i], pl.p1[i]) : side_start(0u);
   int4 st = make_int4(0, 0, 0, 0);
   uint32_t R[4];  // the Philox block of the current ply pair
+  const int par = wave_parity(valid, s.t);
   for (int p = 0; p < plies; ++p) {
     TurnOut o;
     int term, trunc;
-    ply_policy_full(s, st, g, (uint32_t)i, max_steps, true, o, term, trunc, R, p == 0);
+    ply_policy_full(s, st, g, (uint32_t)i, max_steps, true, o, term, trunc, R, p, par);
     if (kOut && valid) store_outs(out, (size_t)p * n + i, s, o, term, trunc, nullptr, false);
   }
   int4 cum = make_int4(0, 0, 0, 0);
@@ -541,7 +582,7 @@ __global__ void __launch_bounds__(kFxThreads) k_rollout_full(Planes pl, int n, R
         dice_from(r[0], g.dice_mode, d0, d1);
         dh = d0 > d1 ? d0 : d1;
         dl = d0 > d1 ? d1 : d0;
-        bs = turn_block_set(s.O, s.S1o, s.P, block_lowmask(s.P), dh, dl);
+        bs = turn_block_set_sl(s.O, s.S1o, s.P, block_lowmask(s.P), dh, dl);
       }
       const bool pk = act && bs != 0u;
       if (pk) {  // block-bound: park the env with the helper
@@ -558,9 +599,9 @@ __global__ void __launch_bounds__(kFxThreads) k_rollout_full(Planes pl, int n, R
         turn_words(r, w);
         const uint32_t mover_black = s.black;
         TurnOut o;
-        turn_free(s, dh, dl, w, o);
+        turn_free_sl(s, dh, dl, w, true, o);
         int term, trunc;
-        ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, true, term, trunc);
+        ply_close_sl(s, st, o.term, o.reward, mover_black, r[3], max_steps, term, trunc);
         if (kOut) {
           if (out.obs) fx_obs_own(out.obs, (size_t)p * n + i, s, lane & 1);
           fx_put(RG, lane, p, s, o, term, trunc);
@@ -874,7 +915,12 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
     ply_words(rv.x, rv.y, g.dice_mode, r);
     StepOut o;
     int term, trunc;
-    env_ply(s, st, r, false, 0, 0, g.dice_mode, true, 0, 0, max_steps, true, o, term, trunc);
+    // short launches: the straight-line ply (0.1605 -> 0.1592 ms per 100
+    // plies of 20-ply launches); long ones keep env_ply, whose instruction
+    // stream the sustained rate is tuned to (0.1259 against 0.1344 with the
+    // straight-line ply, tools/diag/gpu_ab_sl.sh, one box)
+    if constexpr (kNt) env_ply_policy_sl(s, st, r, g.dice_mode, max_steps, o, term, trunc);
+    else env_ply(s, st, r, false, 0, 0, g.dice_mode, true, 0, 0, max_steps, true, o, term, trunc);
     if (kOut) pc_put(L, b % kPcSlots, k, le, s, o, term, trunc);
   };
   if (!producer) draw_block(0);

@@ -464,10 +464,11 @@ int narde_observe(narde_env* e, int32_t* obs, float* tes, void* stream) {
     if (const int rc = check_launch("k_observe")) return rc;
   }
   if (tes) {
-    const int64_t quads = (e->n * 198 + 3) / 4;
-    k_tesauro198<<<(unsigned)((quads + kBlock - 1) / kBlock), kBlock, 0, (hipStream_t)stream>>>(e->pl, (int)e->n,
-                                                                                              tes);
-    return check_launch("k_tesauro198");
+    // kTesEnvs envs per wave, kBlock / 64 waves per workgroup
+    const int64_t per_block = (int64_t)kTesEnvs * (kBlock / 64);
+    k_tesauro198_rows<<<(unsigned)((e->n + per_block - 1) / per_block), kBlock, 0, (hipStream_t)stream>>>(
+        e->pl, (int)e->n, tes);
+    return check_launch("k_tesauro198_rows");
   }
   return NARDE_OK;
 }

@@ -1335,6 +1335,334 @@ NARDE_FN void env_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, con
   if (!o.term) side_flip(s);
 }
 
+// ================================================ FULL4, straight-line forms
+// The device plays a ply in lockstep waves of 64 envs, one wave per SIMD.
+// There a branch whose condition differs between lanes costs its VALU ->
+// SALU turnaround (~30 cycles) plus ~3 scalar issue slots, whether or not a
+// lane skips its body (tools/diag/issue_probe.hip: 59 cycles per divergent
+// if-region around 2 VALU, 45 per ballot branch; one VALU ~4.6 cycles), and
+// in a wave that holds both kinds of turn every side runs anyway.  So the
+// block-free turn below computes every side and selects -- no branch but the
+// loop of the block filter, which only block-bound two-dice lanes take.
+// Same results as env_turn_full (tests/hostcheck: hc_turn_sl_random,
+// hc_selfplay_full_sl; the GPU parity tests).
+
+// all ones iff c (selects written as masks: the compiler turns a select
+// between two computed values into a branch when one side is costly)
+NARDE_FN uint32_t msk(bool c) { return 0u - (uint32_t)c; }
+
+// die_candidates with the bear-off condition as a mask (no select the
+// compiler may turn into a branch)
+NARDE_FN uint32_t die_candidates_sl(uint32_t O, uint32_t P, int d) {
+  const uint32_t normal = O & ~(P << d) & (MASK24 << d) & MASK24;
+  const uint32_t home = 0u - (uint32_t)((O >> 6) == 0u);  // all ones iff every own checker is home
+  return normal | (O & ((1u << d) - 1u) & home);
+}
+
+// apply_move when `en`, else nothing (every update masked)
+NARDE_FN void apply_move_if(Side& s, int f, int t, bool en) {
+  const bool off = t == OFF;
+  const int tq = off ? 0 : t;
+  const uint32_t cf = nib_get(s.own, f);
+  const bool land = en && !off;
+  const uint32_t bf = en ? (1u << f) : 0u;
+  const uint32_t bt = land ? (1u << tq) : 0u;
+  const uint32_t vf = en ? (0xFFFFFFFFu << (4 * (f & 7))) : 0u;
+  const uint32_t vt = (land ? 1u : 0u) << (4 * (tq & 7));
+  const int kf = f >> 3, kt = tq >> 3;
+  s.own.w[0] += (kf == 0 ? vf : 0u) + (kt == 0 ? vt : 0u);
+  s.own.w[1] += (kf == 1 ? vf : 0u) + (kt == 1 ? vt : 0u);
+  s.own.w[2] += (kf == 2 ? vf : 0u) + (kt == 2 ? vt : 0u);
+  const uint32_t t01 = bt & (~s.O | s.S1o);
+  s.O = (s.O & (cf == 1u ? ~bf : ~0u)) | bt;
+  s.S1o ^= (cf - 1u < 2u ? bf : 0u) ^ t01;
+  s.off_own += (en && off) ? 1u : 0u;
+  s.ft_own = en ? 0u : s.ft_own;
+}
+
+// f4_keep_pair_bf with the home test as masks
+NARDE_FN uint32_t f4_keep_pair_bf_sl(uint32_t O, uint32_t S1, uint32_t P, int a, int b, uint32_t L) {
+  const uint32_t G = ~(P << b) & (MASK24 << b) & MASK24;
+  const uint32_t X = O & G;
+  const uint32_t e1 = (nz1(X, S1) & ~HEAD) | (((X & ~HEAD) != 0u) ? HEAD : 0u);
+  const uint32_t e2 = (G << a) & MASK24;
+  const uint32_t LB = (1u << b) - 1u;
+  const uint32_t out = O & ~0x3Fu;
+  const bool lone = (out & (out - 1u)) == 0u && (out & S1) != 0u &&
+                    (int)__builtin_ctz(out | 0x80000000u) - a < 6;
+  const uint32_t homep = (out == 0u ? MASK24 : 0u) | (lone ? out : 0u);
+  const uint32_t e3 = homep & (nz1(O & LB, S1) | ((LB << a) & MASK24));
+  return L & (e1 | e2 | e3);
+}
+
+NARDE_FN bool f4_bearoff_fixed_sl(const Side& s, int rem) {
+  uint32_t x = s.own.w[0] & 0xFFFFFFu;  // points 0..5
+  x = (x & 0x0F0F0Fu) + ((x >> 4) & 0x0F0F0Fu);
+  const uint32_t home = ((x * 0x010101u) >> 16) & 0xFFu;
+  return ((s.O >> 6) == 0u) | ((int)(15u - s.off_own - home) >= rem);
+}
+
+// f4_open_moves without its early returns
+NARDE_FN int f4_open_moves_sl(const Side& s, int d, int hl, int T) {
+  const uint32_t O = s.O, fr = ~s.P & MASK24;
+  const uint32_t r0 = (1u << d) - 1u;
+  const uint32_t r1 = ((r0 & fr) << d) & MASK24;
+  const uint32_t r2 = ((r1 & fr) << d) & MASK24;
+  const uint32_t r3 = ((r2 & fr) << d) & MASK24;
+  const uint32_t R = (r0 | r1 | r2 | r3) & O;
+  const uint32_t h1 = ((0x3Fu & fr) << d) & MASK24;
+  const uint32_t h2 = ((h1 & fr) << d) & MASK24;
+  const uint32_t h3 = ((h2 & fr) << d) & MASK24;
+  const uint32_t X = O & ~0x3Fu;
+  const int head = (int)nib_get(s.own, 23);
+  const bool reach = (X & ~(h1 | h2 | h3)) == 0u && !((X & HEAD) && head > hl);
+  uint32_t ge4;
+  const uint32_t ge3 = nib_ge3_ge4(s.own, ge4);
+  const uint32_t Rb = R & ~HEAD;
+  const int B = __builtin_popcount(Rb) + __builtin_popcount(Rb & ~s.S1o) + __builtin_popcount(Rb & ge3) +
+                __builtin_popcount(Rb & ge4) + ((R & HEAD) ? head : 0);
+  const int t = T + (reach ? B : 0);
+  return t < 4 ? t : 4;
+}
+
+// C_0 and M of a block-free turn, from the masks (env_turn_full's bf
+// branches): two dice from the pair checks (f4_keep_pair_bf), doubles from
+// the exact counts (f4_exact_moves, f4_open_moves).  Lh / Ll: the root
+// candidates; hl0: the turn's head allowance.
+NARDE_FN void turn_c0_free(const Side& s, int dh, int dl, uint32_t& Lh, uint32_t& Ll, uint32_t& Ch, uint32_t& Cl,
+                           int& M, int& hl0) {
+  const bool dbl = dh == dl;
+  Lh = die_candidates_sl(s.O, s.P, dh);
+  Ll = die_candidates_sl(s.O, s.P, dl) & msk(!dbl);
+  const uint32_t kh = f4_keep_pair_bf_sl(s.O, s.S1o, s.P, dh, dl, Lh);
+  const uint32_t kl = f4_keep_pair_bf_sl(s.O, s.S1o, s.P, dl, dh, Ll);
+  hl0 = (dbl && s.ft_own && (dh == 3 || dh == 4 || dh == 6)) ? 2 : 1;
+  const int T0 = f4_exact_moves(s, dh, hl0);
+  const int Mo = f4_open_moves_sl(s, dh, hl0, T0);
+  const int Mx = f4_bearoff_fixed_sl(s, 4) ? T0 : Mo;
+  const bool pair = (kh | kl) != 0u;
+  const bool two = !dbl && pair;  // two dice, both playable in some order
+  Ch = (kh & msk(two)) | (Lh & msk(!two));
+  Cl = (kl & msk(two)) | (Ll & msk(!dbl && !pair && Lh == 0u));
+  const int M2 = two ? 2 : ((Lh | Ll) != 0u ? 1 : 0);
+  M = dbl ? (Lh != 0u ? Mx : 0) : M2;
+}
+
+// C_0 and M of a block-bound TWO-dice turn (env_turn_full's !bf two-dice
+// branch); hs = turn_block_set's holes.  Overwrites the outputs.
+NARDE_FN void turn_c0_pair_bound(const Side& s, uint32_t low, int dh, int dl, uint32_t hs, uint32_t& Lh,
+                                 uint32_t& Ll, uint32_t& Ch, uint32_t& Cl, int& M) {
+  const Blocks bl = block_info_low(s.O, low);
+  Lh = die_filter(s.O, s.S1o, bl, die_candidates(s.O, s.P, dh), dh);
+  Ll = die_filter(s.O, s.S1o, bl, die_candidates(s.O, s.P, dl), dl);
+  const uint32_t sh = f4_sure_pair(s.O, s.P, dl, Lh, hs), sl = f4_sure_pair(s.O, s.P, dh, Ll, hs);
+  const uint32_t kh = sh | f4_keep_pair(s, low, dh, dl, Lh & ~sh, false);
+  const uint32_t kl = sl | f4_keep_pair(s, low, dl, dh, Ll & ~sl, false);
+  const bool pair = (kh | kl) != 0u;
+  Ch = pair ? kh : Lh;
+  Cl = pair ? kl : (Lh ? 0u : Ll);
+  M = pair ? 2 : ((Lh | Ll) ? 1 : 0);
+}
+
+// the mover change as selects (no branch): when `flip`
+NARDE_FN void side_flip_if(Side& s, bool flip) {
+  Side f = s;
+  side_flip(f);
+  s.own.w[0] = flip ? f.own.w[0] : s.own.w[0];
+  s.own.w[1] = flip ? f.own.w[1] : s.own.w[1];
+  s.own.w[2] = flip ? f.own.w[2] : s.own.w[2];
+  s.opp.w[0] = flip ? f.opp.w[0] : s.opp.w[0];
+  s.opp.w[1] = flip ? f.opp.w[1] : s.opp.w[1];
+  s.opp.w[2] = flip ? f.opp.w[2] : s.opp.w[2];
+  s.O = flip ? f.O : s.O;
+  s.P = flip ? f.P : s.P;
+  s.S1o = flip ? f.S1o : s.S1o;
+  s.S1p = flip ? f.S1p : s.S1p;
+  s.off_own = flip ? f.off_own : s.off_own;
+  s.off_opp = flip ? f.off_opp : s.off_opp;
+  s.ft_own = flip ? f.ft_own : s.ft_own;
+  s.ft_opp = flip ? f.ft_opp : s.ft_opp;
+  s.black = flip ? f.black : s.black;
+}
+
+// The sub-moves of a turn whose C_0 = (Ch, Cl) and M are known, straight-
+// line (all three later sub-moves computed, applied where k < M), the
+// random-legal policy (w).  filt: the lane's lists are block-filtered (a
+// block-bound two-dice turn; its only later sub-move is k = 1) -- the one
+// loop (die_filter's), run only by such lanes.  Then _check_game_ended and
+// the flip (every lane when flip_always: callers that auto-reset a finished
+// env in the same ply).
+NARDE_FN void turn_moves_sl(Side& s, int dh, int dl, uint32_t Ch, uint32_t Cl, int M, int hl, const uint32_t w[4],
+                            bool filt, uint32_t low, bool flip_always, TurnOut& o) {
+  const bool dbl = dh == dl;
+  o.legal = (uint64_t)Ch | ((uint64_t)Cl << 24) | ((uint64_t)dh << 48) | ((uint64_t)dl << 52) |
+            ((uint64_t)M << 56);
+  const int nh = __builtin_popcount(Ch), n = nh + __builtin_popcount(Cl);
+  const int idx = (int)mulhi_u32(w[0], (uint32_t)n);
+  const bool hi = idx < nh;
+  const int d0 = hi ? dh : dl;
+  const int p0 = select_bit(hi ? Ch : Cl, hi ? idx : idx - nh);
+  const bool go = M >= 1;
+  apply_move_if(s, p0, p0 - d0 < 0 ? OFF : p0 - d0, go);
+  // the played word as two 32-bit halves (sub-moves 0-1, 2-3)
+  uint32_t pl0 = go ? (0xFFFF0000u | ((uint32_t)d0 << 8) | (uint32_t)p0) : 0xFFFFFFFFu, pl1 = 0xFFFFFFFFu;
+  hl -= (go && p0 == 23) ? 1 : 0;
+  const int d1 = dbl ? dh : (d0 == dh ? dl : dh);
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    const int dk = k == 1 ? d1 : dh;
+    const bool act = k < M;
+    uint32_t Lk = die_candidates_sl(s.O, s.P, dk);
+    if (k == 1 && filt && act) Lk = die_filter(s.O, s.S1o, block_info_low(s.O, low), Lk, dk);
+    Lk &= hl <= 0 ? ~HEAD : ~0u;
+    const uint32_t wk = k == 1 ? w[1] : (k == 2 ? w[2] : w[3]);
+    const int p = select_bit(Lk, (int)mulhi_u32(wk, (uint32_t)__builtin_popcount(Lk)));
+    apply_move_if(s, p, p - dk < 0 ? OFF : p - dk, act);
+    const uint32_t v = ((uint32_t)dk << 8) | (uint32_t)p;
+    if (k == 1) pl0 = act ? ((pl0 & 0xFFFFu) | (v << 16)) : pl0;
+    if (k == 2) pl1 = act ? ((pl1 & 0xFFFF0000u) | v) : pl1;
+    if (k == 3) pl1 = act ? ((pl1 & 0xFFFFu) | (v << 16)) : pl1;
+    hl -= (act && p == 23) ? 1 : 0;
+  }
+  o.played = (uint64_t)pl0 | ((uint64_t)pl1 << 32);
+  o.max_dice = M;
+  o.term = s.off_own == 15u;
+  o.reward = o.term ? (s.off_opp > 0u ? 1 : 2) : 0;
+  if (flip_always) side_flip(s);
+  else side_flip_if(s, !o.term);
+}
+
+// The block-free turn, straight-line (env_turn_full when turn_block_set is 0).
+NARDE_FN void turn_free_sl(Side& s, int dh, int dl, const uint32_t w[4], bool flip_always, TurnOut& o) {
+  uint32_t Lh, Ll, Ch, Cl;
+  int M, hl0;
+  turn_c0_free(s, dh, dl, Lh, Ll, Ch, Cl, M, hl0);
+  turn_moves_sl(s, dh, dl, Ch, Cl, M, hl0, w, false, 0u, flip_always, o);
+}
+
+// ============================================== REF2, straight-line forms
+// NardeEnv.step with the random-legal policy (env_step, policy = true) for
+// the device's lockstep waves: the same arithmetic with every branch whose
+// condition differs between lanes turned into masks, and the three block
+// filters' loops merged into two (the root's two dice in one loop).  Equal
+// to env_step (tests/hostcheck hc_selfplay_sl).
+
+// die_filter of two dice on one board, one loop over both dice's risky
+// single-checker sources
+NARDE_FN void die_filter2(uint32_t O, uint32_t S1, const Blocks& bl, uint32_t Ca, int a, uint32_t Cb, int b,
+                          uint32_t& La, uint32_t& Lb) {
+  const uint32_t hitA = bl.F ? MASK24 : (bl.Q << a);
+  const uint32_t hitB = bl.F ? MASK24 : (bl.Q << b);
+  La = Ca & ~(hitA & ~S1);
+  Lb = Cb & ~(hitB & ~S1);
+  uint32_t ma = Ca & hitA & S1, mb = Cb & hitB & S1;
+  while (ma | mb) {
+    const bool fa = ma != 0u;
+    const uint32_t m = fa ? ma : mb;
+    const int d = fa ? a : b;
+    const int p = __builtin_ctz(m);
+    const uint32_t bp = 1u << p;
+    ma &= fa ? ~bp : ~0u;
+    mb &= fa ? ~0u : ~bp;
+    const uint32_t Op = (O & ~bp) | (p >= d ? (1u << (p - d)) : 0u);
+    const uint32_t rej = (runs6(Op) & bl.low) ? bp : 0u;
+    La &= fa ? ~rej : ~0u;
+    Lb &= fa ? ~0u : ~rej;
+  }
+}
+
+// legal2_low (the step's list #1), straight-line but for the filter loop
+NARDE_FN void legal2_low_sl(const Side& s, int d0, int d1, uint32_t low, Legal& l) {
+  const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
+  const bool dbl = dh == dl;
+  const Blocks bl = block_info_low(s.O, low);
+  uint32_t Lh, Ll;
+  die_filter2(s.O, s.S1o, bl, die_candidates_sl(s.O, s.P, dh), dh,
+              die_candidates_sl(s.O, s.P, dl) & msk(!dbl), dl, Lh, Ll);
+  Ll = dbl ? Lh : Ll;
+  const bool two_heads = s.ft_own && dbl && (dh == 3 || dh == 4 || dh == 6);
+  Ll &= ((Lh >> 23) != 0u && !two_heads) ? ~HEAD : ~0u;
+  l.n = 2;
+  l.d[0] = dh; l.d[1] = dl; l.d[2] = 0; l.d[3] = 0;
+  l.L[0] = Lh; l.L[1] = Ll; l.L[2] = 0u; l.L[3] = 0u;
+  l.count = __builtin_popcount(Lh) + __builtin_popcount(Ll);
+}
+
+// env_step(s, d0, d1, -, -, policy = true, r1, r2, o, flip_always = true)
+NARDE_FN void env_step_policy_sl(Side& s, int d0, int d1, uint32_t r1, uint32_t r2, StepOut& o) {
+  const uint32_t low = block_lowmask(s.P);
+  legal2_low_sl(s, d0, d1, low, o.l1);
+  const int n1 = o.l1.count;
+  int f1, t1;
+  legal2_entry(o.l1, (int)mulhi_u32(r1, (uint32_t)n1), f1, t1);
+  const int code1 = n1 >= 2 ? encode_move(f1, t1) : 0;
+  // the 'off' quirk: a drawn normal move (f, 0), f <= 5, decodes to (f, 'off')
+  const bool quirk = n1 >= 2 && t1 == 0 && f1 <= 5;
+  const uint32_t bf1 = 1u << f1;
+  const bool listed_off = (((o.l1.L[0] & bf1) != 0u) & (f1 < o.l1.d[0])) | (((o.l1.L[1] & bf1) != 0u) & (f1 < o.l1.d[1]));
+  t1 = quirk ? OFF : t1;
+  const bool play1 = quirk ? listed_off : n1 >= 1;
+  apply_move_if(s, f1, t1, play1);
+  // the second list (narde_env.py:63-89): one die, the post-move board
+  const bool has2 = n1 >= 2 && play1;
+  const int dist = t1 == OFF ? f1 + 1 : f1 - t1;
+  const int rem = (d0 == dist) ? d1 : ((d1 == dist) ? d0 : d1);
+  const Blocks bl = block_info_low(s.O, low);
+  uint32_t L2, unused;
+  die_filter2(s.O, s.S1o, bl, die_candidates_sl(s.O, s.P, rem) & msk(has2), rem, 0u, 1, L2, unused);
+  const int c2 = __builtin_popcount(L2);
+  const int f2 = select_bit(L2, (int)mulhi_u32(r2, (uint32_t)c2));
+  const int t2 = f2 - rem < 0 ? OFF : f2 - rem;
+  const bool play2 = c2 > 0 && !(t2 == 0 && f2 <= 5);
+  apply_move_if(s, f2, t2, play2);
+  o.L2 = L2;
+  o.d2 = has2 ? rem : 0;
+  o.count2 = has2 ? c2 : -1;
+  o.code1 = code1;
+  o.code2 = c2 > 0 ? encode_move(f2, t2) : 0;
+  o.term = s.off_own == 15u;
+  o.reward = o.term ? (s.off_opp > 0u ? 1 : 2) : 0;
+  side_flip(s);
+}
+
+// turn_block_set without its early exit and with both kinds' per-window
+// tests computed (a wave holds both kinds of turn)
+NARDE_FN uint32_t turn_block_set_sl(uint32_t O, uint32_t S1, uint32_t P, uint32_t low, int dh, int dl) {
+  const bool dbl = dh == dl;
+  const uint32_t A = O | land_step(O, P, dh) | land_step(O, P, dl);
+  uint32_t U = A | land_step(A, P, dh) | land_step(A, P, dl);
+  const uint32_t V = land_step(U, P, dh);
+  U |= dbl ? (V | land_step(V, P, dh)) : 0u;
+  uint32_t win = runs6(U) & low & windows_few_holes(O, dbl ? 4 : 2), out = 0u;
+  bool full = false;
+  while (win) {
+    const int i = __builtin_ctz(win);
+    win &= win - 1u;
+    const uint32_t W = 0x3Fu << i;
+    const uint32_t H = W & ~O;
+    full = full || H == 0u;
+    const uint32_t src = O & ~(W & S1);
+    uint32_t T = src, seen = 0u;
+    int cost = 0;
+#pragma unroll
+    for (int j = 1; j <= 4; ++j) {
+      T = land_step(T, P, dh);
+      const uint32_t nw = H & T & ~seen;
+      cost += j * __builtin_popcount(nw);
+      seen |= nw;
+    }
+    const bool dfail = seen == H && cost <= 4;
+    const uint32_t Lh = land_step(src, P, dh), Ll = land_step(src, P, dl);
+    const uint32_t h1 = H & (0u - H), h2 = H ^ h1;
+    // (bitwise: && / || would branch)
+    const bool one = (H & (Lh | Ll | land_step(Lh, P, dl) | land_step(Ll, P, dh))) != 0u;
+    const bool two = (((h1 & Lh) != 0u) & ((h2 & Ll) != 0u)) | (((h1 & Ll) != 0u) & ((h2 & Lh) != 0u));
+    const bool tfail = h2 == 0u ? one : two;
+    out |= (W & msk(dbl & dfail)) | (H & msk(!dbl & tfail));
+  }
+  return full ? ~0u : out;
+}
+
 // obs = get_perspective_board(current_player) (narde.py:31-34): int32[24]
 NARDE_FN int obs_point(const Side& s, int p) { return (int)nib_get(s.own, p) - (int)nib_get(s.opp, p); }
 
@@ -1431,6 +1759,36 @@ NARDE_FN void ply_close(Side& s, int4& st, int o_term, int o_reward, uint32_t mo
   s.t += 1u;
 }
 
+// ply_close with auto-reset as selects (the reset state is mostly constants)
+NARDE_FN void ply_close_sl(Side& s, int4& st, int o_term, int o_reward, uint32_t mover_black, uint32_t r3,
+                           int max_steps, int& term, int& trunc) {
+  s.elapsed += 1u;
+  term = o_term;
+  trunc = max_steps > 0 && s.elapsed >= (uint32_t)max_steps;
+  const bool end = (term | trunc) != 0;
+  st.x += end ? 1 : 0;
+  st.y += (term && !mover_black) ? o_reward : 0;
+  st.z += (term && mover_black) ? o_reward : 0;
+  const Side r = side_reset(r3);
+  s.own.w[0] = end ? r.own.w[0] : s.own.w[0];
+  s.own.w[1] = end ? r.own.w[1] : s.own.w[1];
+  s.own.w[2] = end ? r.own.w[2] : s.own.w[2];
+  s.opp.w[0] = end ? r.opp.w[0] : s.opp.w[0];
+  s.opp.w[1] = end ? r.opp.w[1] : s.opp.w[1];
+  s.opp.w[2] = end ? r.opp.w[2] : s.opp.w[2];
+  s.O = end ? r.O : s.O;
+  s.P = end ? r.P : s.P;
+  s.S1o = end ? r.S1o : s.S1o;
+  s.S1p = end ? r.S1p : s.S1p;
+  s.off_own = end ? r.off_own : s.off_own;
+  s.off_opp = end ? r.off_opp : s.off_opp;
+  s.ft_own = end ? r.ft_own : s.ft_own;
+  s.ft_opp = end ? r.ft_opp : s.ft_opp;
+  s.black = end ? r.black : s.black;
+  s.elapsed = end ? 0u : s.elapsed;
+  s.t += 1u;
+}
+
 // the four pick words of a FULL4 turn (see env_ply_full_with)
 NARDE_FN void turn_words(const uint32_t r[4], uint32_t w[4]) {
   w[0] = r[1];
@@ -1456,6 +1814,17 @@ NARDE_FN void env_ply(Side& s, int4& st, const uint32_t r[4], bool have_dice, in
   const uint32_t mover_black = s.black;
   env_step(s, d0, d1, c1, c2, policy, r[1], r[2], o, autoreset, bad);
   ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, autoreset, term, trunc);
+}
+
+// env_ply with device dice, the random-legal policy and auto-reset,
+// straight-line (env_step_policy_sl, ply_close_sl): the rollouts' ply
+NARDE_FN void env_ply_policy_sl(Side& s, int4& st, const uint32_t r[4], int dice_mode, int max_steps, StepOut& o,
+                                int& term, int& trunc) {
+  int d0, d1;
+  dice_from(r[0], dice_mode, d0, d1);
+  const uint32_t mover_black = s.black;
+  env_step_policy_sl(s, d0, d1, r[1], r[2], o);
+  ply_close_sl(s, st, o.term, o.reward, mover_black, r[3], max_steps, term, trunc);
 }
 
 // One FULL4 ply: env_ply with a whole turn per step.  Pick words w = {r1,

@@ -240,7 +240,218 @@ void hc_selfplay_full(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int p
   }
 }
 
+// hc_selfplay through the rollouts' straight-line REF2 ply (env_ply_policy_sl)
+void hc_selfplay_sl(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int plies, int dice_mode,
+                    int max_steps, int8_t* board, uint8_t* off, uint8_t* ft, int8_t* player,
+                    uint16_t* elapsed, int32_t* stats, int8_t* obs, int8_t* reward, uint8_t* term,
+                    uint8_t* trunc, uint8_t* dice_out, int16_t* action_out, int16_t* count1_out) {
+  for (int64_t i = 0; i < n; ++i) {
+    Side s = load(board + i * 24, off + 2 * i, ft + 2 * i, player[i], elapsed[i]);
+    int4 st = make_int4(0, 0, 0, 0);
+    for (int p = 0; p < plies; ++p) {
+      uint32_t r[4];
+      ply_draw(seed, t0 + (uint32_t)p, (uint32_t)(env0 + i), dice_mode, r);
+      int d0, d1;
+      dice_from(r[0], dice_mode, d0, d1);
+      StepOut o;
+      int tm, tr;
+      env_ply_policy_sl(s, st, r, dice_mode, max_steps, o, tm, tr);
+      const int64_t ix = (int64_t)p * n + i;
+      if (obs)
+        for (int q = 0; q < 24; ++q) obs[ix * 24 + q] = (int8_t)obs_point(s, q);
+      if (reward) reward[ix] = (int8_t)o.reward;
+      if (term) term[ix] = (uint8_t)tm;
+      if (trunc) trunc[ix] = (uint8_t)tr;
+      if (dice_out) { dice_out[2 * ix] = (uint8_t)d0; dice_out[2 * ix + 1] = (uint8_t)d1; }
+      if (action_out) { action_out[2 * ix] = (int16_t)o.code1; action_out[2 * ix + 1] = (int16_t)o.code2; }
+      if (count1_out) count1_out[ix] = (int16_t)o.l1.count;
+    }
+    stats[3 * i] += st.x;
+    stats[3 * i + 1] += st.y;
+    stats[3 * i + 2] += st.z;
+    store(s, board + i * 24, off + 2 * i, ft + 2 * i, player + i, elapsed + i);
+  }
+}
+
+// ---- the device's straight-line FULL4 turn (round 4) ----------------------
+// kernels_rollout.h ply_policy_full per lane: turn_block_set_sl; a lane whose
+// turn is not a block-bound double takes the straight-line forms
+// (turn_c0_free, turn_c0_pair_bound for a block-bound two-dice turn,
+// turn_moves_sl), a block-bound double the general turn (on the device the
+// cooperative one, equal to env_turn_full).  flip_always as on the device's
+// auto-resetting rollouts.
+static void turn_device_sl(Side& s, int d0, int d1, const uint32_t w[4], bool flip_always, TurnOut& o) {
+  const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
+  const uint32_t low = block_lowmask(s.P);
+  const uint32_t bs = turn_block_set_sl(s.O, s.S1o, s.P, low, dh, dl);
+  if (bs != 0u && dh == dl) {
+    env_turn_full(s, d0, d1, false, 0ull, w, o);
+    if (flip_always && o.term) side_flip(s);
+    return;
+  }
+  uint32_t Lh, Ll, Ch, Cl;
+  int M, hl0;
+  turn_c0_free(s, dh, dl, Lh, Ll, Ch, Cl, M, hl0);
+  if (bs != 0u) turn_c0_pair_bound(s, low, dh, dl, bs, Lh, Ll, Ch, Cl, M);
+  turn_moves_sl(s, dh, dl, Ch, Cl, M, hl0, w, bs != 0u, low, flip_always, o);
+}
+
+// hc_full4_batch through turn_device_sl
+void hc_full4_batch_sl(int64_t n, int8_t* board, uint8_t* off, uint8_t* ft, const int8_t* player,
+                       const uint8_t* dice, const uint32_t* words, uint64_t* legal, uint64_t* played,
+                       int8_t* reward, uint8_t* done) {
+  for (int64_t i = 0; i < n; ++i) {
+    Side s = load(board + i * 24, off + 2 * i, ft + 2 * i, player[i], 0);
+    TurnOut o;
+    turn_device_sl(s, dice[2 * i], dice[2 * i + 1], words + 4 * i, false, o);
+    if (!o.term) side_flip(s);
+    legal[i] = o.legal;
+    played[i] = o.played;
+    reward[i] = (int8_t)o.reward;
+    done[i] = (uint8_t)o.term;
+    store(s, board + i * 24, off + 2 * i, ft + 2 * i, nullptr, nullptr);
+  }
+}
+
+// hc_selfplay_full through the device's rollout ply: turn_device_sl with
+// flip_always, then ply_close_sl (auto-reset as selects)
+void hc_selfplay_full_sl(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int plies, int dice_mode,
+                         int max_steps, int8_t* board, uint8_t* off, uint8_t* ft, int8_t* player,
+                         uint16_t* elapsed, int32_t* stats, int8_t* obs, int8_t* reward, uint8_t* term,
+                         uint8_t* trunc, uint64_t* legal_out, uint64_t* played_out) {
+  for (int64_t i = 0; i < n; ++i) {
+    Side s = load(board + i * 24, off + 2 * i, ft + 2 * i, player[i], elapsed[i]);
+    s.t = t0;
+    int4 st = make_int4(0, 0, 0, 0);
+    for (int p = 0; p < plies; ++p) {
+      uint32_t r[4];
+      ply_draw(seed, s.t, (uint32_t)(env0 + i), dice_mode, r);
+      int d0, d1;
+      dice_from(r[0], dice_mode, d0, d1);
+      uint32_t w[4];
+      turn_words(r, w);
+      const uint32_t mover_black = s.black;
+      TurnOut o;
+      turn_device_sl(s, d0, d1, w, true, o);
+      int tm, tr;
+      ply_close_sl(s, st, o.term, o.reward, mover_black, r[3], max_steps, tm, tr);
+      const int64_t ix = (int64_t)p * n + i;
+      if (obs)
+        for (int q = 0; q < 24; ++q) obs[ix * 24 + q] = (int8_t)obs_point(s, q);
+      if (reward) reward[ix] = (int8_t)o.reward;
+      if (term) term[ix] = (uint8_t)tm;
+      if (trunc) trunc[ix] = (uint8_t)tr;
+      if (legal_out) legal_out[ix] = o.legal;
+      if (played_out) played_out[ix] = o.played;
+    }
+    stats[3 * i] += st.x;
+    stats[3 * i + 1] += st.y;
+    stats[3 * i + 2] += st.z;
+    store(s, board + i * 24, off + 2 * i, ft + 2 * i, player + i, elapsed + i);
+  }
+}
+
 }  // extern "C"
+
+// env_step_policy_sl against env_step (policy = true, flip_always) on n
+// random positions (hc_block_set_sl_random's boards: run-heavy, head-heavy,
+// endgames), random dice and words.  Returns mismatches of the state, list
+// #1, list #2, codes, reward or end flag; *bound = lists the block rule cut.
+extern "C" int64_t hc_step_sl_random(int64_t n, uint32_t seed, int64_t* bound) {
+  uint64_t x = 0x9E3779B97F4A7C15ull ^ ((uint64_t)seed << 17);
+  auto rnd = [&x](uint32_t m) {
+    x ^= x >> 12; x ^= x << 25; x ^= x >> 27;
+    return (uint32_t)(((x * 0x2545F4914F6CDD1Dull) >> 32) % m);
+  };
+  int64_t bad = 0, nb = 0;
+  for (int64_t done = 0; done < n; ++done) {
+    Side s = side_start(0u);
+    for (int k = 0; k < 3; ++k) { s.own.w[k] = 0u; s.opp.w[k] = 0u; }
+    const uint32_t mode = rnd(4);
+    const int offc = mode == 3 ? (int)rnd(14) : 0;
+    int left = 15 - offc;
+    uint32_t used = 0u;
+    while (left > 0) {
+      int p = mode >= 2 ? (int)rnd(mode == 3 ? 6 : 12) : (int)rnd(24);
+      if (mode == 1 && rnd(3) == 0) p = 23;
+      const int c = 1 + (int)rnd(left < 3 ? left : 3);
+      for (int j = 0; j < c; ++j) nib_inc(s.own, p);
+      used |= 1u << p;
+      left -= c;
+    }
+    for (int lo = 15 - (int)rnd(3); lo > 0;) {
+      const int p = (int)rnd(24);
+      if ((used >> p) & 1u) continue;
+      nib_inc(s.opp, p);
+      --lo;
+    }
+    s.off_own = (uint32_t)offc;
+    s.ft_own = rnd(4) == 0;
+    side_masks(s);
+    const int d0 = 1 + (int)rnd(6), d1 = rnd(4) == 0 ? d0 : 1 + (int)rnd(6);
+    const uint32_t r1 = (uint32_t)(x >> 7), r2 = (uint32_t)(x >> 29) * 2654435761u;
+    Side a = s, b = s;
+    StepOut oa, ob;
+    env_step(a, d0, d1, 0, 0, true, r1, r2, oa, true);
+    env_step_policy_sl(b, d0, d1, r1, r2, ob);
+    uint4 ra0, ra1, rb0, rb1;
+    side_to_record(a, ra0, ra1);
+    side_to_record(b, rb0, rb1);
+    const bool same = ra0.x == rb0.x && ra0.y == rb0.y && ra0.z == rb0.z && ra0.w == rb0.w && ra1.x == rb1.x &&
+                      ra1.y == rb1.y && ra1.z == rb1.z && a.O == b.O && a.P == b.P && a.S1o == b.S1o &&
+                      a.S1p == b.S1p && oa.l1.L[0] == ob.l1.L[0] && oa.l1.L[1] == ob.l1.L[1] &&
+                      oa.l1.count == ob.l1.count && oa.L2 == ob.L2 && oa.d2 == ob.d2 && oa.count2 == ob.count2 &&
+                      oa.code1 == ob.code1 && oa.code2 == ob.code2 && oa.reward == ob.reward && oa.term == ob.term;
+    bad += !same;
+    Legal l;
+    legal2(s, d0, d1, l);
+    nb += (uint32_t)__builtin_popcount(die_candidates(s.O, s.P, d0 > d1 ? d0 : d1)) != (uint32_t)__builtin_popcount(l.L[0]);
+  }
+  *bound = nb;
+  return bad;
+}
+
+// turn_block_set_sl (no early exit, both kinds' window tests) against
+// turn_block_set on n random positions (hc_pair_bf_random's boards, both
+// kinds of roll).  Returns mismatches; *bound = block-bound cases.
+extern "C" int64_t hc_block_set_sl_random(int64_t n, uint32_t seed, int64_t* bound) {
+  uint64_t x = 0x2545F4914F6CDD1Dull ^ seed;
+  auto rnd = [&x](uint32_t m) {
+    x ^= x >> 12; x ^= x << 25; x ^= x >> 27;
+    return (uint32_t)(((x * 0x2545F4914F6CDD1Dull) >> 32) % m);
+  };
+  int64_t bad = 0, nb = 0;
+  for (int64_t done = 0; done < n; ++done) {
+    Side s = side_start(0u);
+    for (int k = 0; k < 3; ++k) { s.own.w[k] = 0u; s.opp.w[k] = 0u; }
+    const uint32_t mode = rnd(4);
+    int left = 15 - (mode == 3 ? (int)rnd(14) : 0);
+    uint32_t used = 0u;
+    while (left > 0) {
+      int p = mode >= 2 ? (int)rnd(12) : (int)rnd(24);
+      if (mode == 1 && rnd(3) == 0) p = 23;
+      const int c = 1 + (int)rnd(left < 3 ? left : 3);
+      for (int j = 0; j < c; ++j) nib_inc(s.own, p);
+      used |= 1u << p;
+      left -= c;
+    }
+    for (int lo = 15; lo > 0;) {
+      const int p = (int)rnd(24);
+      if ((used >> p) & 1u) continue;
+      nib_inc(s.opp, p);
+      --lo;
+    }
+    side_masks(s);
+    const int a = 1 + (int)rnd(6), b = rnd(3) == 0 ? a : 1 + (int)rnd(6);
+    const int dh = a > b ? a : b, dl = a > b ? b : a;
+    const uint32_t low = block_lowmask(s.P);
+    const uint32_t ref = turn_block_set(s.O, s.S1o, s.P, low, dh, dl);
+    bad += ref != turn_block_set_sl(s.O, s.S1o, s.P, low, dh, dl);
+    nb += ref != 0u;
+  }
+  *bound = nb;
+  return bad;
+}
 
 // f4_keep_pair_bf (all sources from the masks) against f4_keep_pair (the
 // per-source child check) on n random block-free two-dice positions, both

@@ -265,3 +265,82 @@ def test_hostcheck_sure_pair_is_sound(hostcheck):
     su, tot = ctypes.c_int64(0), ctypes.c_int64(0)
     assert f(ctypes.c_int64(100000 // SAN_DIV), ctypes.c_uint32(3), ctypes.byref(su), ctypes.byref(tot)) == 0
     assert su.value > tot.value // 4  # it settles a real share of the sources
+
+
+# ---- round 4: the device's straight-line turn (narde_rules.h turn_c0_free,
+# turn_c0_pair_bound, turn_moves_sl, turn_block_set_sl, ply_close_sl), host
+# mirror hc_full4_batch_sl / hc_selfplay_full_sl (tests/hostcheck)
+
+def test_hostcheck_full4_golden_straight_line(hostcheck):
+    d = golden("full4.npz")
+    n = len(d["dice"])
+    b, off, ft = d["board"].copy(), d["off"].copy(), d["ft"].copy()
+    legal = np.empty(n, np.uint64)
+    played = np.empty(n, np.uint64)
+    rw = np.empty(n, np.int8)
+    dn = np.empty(n, np.uint8)
+    hostcheck.hc_full4_batch_sl(ctypes.c_int64(n), P(b), P(off), P(ft), P(d["player"]), P(d["dice"]),
+                                P(np.ascontiguousarray(d["words"])), P(legal), P(played), P(rw), P(dn))
+    assert np.array_equal(legal, compact_c0(d))
+    assert np.array_equal(played, played_u64(d["played"]))
+    assert np.array_equal(b, d["board_after"])
+    assert np.array_equal(off, d["off_after"]) and np.array_equal(ft, d["ft_after"])
+    assert np.array_equal(rw, d["reward"]) and np.array_equal(dn, d["done"])
+
+
+def test_hostcheck_full4_random_positions_straight_line(hostcheck):
+    """The straight-line turn on run-heavy / bear-off positions equals the
+    oracle's exhaustive composition (block-bound two-dice turns included)."""
+    from fuzz_positions import random_positions
+
+    n = 6000
+    b, off, ft, pl, rng = random_positions(n, 404)
+    d0 = rng.integers(1, 7, n)
+    d1 = np.where(rng.random(n) < 0.3, d0, rng.integers(1, 7, n))
+    dice = np.stack([d0, d1], 1).astype(np.uint8)
+    words = rng.integers(0, 2 ** 32, (n, 4), dtype=np.uint64).astype(np.uint32)
+    ro = O.full4_turn(b, off, ft, pl, dice, words)
+    legal = np.empty(n, np.uint64)
+    played = np.empty(n, np.uint64)
+    rw = np.empty(n, np.int8)
+    dn = np.empty(n, np.uint8)
+    b2, off2, ft2 = b.copy(), off.copy(), ft.copy()
+    hostcheck.hc_full4_batch_sl(ctypes.c_int64(n), P(b2), P(off2), P(ft2), P(pl), P(dice), P(words),
+                                P(legal), P(played), P(rw), P(dn))
+    assert np.array_equal(legal, compact_c0({"dice": dice, "cmask": ro["cmask"], "max_dice": ro["max_dice"]}))
+    assert np.array_equal(played, played_u64(ro["played"]))
+    assert np.array_equal(b2, ro["board"]) and np.array_equal(off2, ro["off"])
+
+
+@pytest.mark.parametrize("dice_mode", [0, 1])
+def test_hostcheck_selfplay_full_straight_line_vs_oracle(hostcheck, dice_mode):
+    n, plies, seed, env0 = 384, 300, 0x5EED0F12, 91
+    sp = O.SelfPlay(n, seed=seed, env0=env0, dice_mode=dice_mode, max_steps=100)
+    sp.reset(0)
+    ro = sp.run_full(plies)
+    b = np.zeros((n, 24), np.int8)
+    off = np.zeros((n, 2), np.uint8)
+    ft = np.zeros((n, 2), np.uint8)
+    pl = np.zeros(n, np.int8)
+    el = np.zeros(n, np.uint16)
+    st = np.zeros((n, 3), np.int32)
+    hostcheck.hc_reset_batch(ctypes.c_int64(n), ctypes.c_int64(env0), ctypes.c_uint64(seed),
+                             ctypes.c_uint32(0), P(b), P(off), P(ft), P(pl), P(el))
+    out = {k: np.empty_like(v) for k, v in ro.items() if k != "dice"}
+    hostcheck.hc_selfplay_full_sl(ctypes.c_int64(n), ctypes.c_int64(env0), ctypes.c_uint64(seed),
+                                  ctypes.c_uint32(0), ctypes.c_int(plies), ctypes.c_int(dice_mode),
+                                  ctypes.c_int(100), P(b), P(off), P(ft), P(pl), P(el), P(st),
+                                  P(out["obs"]), P(out["reward"]), P(out["terminated"]),
+                                  P(out["truncated"]), P(out["legal"]), P(out["played"]))
+    for k in out:
+        assert np.array_equal(out[k], ro[k]), k
+    assert np.array_equal(st, sp.stats) and np.array_equal(b, sp.board)
+    assert ro["truncated"].any() and ro["terminated"].any()
+
+
+def test_hostcheck_block_set_straight_line(hostcheck):
+    f = hostcheck.hc_block_set_sl_random
+    f.restype = ctypes.c_int64
+    nb = ctypes.c_int64(0)
+    assert f(ctypes.c_int64(400000 // SAN_DIV), ctypes.c_uint32(11), ctypes.byref(nb)) == 0
+    assert nb.value > 1000 // SAN_DIV

@@ -336,14 +336,26 @@ def test_mask576_matches_reference_acceptance():
             assert bit == accepted, (i, c)
 
 
-def test_tesauro198_vs_oracle():
-    n = 4096
+@pytest.mark.parametrize("n", [4096, 4099, 17, 65536])
+def test_tesauro198_vs_oracle(n):
+    """k_tesauro198_rows (16 envs a wave, rows staged in LDS): every row of a
+    ragged batch (a partial last wave, an odd row count ending inside a 16-B
+    piece) equals the oracle's; the int32[24] observation (k_observe, whole
+    waves through LDS) equals the perspective board."""
     env = vec(n, seed=3)
     env.selfplay(120)
     st = env.get_state()
     t = np_(env.tesauro198())
     ref = O.tesauro198(np_(st["board"]), np_(st["off"]), np_(st["player"]))
     assert np.array_equal(t, ref)  # exact: every value is k/2 or k/15 computed once in f32
+    # a fresh buffer full of NaN: nothing past the last row is written, nothing is left unwritten
+    out = torch.full((n + 3, 198), float("nan"), device="cuda")
+    env.tesauro198(out=out[:n])
+    assert np.array_equal(np_(out[:n]), ref) and torch.isnan(out[n:]).all()
+    obs = np_(env.observe()).astype(np.int64)
+    board = np_(st["board"]).astype(np.int64)
+    persp = np.where((np_(st["player"]) == 1)[:, None], board, -np.roll(board, 12, axis=1))
+    assert np.array_equal(obs, persp)
 
 
 def test_reset_mask_and_opening_law():

@@ -151,10 +151,14 @@ def test_hostcheck_step_golden(hostcheck):
         assert np.array_equal(a, s[ref]), ref
 
 
+@pytest.mark.parametrize("fn,max_steps", [("hc_selfplay", 1000), ("hc_selfplay_sl", 1000), ("hc_selfplay_sl", 130)])
 @pytest.mark.parametrize("dice_mode", [0, 1])
-def test_hostcheck_selfplay_vs_oracle(hostcheck, dice_mode):
+def test_hostcheck_selfplay_vs_oracle(hostcheck, dice_mode, fn, max_steps):
+    """The host build of the device's REF2 ply -- env_ply, and the rollouts'
+    straight-line env_ply_policy_sl (round 4) -- equals the oracle's
+    self-play on every per-ply output."""
     n, plies, seed, env0 = 512, 400, 0xDEADBEEF12345, 1000
-    sp = O.SelfPlay(n, seed=seed, env0=env0, dice_mode=dice_mode, max_steps=1000)
+    sp = O.SelfPlay(n, seed=seed, env0=env0, dice_mode=dice_mode, max_steps=max_steps)
     sp.reset(0)
     ro = sp.run(plies)
     b = np.zeros((n, 24), np.int8)
@@ -166,9 +170,9 @@ def test_hostcheck_selfplay_vs_oracle(hostcheck, dice_mode):
     hostcheck.hc_reset_batch(ctypes.c_int64(n), ctypes.c_int64(env0), ctypes.c_uint64(seed),
                              ctypes.c_uint32(0), P(b), P(off), P(ft), P(pl), P(el))
     out = {k: np.empty_like(v) for k, v in ro.items()}
-    hostcheck.hc_selfplay(ctypes.c_int64(n), ctypes.c_int64(env0), ctypes.c_uint64(seed),
+    getattr(hostcheck, fn)(ctypes.c_int64(n), ctypes.c_int64(env0), ctypes.c_uint64(seed),
                           ctypes.c_uint32(0), ctypes.c_int(plies), ctypes.c_int(dice_mode),
-                          ctypes.c_int(1000), P(b), P(off), P(ft), P(pl), P(el), P(st),
+                          ctypes.c_int(max_steps), P(b), P(off), P(ft), P(pl), P(el), P(st),
                           P(out["obs"]), P(out["reward"]), P(out["terminated"]), P(out["truncated"]),
                           P(out["dice"]), P(out["action"]), P(out["count1"]))
     for k in ro:
@@ -297,3 +301,14 @@ def test_oracle_replays_trainer_fixture_steps():
     # (float64, train_deepq_pytorch.py:892-912)
     assert (d["shaped"] >= d["reward"]).all()
     assert len(d["blocks"]) == int(d["blocks_len"].sum()) > 0
+
+
+def test_hostcheck_step_policy_straight_line_random(hostcheck):
+    """env_step_policy_sl (the rollouts' straight-line REF2 step) equals
+    env_step with the random-legal policy on random run-heavy, head-heavy
+    and bear-off positions: state, both lists, codes, reward, end."""
+    f = hostcheck.hc_step_sl_random
+    f.restype = ctypes.c_int64
+    nb = ctypes.c_int64(0)
+    assert f(ctypes.c_int64(300000), ctypes.c_uint32(5), ctypes.byref(nb)) == 0
+    assert nb.value > 1000  # the block rule cuts list #1 often enough to matter

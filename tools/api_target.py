@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""The per-call API kernels warm, at B = 65,536:
+k_step<false> (REF2 VecNardeEnv.step), k_step<true> (FULL4 step),
+k_observe's 198-float Tesauro observation and its int32[24] one.  Each runs
+`--warm` untimed then `--reps` timed calls back to back; HIP events around
+each run give microseconds per call, and the same command under
+`rocprofv3 --kernel-trace --stats` gives the per-dispatch durations
+(tools/gpu_round.sh commits that summary).  Prints one JSON line.
+
+Algorithmic bytes per env: k_step 64 (record r+w) +
+114 (REF2 outputs) / 118 (FULL4) B; the observations 32 (record read) +
+792 / 96 B."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gym-narde_amd"))
+
+import torch  # noqa: E402
+
+from gym_narde.vector import VecNardeEnv  # noqa: E402
+
+HBM_PEAK = 8.0e12
+
+
+def timed(fn, warm, reps):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1e3 / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--warm", type=int, default=100)
+    ap.add_argument("--reps", type=int, default=300)
+    a = ap.parse_args()
+    n = a.envs
+    out = {"envs": n, "reps": a.reps}
+    for rules, per_env in (("ref2", 64 + 114), ("full4", 64 + 118)):
+        env = VecNardeEnv(n, device="cuda:0", seed=0, rules=rules)
+        us = timed(env.step, a.warm, a.reps)
+        out[f"k_step_{rules}"] = {"us": round(us, 2), "bytes": n * per_env,
+                                  "frac": round(n * per_env / (us * 1e-6) / HBM_PEAK, 4)}
+        env.close()
+    env = VecNardeEnv(n, device="cuda:0", seed=0)
+    env.selfplay(100)
+    obs198 = torch.empty((n, 198), dtype=torch.float32, device="cuda:0")
+    for kind, per_env, fn in (("tesauro198", 32 + 792, lambda: env.tesauro198(out=obs198)),
+                              ("observe_int24", 32 + 96, env.observe)):
+        us = timed(fn, a.warm, a.reps)
+        out[kind] = {"us": round(us, 2), "bytes": n * per_env,
+                     "frac": round(n * per_env / (us * 1e-6) / HBM_PEAK, 4)}
+    env.close()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
