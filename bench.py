@@ -135,21 +135,21 @@ def cpu_baseline(seconds, cores, how):
 def kernel_name(full4, plies):
     """The kernel narde_rollout[_full] launches for this shape (narde.hip):
     REF2 stores non-temporally up to 32 plies per launch (kPcNtMaxPlies);
-    FULL4 takes k_rollout_full (rule + helper waves) from 48 plies per launch,
-    k_rollout_wave (one wave per 64 envs) below."""
+    FULL4 takes k_rollout_wave (one wave per 64 envs) at every length."""
     if not full4:
         return "k_rollout_pc<true, true>" if plies <= 32 else "k_rollout_pc<true, false>"
-    return "k_rollout_full<true>" if plies >= 48 else "k_rollout_wave<true>"
+    return "k_rollout_wave<true>"
 
 
-def load_traffic(path, envs, plies):
+def load_traffic(path, envs, plies, kernel):
     """HBM bytes per k_rollout launch from the committed rocprofv3 PMC
-    summary (tools/pmc_summary.py), if it was measured at this shape."""
+    summary (tools/pmc_summary.py), if it was measured at this shape on this
+    kernel (its `kernel` filter is a prefix of the launched kernel's name)."""
     try:
         d = json.load(open(path))
     except (OSError, ValueError):
         return None
-    if d.get("envs") != envs or d.get("plies") != plies:
+    if d.get("envs") != envs or d.get("plies") != plies or d.get("kernel", "") not in kernel:
         return None
     return d.get("hbm_bytes_per_launch")
 
@@ -691,7 +691,7 @@ def main():
         base = os.path.join(ROOT, "profiles", "pmc_k_rollout_full" if is_full4 else "pmc_k_rollout")
         traffic = None
         for tj in ([args.traffic_json] if args.traffic_json else [f"{base}_p{P}.json", f"{base}.json"]):
-            traffic = load_traffic(tj, per, P)
+            traffic = load_traffic(tj, per, P, kernel_name(is_full4, P))
             if traffic is not None:
                 break
         # what each rules mode is, and which BASELINE.json config it times

@@ -1,5 +1,6 @@
 // kernels_full4.h -- the FULL4 turn on the device: the wave-cooperative general
-// turn, the block-free turn of the rollout's rule waves, and the list query
+// turn (explicit plays, given dice), the block-bound doubles waves of the
+// rollout (ply_bound_turn: the failing-window search), and the list query
 // (DESIGN.md section 10).
 // Part of the one translation unit narde.hip (included there, in order);
 // not a standalone header.
@@ -169,20 +170,18 @@ __device__ __forceinline__ void turn_play(Side& s, int dh, int dl, uint32_t Ch, 
   if (!o.term) side_flip(s);
 }
 
-// env_turn_full with the per-source checks done cooperatively (see above).
-// kBound: every lane that has a turn is block-bound, with turn_block_set =
-// bs_given (the rollout's helper wave: its rule wave ran the test); the
-// block-free code is compiled out.  kGiven: bs_given is every lane's
-// turn_block_set, computed by the caller (k_rollout_wave).
-template <bool kBound = false, bool kGiven = false>
+// env_turn_full with the per-source checks done cooperatively (see above):
+// the device turn for explicit plays and given dice (k_step<true>) and the
+// FULL4 list query (k_legal_full); the rollouts' policy turn is
+// ply_policy_full's straight-line one (kernels_rollout.h)
 __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, const uint32_t w[4],
-                               TurnOut& o, int lane, uint32_t bs_given = 0u) {
+                               TurnOut& o, int lane) {
   const uint32_t low = block_lowmask(s.P);
   const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
   const bool dbl = dh == dl;
   // one block test for both kinds of turn (turn_block_set)
-  const uint32_t bs = (kBound || kGiven) ? bs_given : turn_block_set(s.O, s.S1o, s.P, low, dh, dl);
-  const bool bf = kBound ? false : bs == 0u;
+  const uint32_t bs = turn_block_set(s.O, s.S1o, s.P, low, dh, dl);
+  const bool bf = bs == 0u;
   const uint32_t hs = dbl ? 0u : bs, ws = dbl ? bs : 0u;
   // first sub-move: the lists, the shortcuts, then every lane's checks at once
   // (both dice's lists from one block-info of the root: legal1 twice would
@@ -265,62 +264,131 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
             });
 }
 
-// The turn of a lane whose turn_block_set is 0 (block-free: no block filter
-// can remove a candidate anywhere in the turn): coop_turn_full with bf = true,
-// which needs no cooperative pass -- two dice take the pair checks from the
-// masks (f4_keep_pair_bf), doubles the exact counts (f4_exact_moves,
-// f4_open_moves) with every C_k = L_k.  No cross-lane operation but the
-// sub-move loop's early exit, so it may run with lanes masked off.  The
-// random-legal policy only (the rollout).
-// kBound2: lanes with bs != 0 (turn_block_set's holes) are block-bound
-// TWO-dice turns (the caller sends waves with a block-bound doubles lane to
-// coop_turn_full): their lists block-filtered, their first moves kept from
-// the sure-move masks (f4_sure_pair) and, for the rest, the per-source pair
-// check (f4_keep_pair: a per-lane loop, usually empty) -- env_turn_full's
-// two-dice branch inline, with no cooperative pass.
-template <bool kBound2 = false>
-__device__ __forceinline__ void turn_free(Side& s, int dh, int dl, const uint32_t w[4], TurnOut& o,
-                                          uint32_t bs = 0u) {
-  const bool dbl = dh == dl;
-  uint32_t Lh = die_candidates(s.O, s.P, dh);
-  uint32_t Ll = dbl ? 0u : die_candidates(s.O, s.P, dl);
-  const int hl0 = (dbl && s.ft_own && (dh == 3 || dh == 4 || dh == 6)) ? 2 : 1;
-  const bool b2 = kBound2 && bs != 0u;
-  const uint32_t low = kBound2 ? block_lowmask(s.P) : 0u;
-  uint32_t Ch, Cl;
-  int M;
-  if (!dbl) {
-    if (b2) {
-      const Blocks bl = block_info_low(s.O, low);
-      Lh = die_filter(s.O, s.S1o, bl, Lh, dh);
-      Ll = die_filter(s.O, s.S1o, bl, Ll, dl);
-      const uint32_t sh = f4_sure_pair(s.O, s.P, dl, Lh, bs), sl = f4_sure_pair(s.O, s.P, dh, Ll, bs);
-      Ch = sh | f4_keep_pair(s, low, dh, dl, Lh & ~sh, false);
-      Cl = sl | f4_keep_pair(s, low, dl, dh, Ll & ~sl, false);
-    } else {
-      Ch = f4_keep_pair_bf(s.O, s.S1o, s.P, dh, dl, Lh);
-      Cl = f4_keep_pair_bf(s.O, s.S1o, s.P, dl, dh, Ll);
+// ---------------------------------------------------------------------------
+// Round 4: waves with a block-bound doubles lane.  Every lane's turn goes
+// the straight-line way (turn_c0_free, turn_c0_pair_bound_w), and only the
+// block-bound doubles lanes that f4_safe_bound does not settle search --
+// cooperatively, over lists filtered by the turn's failing windows
+// (block_reject_w, f4_depth_w: no block_info / die_filter loop at the nodes).
+// Same result as coop_turn_full (the host check: env_turn_full against
+// f4_depth_w, hc_dbl_bound_w_random).
+
+// coop_run's depth mode over the failing-window lists: for each owner lane
+// (m0 != 0) in turn, every lane takes one source of its m0 (lanes 0-23) and
+// searches f4_depth_w<need> below it; out[j] (owner lane) = the sources
+// with depth >= j + 1 after them
+__device__ void coop_depth_w(const Side& s, uint32_t fw, int d, int hl, uint32_t m0, int need, int lane,
+                             uint32_t out[3]) {
+  out[0] = out[1] = out[2] = 0u;
+  uint64_t owners = __ballot(m0 != 0u);
+  while (owners) {
+    const int ow = (int)__builtin_ctzll(owners);
+    owners &= owners - 1ull;
+    Side c;
+    c.own.w[0] = rl(s.own.w[0], ow); c.own.w[1] = rl(s.own.w[1], ow); c.own.w[2] = rl(s.own.w[2], ow);
+    c.O = rl(s.O, ow); c.S1o = rl(s.S1o, ow); c.P = rl(s.P, ow);
+    c.off_own = rl(s.off_own, ow);
+    c.opp.w[0] = c.opp.w[1] = c.opp.w[2] = 0u;
+    c.S1p = 0u; c.off_opp = 0u; c.ft_own = 0u; c.ft_opp = 0u; c.black = 0u; c.elapsed = 0u; c.t = 0u;
+    const uint32_t ofw = rl(fw, ow), om = rl(m0, ow);
+    const int od = (int)rl((uint32_t)d, ow), ohl = (int)rl((uint32_t)hl, ow), oneed = (int)rl((uint32_t)need, ow);
+    const bool has = lane < 24 && ((om >> lane) & 1u);
+    bool k0 = false, k1 = false, k2 = false;
+    if (has) {
+      Side cc = c;
+      apply_die(cc, lane, od);
+      const int hl2 = ohl - (lane == 23 ? 1 : 0);
+      const int dep = oneed == 1 ? f4_depth_w<1>(cc, ofw, od, hl2)
+                                 : (oneed == 2 ? f4_depth_w<2>(cc, ofw, od, hl2) : f4_depth_w<3>(cc, ofw, od, hl2));
+      k0 = dep >= 1; k1 = dep >= 2; k2 = dep >= 3;
     }
-    if (Ch | Cl) {
-      M = 2;
-    } else {
-      M = (Lh | Ll) ? 1 : 0;
-      Ch = Lh;
-      Cl = Lh ? 0u : Ll;
-    }
-  } else {
-    const int T0 = f4_exact_moves(s, dh, hl0);
-    const int Mx = !f4_bearoff_fixed(s) ? f4_open_moves(s, dh, hl0, T0) : T0;
-    Ch = Lh;
-    Cl = 0u;
-    M = Lh ? Mx : 0;
+    const uint32_t r0 = (uint32_t)__ballot(k0), r1 = (uint32_t)__ballot(k1), r2 = (uint32_t)__ballot(k2);
+    out[0] = lane == ow ? r0 : out[0];
+    out[1] = lane == ow ? r1 : out[1];
+    out[2] = lane == ow ? r2 : out[2];
   }
-  turn_play(s, dh, dl, Ch, Cl, M, hl0, false, ~0ull, w, o,
-            [&](int k, int dk, int need, bool act, int hl, uint32_t Lk) -> uint32_t {
-              (void)k; (void)need;
-              if (kBound2 && b2 && act) Lk = die_filter(s.O, s.S1o, block_info_low(s.O, low), Lk, dk);
-              return hl <= 0 ? (Lk & ~HEAD) : Lk;
-            });
+}
+
+// The turn of every lane of a wave holding a block-bound doubles lane (bs,
+// fw: turn_block_set_sl): C_0 / M from the masks (turn_c0_free);
+// block-bound two-dice lanes from the failing windows
+// (turn_c0_pair_bound_w); block-bound doubles lanes: the filtered root
+// list, M = 4 with every C_k = L_k when the moves that can never be
+// rejected give >= 4 (f4_safe_bound), else the cooperative search; then the
+// sub-moves, the bound lanes' lists filtered (block_reject_w) and the
+// searching lanes' checks (coop_depth_w).  The rare blocks sit behind
+// wave-uniform ballots.  Every lane must call it.  (Round 3's
+// coop_turn_full here, per-lane branches and the die_filter search: 20-ply
+// launches 0.454 -> 0.437 ms per 100 plies.)
+__device__ __forceinline__ void ply_bound_turn(Side& s, int dh, int dl, uint32_t bs, uint32_t fw, const uint32_t w[4],
+                                         bool flip_always, TurnOut& o, int lane) {
+  uint32_t Lh, Ll, Ch, Cl;
+  int M, hl0;
+  turn_c0_free(s, dh, dl, Lh, Ll, Ch, Cl, M, hl0);
+  const bool dbl = dh == dl;
+  const bool b2 = bs != 0u && !dbl, bd = bs != 0u && dbl;
+  if (__ballot(b2) != 0ull) {
+    if (b2) turn_c0_pair_bound_w(s, dh, dl, bs, fw, Lh, Ll, Ch, Cl, M);
+  }
+  bool srch = false;
+  if (__ballot(bd) != 0ull) {
+    // block-bound doubles: the filtered root list; M = 4 with every C_k =
+    // L_k when the never-rejected moves give >= 4; else the search
+    const uint32_t Lb = Lh & ~block_reject_w(s.O, s.S1o, bd ? fw : 0u, Lh, dh);
+    const bool fast = bd && f4_safe_bound(s, dh, hl0, bs) >= 4;
+    srch = bd && !fast && Lb != 0u;
+    uint32_t r0[3];
+    coop_depth_w(s, fw, dh, hl0, srch ? Lb : 0u, 3, lane, r0);
+    const int Ms = r0[2] ? 4 : (r0[1] ? 3 : (r0[0] ? 2 : 1));
+    const uint32_t Cs = r0[2] ? r0[2] : (r0[1] ? r0[1] : (r0[0] ? r0[0] : Lb));
+    Ch = bd ? (fast ? Lb : (Lb ? Cs : 0u)) : Ch;
+    M = bd ? (fast ? 4 : (Lb ? Ms : 0)) : M;
+  }
+  o.legal = (uint64_t)Ch | ((uint64_t)Cl << 24) | ((uint64_t)dh << 48) | ((uint64_t)dl << 52) |
+            ((uint64_t)M << 56);
+  const int nh = __builtin_popcount(Ch), n = nh + __builtin_popcount(Cl);
+  const int idx = (int)mulhi_u32(w[0], (uint32_t)n);
+  const bool hi = idx < nh;
+  const int d0 = hi ? dh : dl;
+  const int p0 = select_bit(hi ? Ch : Cl, hi ? idx : idx - nh);
+  const bool go = M >= 1;
+  apply_move_if(s, p0, p0 - d0 < 0 ? OFF : p0 - d0, go);
+  uint32_t pl0 = go ? (0xFFFF0000u | ((uint32_t)d0 << 8) | (uint32_t)p0) : 0xFFFFFFFFu, pl1 = 0xFFFFFFFFu;
+  int hl = hl0 - ((go && p0 == 23) ? 1 : 0);
+  const int d1 = dbl ? dh : (d0 == dh ? dl : dh);
+  const bool anyb = __ballot(bs != 0u) != 0ull;  // wave-uniform
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    const int dk = k == 1 ? d1 : dh;
+    const bool act = k < M;
+    uint32_t Lk = die_candidates_sl(s.O, s.P, dk);
+    if (anyb) {
+      const bool filt = bd || (k == 1 && b2);
+      Lk &= ~block_reject_w(s.O, s.S1o, filt ? fw : 0u, Lk, dk);
+    }
+    Lk &= hl <= 0 ? ~HEAD : ~0u;
+    const int need = M - k - 1;
+    const bool chk = srch && act && need > 0;
+    if (__ballot(chk) != 0ull) {  // wave-uniform
+      uint32_t rk[3];
+      coop_depth_w(s, fw, dk, hl, chk ? Lk : 0u, need, lane, rk);
+      Lk = chk ? (need >= 2 ? rk[1] : rk[0]) : Lk;
+    }
+    const uint32_t wk = k == 1 ? w[1] : (k == 2 ? w[2] : w[3]);
+    const int p = select_bit(Lk, (int)mulhi_u32(wk, (uint32_t)__builtin_popcount(Lk)));
+    apply_move_if(s, p, p - dk < 0 ? OFF : p - dk, act);
+    const uint32_t v = ((uint32_t)dk << 8) | (uint32_t)p;
+    if (k == 1) pl0 = act ? ((pl0 & 0xFFFFu) | (v << 16)) : pl0;
+    if (k == 2) pl1 = act ? ((pl1 & 0xFFFF0000u) | v) : pl1;
+    if (k == 3) pl1 = act ? ((pl1 & 0xFFFFu) | (v << 16)) : pl1;
+    hl -= (act && p == 23) ? 1 : 0;
+  }
+  o.played = (uint64_t)pl0 | ((uint64_t)pl1 << 32);
+  o.max_dice = M;
+  o.term = s.off_own == 15u;
+  o.reward = o.term ? (s.off_opp > 0u ? 1 : 2) : 0;
+  if (flip_always) side_flip(s);
+  else side_flip_if(s, !o.term);
 }
 
 // FULL4 first-sub-move set C_0 and max dice M for the given (or the next

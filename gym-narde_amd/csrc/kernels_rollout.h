@@ -154,24 +154,25 @@ __device__ __forceinline__ int wave_parity(bool valid, uint32_t t) {
 }
 
 // one FULL4 ply of the random-legal policy with device dice (ply p of the
-// launch), the block test first.  A wave with no block-bound doubles lane
-// plays every lane's turn straight-line (narde_rules.h turn_c0_free +
-// turn_moves_sl: no branch whose condition differs between lanes), its
-// block-bound two-dice lanes taking env_turn_full's bound branch for C_0
-// (turn_c0_pair_bound) and block-filtered lists; a wave with a block-bound
-// doubles lane plays the cooperative turn with the test's result.  Every
-// lane of the wave must call it.  (Round 3 -- turn_free / turn_free<true>
-// with per-lane branches: 0.460 ms per 100 plies of 20-ply k_rollout_wave
-// launches)
+// launch): the draw, the block test (turn_block_set_sl: the failing
+// windows), the turn of every lane (ply_free_turn, or kernels_full4.h
+// ply_bound_turn in a wave with a block-bound doubles lane), the end of the
+// ply.  Every lane of the wave must call it.  (Round 3 -- turn_free /
+// turn_free<true> / coop_turn_full by kind of wave, per-lane branches: 0.460
+// ms per 100 plies of 20-ply k_rollout_wave launches)
+// a wave with no block-bound doubles lane: every lane's C_0 / M from the
+// masks (turn_c0_free), the block-bound two-dice lanes' (kFilt: the wave has
+// one) from the failing windows (turn_c0_pair_bound_w), the sub-moves
+// straight-line (turn_moves_sl)
 template <bool kFilt>
-__device__ __forceinline__ void ply_free_turn(Side& s, int dh, int dl, uint32_t low, uint32_t bs, const uint32_t w[4],
+__device__ __forceinline__ void ply_free_turn(Side& s, int dh, int dl, uint32_t bs, uint32_t fw, const uint32_t w[4],
                                               bool flip_always, TurnOut& o) {
   uint32_t Lh, Ll, Ch, Cl;
   int M, hl0;
   turn_c0_free(s, dh, dl, Lh, Ll, Ch, Cl, M, hl0);
   const bool b2 = kFilt && bs != 0u;
-  if (kFilt && b2) turn_c0_pair_bound(s, low, dh, dl, bs, Lh, Ll, Ch, Cl, M);
-  turn_moves_sl(s, dh, dl, Ch, Cl, M, hl0, w, b2, low, flip_always, o);
+  if (kFilt && b2) turn_c0_pair_bound_w(s, dh, dl, bs, fw, Lh, Ll, Ch, Cl, M);
+  turn_moves_sl(s, dh, dl, Ch, Cl, M, hl0, w, b2, fw, flip_always, o);
 }
 
 __device__ __forceinline__ void ply_policy_full(Side& s, int4& st, const Rng& g, uint32_t i, int max_steps,
@@ -183,16 +184,20 @@ __device__ __forceinline__ void ply_policy_full(Side& s, int4& st, const Rng& g,
   dice_from(r[0], g.dice_mode, d0, d1);
   const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
   const uint32_t low = block_lowmask(s.P);
-  const uint32_t bs = turn_block_set_sl(s.O, s.S1o, s.P, low, dh, dl);
+  uint32_t fw;
+  const uint32_t bs = turn_block_set_sl(s.O, s.S1o, s.P, low, dh, dl, fw);
   uint32_t w[4];
   turn_words(r, w);
   const uint32_t mover_black = s.black;
+  // three kinds of wave (one instruction stream each): no block-bound
+  // lane, block-bound two-dice lanes only, a block-bound doubles lane
+  // (one copy of the turn for all three: 0.448 against 0.437 ms per 100
+  // plies of 20-ply launches, tools/diag/gpu_ab_f4.sh)
   if (__ballot(bs != 0u && dh == dl) == 0ull) {
-    if (__ballot(bs != 0u) == 0ull) ply_free_turn<false>(s, dh, dl, low, bs, w, autoreset, o);
-    else ply_free_turn<true>(s, dh, dl, low, bs, w, autoreset, o);
+    if (__ballot(bs != 0u) == 0ull) ply_free_turn<false>(s, dh, dl, bs, fw, w, autoreset, o);
+    else ply_free_turn<true>(s, dh, dl, bs, fw, w, autoreset, o);
   } else {
-    coop_turn_full<false, true>(s, d0, d1, false, ~0ull, w, o, (int)(threadIdx.x & 63), bs);
-    // (coop_turn_full flips only a live game; ply_close_sl resets a finished one)
+    ply_bound_turn(s, dh, dl, bs, fw, w, autoreset, o, (int)(threadIdx.x & 63));
   }
   if (autoreset) ply_close_sl(s, st, o.term, o.reward, mover_black, r[3], max_steps, term, trunc);
   else ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, false, term, trunc);
@@ -300,13 +305,18 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_rollout_wave: the FULL4 rollout for short launches (plies < kFxMinPlies),
-// one wave per 64 envs, every lane's turn played wave-cooperatively
-// (coop_turn_full): `plies` whole turns of random-legal self-play with
-// auto-reset, the record in VGPRs, every ply's outputs stored straight from
-// registers.  k_rollout_full below is faster per ply but its launch lasts
-// until the most-delayed env has played its plies, which a short launch does
-// not amortise.
+// k_rollout_wave: the FULL4 rollout, one wave per 64 envs (ply_policy_full):
+// `plies` whole turns of random-legal self-play with auto-reset, the record
+// in VGPRs, every ply's outputs stored straight from registers (the lanes
+// play in lockstep, so a wave's rows of a ply go out together).  Round 3's
+// k_rollout_full -- rule waves playing the block-free turns and parking
+// block-bound envs with a helper wave on the same SIMD, lanes drifting up
+// to 16 plies apart, the narrow rows through an LDS ring -- was the faster
+// kernel from 48 plies per launch; with the straight-line turn this one is
+// faster at every length (100 plies 0.414 -> 0.353, 1,000 plies 0.349 ->
+// 0.319 ms per 100 plies; stats only 0.375 -> 0.306 / 0.306 -> 0.274;
+// tools/diag/gpu_ab_len.sh, one box) and k_rollout_full is retired
+// (DESIGN.md section 10, Appendix M.10).
 template <bool kOut>
 __global__ void __launch_bounds__(kBlock, 1) k_rollout_wave(Planes pl, int n, Rng g, int plies, int max_steps,
                                                             Outs out) {
@@ -329,344 +339,6 @@ __global__ void __launch_bounds__(kBlock, 1) k_rollout_wave(Planes pl, int n, Rn
     pl.p0[i] = ra;
     pl.p1[i] = rb;
     cum = stats_after(pl.stats, i, st, out.totals != nullptr);
-  }
-  if (out.totals) wg_totals(cum, out.totals);
-}
-
-// ---------------------------------------------------------------------------
-// k_rollout_full: the FULL4 rollout (`plies` whole turns of random-legal
-// self-play per env, auto-reset) as rule waves and helper waves.
-//
-// A FULL4 turn is cheap when it is block-free (turn_block_set == 0: no block
-// filter can bite anywhere in the turn) -- ~99 % of turns -- and costly when
-// it is not: block filters, sure-move tests and the cooperative searches of
-// coop_turn_full, ~3x the instructions of a free turn.  Run in one wave,
-// that general code is paid by every wave holding such a lane: ~37 % of
-// wave-plies for ~0.7 % of lanes (the one-wave kernel spent 0.409 ms per 100
-// plies against 0.289 with every turn forced free).  And one wave per SIMD
-// (B = 65,536 envs = 1,024 waves) issues only every other VALU slot of its
-// SIMD.  So each workgroup holds 256 envs on 4 rule waves and 4 helper
-// waves, one of each per SIMD:
-//   * a rule wave plays the block-free turns of its 64 envs (turn_free: no
-//     cooperative pass, no block filter) and stores their outputs.  A lane
-//     whose turn is block-bound parks its env in its LDS mailbox and posts it
-//     to the helper; the lane sits out until the env comes back, then goes
-//     on from its own ply.  So lanes drift apart; a lane more than
-//     kFxDrift - 1 plies ahead of the wave's slowest lane waits;
-//   * the helper wave sleeps until a park wakes it (s_wakeup), then plays
-//     the posted turns with the general turn, block-free code compiled out
-//     (helper lane l serves rule lane l's mailbox; the wave is converged, as
-//     coop_turn_full needs), stores their outputs and hands the envs back --
-//     in the issue slots its rule wave leaves free.
-// (The helper plays what is posted at once: waiting for 2 or 3 parked envs
-// per pass -- its pass costs about the same for one env as for several --
-// was slower, 0.490 / 0.542 against 0.444 ms per 100 plies at that stage:
-// the parked lanes' latency, not the helper's issue, bounds the wave.)
-// Drift bound, measured (sustained 1,000-ply launches, one box): every ply
-// waiting for the parked envs 0.513 ms per 100 plies (the general turn's
-// latency stalls the wave); with every output stored straight from the
-// lanes, 2 / 4 / 8 / 12 / 16 / unbounded: 0.412 / 0.395 / 0.374 / 0.372 /
-// 0.409 / 0.465 -- past ~12 plies the lanes' narrow rows scattered over more
-// lines than the caches merge.  Staging the whole rows in an LDS ring (obs
-// too, expanded by the helper) kept every store coalesced but cost ~120 VALU
-// + 20 LDS instructions per ply: 0.404.  Round 3 (profiles/r03/full4_ring/):
-// the narrow outputs through a 16-slot ring (FxRing, fx_flush), the obs rows
-// from the lanes' registers, drift 16: 0.3700-0.3711 against 0.3723-0.3725
-// at drift 10 without the ring (drift 13: 0.3704-0.3707), PMC 1.07 x the
-// algorithmic bytes against 1.45 x; every obs row through the ring as well
-// (12 or 8 slots): PMC 1.002 x but 0.400 / 0.408.  Kept: the narrow ring
-// plus each row pair's shared 64-B granule at the flush (fx_obs_own), drift
-// 16: PMC 1.026 x, 0.3743-0.3753 (1.1 % behind the narrow ring alone).
-// The two waves of a pair meet only through per-lane LDS words: rule lane l
-// counts its parks and stores the count to post[l] after filling its
-// mailbox; helper lane l plays the turn when post[l] moves past the count it
-// has answered, and stores that count to back[l] after writing the env back;
-// the rule lane takes the env back when back[l] reaches its count.
-// `fin`: the rule wave has finished.  Every
-// branch around a cross-lane operation is wave-uniform (a ballot or a
-// readfirstlane): a handshake run by one lane inside these loops lets the
-// compiler split the loop per lane, which breaks the cooperative turn.  No
-// workgroup barrier after the start.
-// Every env plays exactly the plies it would in k_step<true> (same draws,
-// same turn), so the outputs equal `plies` launches of narde_step_full.
-constexpr int kFxGroups = 4;                 // rule waves per workgroup (one per SIMD)
-constexpr int kFxEnvs = 64 * kFxGroups;      // envs per workgroup
-constexpr int kFxThreads = 2 * kFxEnvs;      // + one helper wave per rule wave
-constexpr int kFxDrift = 16;                 // lanes stay within kFxDrift plies of the slowest
-// launches shorter than this take k_rollout_wave (sustained, ms per 100
-// plies, k_rollout_wave / k_rollout_full: 20 plies 0.540 / 0.602, 50 plies
-// 0.477 / 0.471, 100 plies 0.447 / 0.420, 200 plies 0.429 / 0.397)
-constexpr int kFxMinPlies = 48;
-
-struct FxLds {  // the mailboxes of one rule/helper pair
-  uint4 m0[64], m1[64], m2[64];  // the parked env's side (mover's view): mail_put
-  uint4 r[64];                   // its ply words (rule -> helper)
-  uint32_t ply[64];              // the rollout ply of the parked turn (its output row)
-  uint32_t bs[64];               // its turn_block_set (rule -> helper)
-  uint32_t ret[64];              // statistics of the turn (helper -> rule): episodes | white << 4 | black << 8
-  uint32_t post[64], back[64];   // park counts: posted by the rule lane, answered by the helper lane
-  uint32_t fin;                  // the rule wave has finished
-};
-
-// The narrow per-ply outputs of one rule/helper pair (the legal word with
-// reward, term and trunc in its top 4 bits, the played word), staged in LDS
-// slot ply & 15 (a lane plays at most kFxDrift - 1 plies past the slowest),
-// with 32 B of each obs row (fx_obs_own).  A lane's turn writes its slot (the
-// rule lane, or the helper lane for a parked turn before it hands the env
-// back); the rule wave stores the whole 64-env rows of a ply once its
-// slowest lane has passed it (fx_flush).  Written straight from each lane,
-// the rows of drifted lanes went out at different times in pieces of 1-8 B,
-// and the L2 wrote each piece back on its own: PMC WRITE_SIZE 1.45 x the
-// algorithmic bytes; 1.07 x with the narrow outputs through the ring; 1.026 x
-// with the obs rows' shared granules too.
-constexpr int kFxSlots = 16;
-static_assert(kFxSlots >= kFxDrift && (kFxSlots & (kFxSlots - 1)) == 0, "ring slots");
-struct FxRing {
-  uint4 lp[kFxSlots][64];    // legal word | reward << 60 | term << 62 | trunc << 63, played word
-  uint2 half[kFxSlots][64];  // the own / opp nibble word of the row's shared 32 B (fx_put)
-};
-
-// Lanes 2j and 2j + 1 hold adjacent 96-B obs rows: 192 B = three 64-B
-// granules, of which the middle one holds 32 B of each row (points 16..23
-// of the even lane's env, points 0..7 of the odd lane's).  A lane stores its
-// own whole granule from its registers at its turn (fx_obs_own) and leaves
-// its share of the middle one in the ring, stored with the pair's other
-// half at the flush.
-__device__ __forceinline__ void fx_obs_own(int32_t* __restrict__ obs, size_t ix, const Side& s, bool odd) {
-  // even: points 0..15 (nibble words 0, 1); odd: points 8..23 (words 1, 2)
-  const uint32_t o0 = odd ? s.own.w[1] : s.own.w[0], o1 = odd ? s.own.w[2] : s.own.w[1];
-  const uint32_t q0 = odd ? s.opp.w[1] : s.opp.w[0], q1 = odd ? s.opp.w[2] : s.opp.w[1];
-  int4* dst = reinterpret_cast<int4*>(obs + ix * 24 + (odd ? 8 : 0));
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const uint32_t ow = (c < 2 ? o0 : o1) >> (16 * (c & 1)), pw = (c < 2 ? q0 : q1) >> (16 * (c & 1));
-    st_out(dst + c, make_int4((int)(ow & 15u) - (int)(pw & 15u), (int)((ow >> 4) & 15u) - (int)((pw >> 4) & 15u),
-                              (int)((ow >> 8) & 15u) - (int)((pw >> 8) & 15u),
-                              (int)((ow >> 12) & 15u) - (int)((pw >> 12) & 15u)));
-  }
-}
-
-__device__ __forceinline__ void fx_put(FxRing& R, int l, int p, const Side& s, const TurnOut& o, int term,
-                                       int trunc) {
-  const int k = p & (kFxSlots - 1);
-  const uint64_t lg = o.legal | ((uint64_t)o.reward << 60) | ((uint64_t)term << 62) | ((uint64_t)trunc << 63);
-  R.lp[k][l] = make_uint4((uint32_t)lg, (uint32_t)(lg >> 32), (uint32_t)o.played, (uint32_t)(o.played >> 32));
-  const bool odd = l & 1;
-  R.half[k][l] = make_uint2(odd ? s.own.w[0] : s.own.w[2], odd ? s.opp.w[0] : s.opp.w[2]);
-}
-
-// the rows of ply q (every valid lane has played it): the narrow outputs as
-// coalesced 64-env stores, and each lane's 32 B of its pair's middle granule
-__device__ __forceinline__ void fx_flush(const FxRing& R, const Outs& out, int l, int q, int n, int i,
-                                         bool valid) {
-  const int k = q & (kFxSlots - 1);
-  const uint4 lp = R.lp[k][l];
-  const uint2 h = R.half[k][l];
-  if (valid) {
-    const size_t ix = (size_t)q * n + i;
-    if (out.obs) {
-      int4* dst = reinterpret_cast<int4*>(out.obs + ix * 24 + ((l & 1) ? 0 : 16));
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const uint32_t ow = h.x >> (16 * c), pw = h.y >> (16 * c);
-        st_out(dst + c, make_int4((int)(ow & 15u) - (int)(pw & 15u), (int)((ow >> 4) & 15u) - (int)((pw >> 4) & 15u),
-                                  (int)((ow >> 8) & 15u) - (int)((pw >> 8) & 15u),
-                                  (int)((ow >> 12) & 15u) - (int)((pw >> 12) & 15u)));
-      }
-    }
-    const uint32_t hi = lp.y;
-    if (out.reward) st_out(out.reward + ix, (int32_t)((hi >> 28) & 3u));
-    if (out.term) st_out(out.term + ix, (uint8_t)((hi >> 30) & 1u));
-    if (out.trunc) st_out(out.trunc + ix, (uint8_t)(hi >> 31));
-    if (out.legal) st_out(out.legal + ix, (uint64_t)lp.x | ((uint64_t)(hi & 0x0FFFFFFFu) << 32));
-    if (out.played) st_out(out.played + ix, (uint64_t)lp.z | ((uint64_t)lp.w << 32));
-  }
-}
-
-__device__ __forceinline__ void mail_put(FxLds& M, int l, const Side& s) {
-  const uint32_t misc = s.off_own | (s.off_opp << 4) | (s.ft_own << 8) | (s.ft_opp << 9) | (s.black << 10) |
-                        (s.elapsed << 16);
-  M.m0[l] = make_uint4(s.own.w[0], s.own.w[1], s.own.w[2], s.opp.w[0]);
-  M.m1[l] = make_uint4(s.opp.w[1], s.opp.w[2], misc, s.t);
-  M.m2[l] = make_uint4(s.O, s.P, s.S1o, s.S1p);
-}
-
-__device__ __forceinline__ Side mail_get(const FxLds& M, int l) {
-  const uint4 a = M.m0[l], b = M.m1[l], c = M.m2[l];
-  Side s;
-  s.own.w[0] = a.x; s.own.w[1] = a.y; s.own.w[2] = a.z;
-  s.opp.w[0] = a.w; s.opp.w[1] = b.x; s.opp.w[2] = b.y;
-  s.off_own = b.z & 15u; s.off_opp = (b.z >> 4) & 15u;
-  s.ft_own = (b.z >> 8) & 1u; s.ft_opp = (b.z >> 9) & 1u;
-  s.black = (b.z >> 10) & 1u; s.elapsed = b.z >> 16;
-  s.t = b.w;
-  s.O = c.x; s.P = c.y; s.S1o = c.z; s.S1p = c.w;
-  return s;
-}
-
-// LDS hand-over words.  The data a word publishes is written by the same
-// lane with plain LDS stores just before it (and LDS executes one wave's
-// operations in order): a compiler-only release fence keeps the stores
-// ahead of the word, without waiting for them.
-__device__ __forceinline__ uint32_t lds_acquire(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_publish(uint32_t* p, uint32_t v) {
-  __atomic_signal_fence(__ATOMIC_RELEASE);
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// s_wakeup: ends the s_sleep of every wave of the workgroup (no builtin)
-__device__ __forceinline__ void wake_workgroup() { asm volatile("s_wakeup" ::: "memory"); }
-
-template <bool kOut>
-__global__ void __launch_bounds__(kFxThreads) k_rollout_full(Planes pl, int n, Rng g, int plies,
-                                                             int max_steps, Outs out) {
-  __shared__ FxLds fx[kFxGroups];
-  __shared__ FxRing fring[kOut ? kFxGroups : 1];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int grp = wave % kFxGroups;
-  FxLds& M = fx[grp];
-  FxRing& RG = fring[kOut ? grp : 0];
-  const int i = blockIdx.x * kFxEnvs + grp * 64 + lane;
-  const bool valid = i < n;
-  int4 cum = make_int4(0, 0, 0, 0);  // the env's statistics after the launch (wg_totals)
-  if (wave < kFxGroups) {
-    M.post[lane] = 0u;
-    M.back[lane] = 0u;
-    M.fin = 0u;  // (every lane of the rule wave stores the same word)
-  }
-  __syncthreads();
-
-  if (wave < kFxGroups) {
-    // ---- rule wave: block-free turns; block-bound ones go to the helper
-    Side s = valid ? side_from_record(pl.p0[i], pl.p1[i]) : side_start(0u);
-    int4 st = make_int4(0, 0, 0, 0);
-    uint32_t R[4];       // the Philox block of the current ply pair
-    bool fresh = true;   // R not drawn yet
-    bool parked = false;
-    uint32_t seq = 0u;   // parks of this lane
-    int p = 0;           // this env's next ply of the launch
-    int lo = 0;          // the slowest lane's next ply (wave-uniform)
-    int fl = 0;          // plies whose narrow rows are stored (wave-uniform)
-    for (;;) {
-      if (__ballot(parked) != 0ull) {  // wave-uniform: take the envs handed back
-        if (parked && lds_acquire(&M.back[lane]) == seq) {
-          // the state after ply p; R still holds the Philox block of ply p's
-          // pair, which also serves ply p + 1 if that one is odd
-          s = mail_get(M, lane);
-          const uint32_t rt = M.ret[lane];
-          st.x += (int)(rt & 15u); st.y += (int)((rt >> 4) & 15u); st.z += (int)((rt >> 8) & 15u);
-          parked = false;
-          ++p;
-        }
-      }
-      while (lo < plies && __ballot(valid && p <= lo) == 0ull) ++lo;
-      // before any turn below reuses a slot: every ply below lo is complete
-      if (kOut)
-        for (; fl < lo; ++fl) fx_flush(RG, out, lane, fl, n, i, valid);
-      const bool act = valid && !parked && p < plies && p < lo + kFxDrift;
-      if (__ballot(act) == 0ull) {
-        if (__ballot(parked) == 0ull) break;  // every ply played
-        // parked lanes hold the wave: wait for the helper
-        wake_workgroup();
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      uint32_t r[4] = {0u, 0u, 0u, 0u};
-      int dh = 1, dl = 1;
-      uint32_t bs = 0u;
-      if (act) {
-        ply_draw_cached(g, s.t, (uint32_t)i, R, fresh, r);
-        fresh = false;
-        int d0, d1;
-        dice_from(r[0], g.dice_mode, d0, d1);
-        dh = d0 > d1 ? d0 : d1;
-        dl = d0 > d1 ? d1 : d0;
-        bs = turn_block_set_sl(s.O, s.S1o, s.P, block_lowmask(s.P), dh, dl);
-      }
-      const bool pk = act && bs != 0u;
-      if (pk) {  // block-bound: park the env with the helper
-        mail_put(M, lane, s);
-        M.r[lane] = make_uint4(r[0], r[1], r[2], r[3]);
-        M.ply[lane] = (uint32_t)p;
-        M.bs[lane] = bs;
-        lds_publish(&M.post[lane], ++seq);
-        parked = true;
-      }
-      if (__ballot(pk) != 0ull) wake_workgroup();  // the helper sleeps
-      if (act && !pk) {
-        uint32_t w[4];
-        turn_words(r, w);
-        const uint32_t mover_black = s.black;
-        TurnOut o;
-        turn_free_sl(s, dh, dl, w, true, o);
-        int term, trunc;
-        ply_close_sl(s, st, o.term, o.reward, mover_black, r[3], max_steps, term, trunc);
-        if (kOut) {
-          if (out.obs) fx_obs_own(out.obs, (size_t)p * n + i, s, lane & 1);
-          fx_put(RG, lane, p, s, o, term, trunc);
-        }
-        ++p;
-      }
-    }
-    lds_publish(&M.fin, 1u);
-    if (valid) {
-      uint4 ra, rb;
-      side_to_record(s, ra, rb);
-      pl.p0[i] = ra;
-      pl.p1[i] = rb;
-      cum = stats_after(pl.stats, i, st, out.totals != nullptr);
-    }
-  } else {
-    // ---- helper wave: the posted (block-bound) turns
-    uint32_t done = 0u;  // parks of rule lane `lane` answered
-    for (;;) {
-      const uint32_t want = lds_acquire(&M.post[lane]);
-      const bool mine = want != done;
-      if (__ballot(mine) != 0ull) {  // wave-uniform
-        Side s;
-        uint32_t r[4] = {0u, 0u, 0u, 0u};
-        int p = 0;
-        uint32_t bs = 0u;
-        if (mine) {
-          s = mail_get(M, lane);
-          const uint4 rr = M.r[lane];
-          r[0] = rr.x; r[1] = rr.y; r[2] = rr.z; r[3] = rr.w;
-          p = (int)M.ply[lane];
-          bs = M.bs[lane];
-        } else {  // an empty board: no candidate, no check, no pass task
-          s.own.w[0] = s.own.w[1] = s.own.w[2] = 0u;
-          s.opp.w[0] = s.opp.w[1] = s.opp.w[2] = 0u;
-          s.O = s.P = s.S1o = s.S1p = 0u;
-          s.off_own = s.off_opp = s.ft_own = s.ft_opp = s.black = s.elapsed = s.t = 0u;
-        }
-        int d0, d1;
-        dice_from(r[0], g.dice_mode, d0, d1);
-        uint32_t w[4];
-        turn_words(r, w);
-        const uint32_t mover_black = s.black;
-        TurnOut o;
-        coop_turn_full<true>(s, d0, d1, false, ~0ull, w, o, lane, bs);  // the whole wave: cooperative passes
-        int4 st = make_int4(0, 0, 0, 0);
-        int term, trunc;
-        ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, true, term, trunc);
-        if (mine) {
-          if (kOut) {
-            if (out.obs) fx_obs_own(out.obs, (size_t)p * n + i, s, lane & 1);
-            fx_put(RG, lane, p, s, o, term, trunc);
-          }
-          mail_put(M, lane, s);
-          M.ret[lane] = (uint32_t)st.x | ((uint32_t)st.y << 4) | ((uint32_t)st.z << 8);
-          done = want;
-          lds_publish(&M.back[lane], want);
-        }
-        continue;
-      }
-      if (__builtin_amdgcn_readfirstlane((int)lds_acquire(&M.fin)) != 0) break;
-      // idle: a long sleep (a poll costs ~30 instructions of its SIMD's issue,
-      // which the rule wave needs); a park's s_wakeup ends it early
-      __builtin_amdgcn_s_sleep(24);
-    }
   }
   if (out.totals) wg_totals(cum, out.totals);
 }

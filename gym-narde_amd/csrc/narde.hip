@@ -335,20 +335,14 @@ int launch_rollout_ref2(narde_env* e, int plies, const Outs& out, bool any, hipS
 }
 
 int launch_rollout_full(narde_env* e, int plies, const Outs& out, bool any, hipStream_t stream) {
-  if (plies < kFxMinPlies) {  // short launches: one wave per 64 envs
-    const dim3 g((unsigned)grid(e->n)), b(kBlock);
-    if (any)
-      k_rollout_wave<true><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
-    else
-      k_rollout_wave<false><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
-  } else {
-    const dim3 g((unsigned)((e->n + kFxEnvs - 1) / kFxEnvs)), b(kFxThreads);
-    if (any)
-      k_rollout_full<true><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
-    else
-      k_rollout_full<false><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
-  }
-  return check_launch("k_rollout<full>");
+  // one wave per 64 envs at every length (round 4: faster than round 3's
+  // rule + helper waves from 100 plies up)
+  const dim3 g((unsigned)grid(e->n)), b(kBlock);
+  if (any)
+    k_rollout_wave<true><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
+  else
+    k_rollout_wave<false><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
+  return check_launch("k_rollout_wave");
 }
 
 }  // namespace

@@ -1448,22 +1448,6 @@ NARDE_FN void turn_c0_free(const Side& s, int dh, int dl, uint32_t& Lh, uint32_t
   M = dbl ? (Lh != 0u ? Mx : 0) : M2;
 }
 
-// C_0 and M of a block-bound TWO-dice turn (env_turn_full's !bf two-dice
-// branch); hs = turn_block_set's holes.  Overwrites the outputs.
-NARDE_FN void turn_c0_pair_bound(const Side& s, uint32_t low, int dh, int dl, uint32_t hs, uint32_t& Lh,
-                                 uint32_t& Ll, uint32_t& Ch, uint32_t& Cl, int& M) {
-  const Blocks bl = block_info_low(s.O, low);
-  Lh = die_filter(s.O, s.S1o, bl, die_candidates(s.O, s.P, dh), dh);
-  Ll = die_filter(s.O, s.S1o, bl, die_candidates(s.O, s.P, dl), dl);
-  const uint32_t sh = f4_sure_pair(s.O, s.P, dl, Lh, hs), sl = f4_sure_pair(s.O, s.P, dh, Ll, hs);
-  const uint32_t kh = sh | f4_keep_pair(s, low, dh, dl, Lh & ~sh, false);
-  const uint32_t kl = sl | f4_keep_pair(s, low, dl, dh, Ll & ~sl, false);
-  const bool pair = (kh | kl) != 0u;
-  Ch = pair ? kh : Lh;
-  Cl = pair ? kl : (Lh ? 0u : Ll);
-  M = pair ? 2 : ((Lh | Ll) ? 1 : 0);
-}
-
 // the mover change as selects (no branch): when `flip`
 NARDE_FN void side_flip_if(Side& s, bool flip) {
   Side f = s;
@@ -1488,12 +1472,13 @@ NARDE_FN void side_flip_if(Side& s, bool flip) {
 // The sub-moves of a turn whose C_0 = (Ch, Cl) and M are known, straight-
 // line (all three later sub-moves computed, applied where k < M), the
 // random-legal policy (w).  filt: the lane's lists are block-filtered (a
-// block-bound two-dice turn; its only later sub-move is k = 1) -- the one
-// loop (die_filter's), run only by such lanes.  Then _check_game_ended and
+// block-bound two-dice turn with failing windows fw; its only later sub-move
+// is k = 1) -- block_reject_w's loop over fw, the only loop.  Then _check_game_ended and
 // the flip (every lane when flip_always: callers that auto-reset a finished
 // env in the same ply).
+NARDE_FN uint32_t block_reject_w(uint32_t O, uint32_t S1, uint32_t fw, uint32_t C, int d);
 NARDE_FN void turn_moves_sl(Side& s, int dh, int dl, uint32_t Ch, uint32_t Cl, int M, int hl, const uint32_t w[4],
-                            bool filt, uint32_t low, bool flip_always, TurnOut& o) {
+                            bool filt, uint32_t fw, bool flip_always, TurnOut& o) {
   const bool dbl = dh == dl;
   o.legal = (uint64_t)Ch | ((uint64_t)Cl << 24) | ((uint64_t)dh << 48) | ((uint64_t)dl << 52) |
             ((uint64_t)M << 56);
@@ -1513,7 +1498,7 @@ NARDE_FN void turn_moves_sl(Side& s, int dh, int dl, uint32_t Ch, uint32_t Cl, i
     const int dk = k == 1 ? d1 : dh;
     const bool act = k < M;
     uint32_t Lk = die_candidates_sl(s.O, s.P, dk);
-    if (k == 1 && filt && act) Lk = die_filter(s.O, s.S1o, block_info_low(s.O, low), Lk, dk);
+    if (k == 1 && filt) Lk &= ~block_reject_w(s.O, s.S1o, fw, Lk, dk);
     Lk &= hl <= 0 ? ~HEAD : ~0u;
     const uint32_t wk = k == 1 ? w[1] : (k == 2 ? w[2] : w[3]);
     const int p = select_bit(Lk, (int)mulhi_u32(wk, (uint32_t)__builtin_popcount(Lk)));
@@ -1625,9 +1610,38 @@ NARDE_FN void env_step_policy_sl(Side& s, int d0, int d1, uint32_t r1, uint32_t 
   side_flip(s);
 }
 
+// f4_depth<N, 0> of a block-bound doubles node with the lists filtered by
+// the turn's failing windows (block_reject_w: a loop over the windows,
+// usually one, instead of block_info_low + die_filter's per-source loop at
+// every node of the search)
+template <int N>
+NARDE_FN int f4_depth_w(const Side& s, uint32_t fw, int d, int hl) {
+  uint32_t L = die_candidates_sl(s.O, s.P, d);
+  L &= ~block_reject_w(s.O, s.S1o, fw, L, d);
+  if (hl <= 0) L &= ~HEAD;
+  if (!L) return 0;
+  if constexpr (N == 1) {
+    return 1;
+  } else {
+    int best = 1;
+    while (L && best < N) {
+      const int p = __builtin_ctz(L);
+      L &= L - 1u;
+      Side c = s;
+      apply_die(c, p, d);
+      const int v = 1 + f4_depth_w<N - 1>(c, fw, d, hl - (p == 23 ? 1 : 0));
+      best = v > best ? v : best;
+    }
+    return best;
+  }
+}
+
 // turn_block_set without its early exit and with both kinds' per-window
 // tests computed (a wave holds both kinds of turn)
-NARDE_FN uint32_t turn_block_set_sl(uint32_t O, uint32_t S1, uint32_t P, uint32_t low, int dh, int dl) {
+// fw (out): the failing windows' start points (bit i = points i..i+5): the
+// only windows that can be full at a node of the turn (block_reject_w)
+NARDE_FN uint32_t turn_block_set_sl(uint32_t O, uint32_t S1, uint32_t P, uint32_t low, int dh, int dl,
+                                    uint32_t& fw) {
   const bool dbl = dh == dl;
   const uint32_t A = O | land_step(O, P, dh) | land_step(O, P, dl);
   uint32_t U = A | land_step(A, P, dh) | land_step(A, P, dl);
@@ -1635,6 +1649,7 @@ NARDE_FN uint32_t turn_block_set_sl(uint32_t O, uint32_t S1, uint32_t P, uint32_
   U |= dbl ? (V | land_step(V, P, dh)) : 0u;
   uint32_t win = runs6(U) & low & windows_few_holes(O, dbl ? 4 : 2), out = 0u;
   bool full = false;
+  fw = 0u;
   while (win) {
     const int i = __builtin_ctz(win);
     win &= win - 1u;
@@ -1659,8 +1674,67 @@ NARDE_FN uint32_t turn_block_set_sl(uint32_t O, uint32_t S1, uint32_t P, uint32_
     const bool two = (((h1 & Lh) != 0u) & ((h2 & Ll) != 0u)) | (((h1 & Ll) != 0u) & ((h2 & Lh) != 0u));
     const bool tfail = h2 == 0u ? one : two;
     out |= (W & msk(dbl & dfail)) | (H & msk(!dbl & tfail));
+    fw |= (H == 0u || (dbl ? dfail : tfail)) ? (1u << i) : 0u;
   }
   return full ? ~0u : out;
+}
+NARDE_FN uint32_t turn_block_set_sl(uint32_t O, uint32_t S1, uint32_t P, uint32_t low, int dh, int dl) {
+  uint32_t fw;
+  return turn_block_set_sl(O, S1, P, low, dh, dl, fw);
+}
+
+// The block filter of one die from a turn's failing windows fw, masks only
+// (die_filter's result at any node of the turn, whose full windows can only
+// be failing ones): a candidate x -> x - d is rejected iff it leaves some
+// failing window W full -- W full already (no hole) and x not a single
+// checker of W, or W's one hole is the landing and x not a single checker of
+// W.  A loop over the failing windows (usually one), no per-source loop.
+NARDE_FN uint32_t block_reject_w(uint32_t O, uint32_t S1, uint32_t fw, uint32_t C, int d) {
+  uint32_t rej = 0u;
+  for (uint32_t f = fw; f; f &= f - 1u) {
+    const uint32_t W = 0x3Fu << __builtin_ctz(f);
+    const uint32_t H = W & ~O;
+    const uint32_t stay = C & ~(W & S1);  // moving it does not open a hole in W
+    const uint32_t one = (H & (H - 1u)) == 0u ? (H << d) : 0u;  // landing on the one hole
+    rej |= H == 0u ? stay : (stay & one & MASK24);
+  }
+  return rej;
+}
+
+// after first move p of die a (a two-dice turn with failing windows fw):
+// does die b still have a move (head rule: not a second head move)?
+NARDE_FN bool pair_child_ok_w(const Side& s, uint32_t fw, int p, int a, int b) {
+  uint32_t O2, S2;
+  child_masks(s, p, a, O2, S2);
+  const uint32_t Cb = die_candidates_sl(O2, s.P, b) & (p == 23 ? ~HEAD : ~0u);
+  return (Cb & ~block_reject_w(O2, S2, fw, Cb, b)) != 0u;
+}
+
+// turn_c0_pair_bound from the failing windows (hs: their holes, fw: their
+// starts; turn_block_set_sl): the lists filtered by block_reject_w, the sure
+// first moves from the masks (f4_sure_pair), the child check for the rest in
+// one loop over both dice's unsure sources (usually none)
+NARDE_FN void turn_c0_pair_bound_w(const Side& s, int dh, int dl, uint32_t hs, uint32_t fw, uint32_t& Lh,
+                                   uint32_t& Ll, uint32_t& Ch, uint32_t& Cl, int& M) {
+  const uint32_t Chc = die_candidates_sl(s.O, s.P, dh), Clc = die_candidates_sl(s.O, s.P, dl);
+  Lh = Chc & ~block_reject_w(s.O, s.S1o, fw, Chc, dh);
+  Ll = Clc & ~block_reject_w(s.O, s.S1o, fw, Clc, dl);
+  uint32_t kh = f4_sure_pair(s.O, s.P, dl, Lh, hs), kl = f4_sure_pair(s.O, s.P, dh, Ll, hs);
+  uint32_t mh = Lh & ~kh, ml = Ll & ~kl;
+  while (mh | ml) {
+    const bool hi = mh != 0u;
+    const int p = __builtin_ctz(hi ? mh : ml);
+    const uint32_t bp = 1u << p;
+    mh &= hi ? ~bp : ~0u;
+    ml &= hi ? ~0u : ~bp;
+    const bool ok = pair_child_ok_w(s, fw, p, hi ? dh : dl, hi ? dl : dh);
+    kh |= (hi && ok) ? bp : 0u;
+    kl |= (!hi && ok) ? bp : 0u;
+  }
+  const bool pair = (kh | kl) != 0u;
+  Ch = pair ? kh : Lh;
+  Cl = pair ? kl : (Lh ? 0u : Ll);
+  M = pair ? 2 : ((Lh | Ll) ? 1 : 0);
 }
 
 // obs = get_perspective_board(current_player) (narde.py:31-34): int32[24]

@@ -283,7 +283,8 @@ void hc_selfplay_sl(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int pli
 static void turn_device_sl(Side& s, int d0, int d1, const uint32_t w[4], bool flip_always, TurnOut& o) {
   const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
   const uint32_t low = block_lowmask(s.P);
-  const uint32_t bs = turn_block_set_sl(s.O, s.S1o, s.P, low, dh, dl);
+  uint32_t fw;
+  const uint32_t bs = turn_block_set_sl(s.O, s.S1o, s.P, low, dh, dl, fw);
   if (bs != 0u && dh == dl) {
     env_turn_full(s, d0, d1, false, 0ull, w, o);
     if (flip_always && o.term) side_flip(s);
@@ -292,8 +293,8 @@ static void turn_device_sl(Side& s, int d0, int d1, const uint32_t w[4], bool fl
   uint32_t Lh, Ll, Ch, Cl;
   int M, hl0;
   turn_c0_free(s, dh, dl, Lh, Ll, Ch, Cl, M, hl0);
-  if (bs != 0u) turn_c0_pair_bound(s, low, dh, dl, bs, Lh, Ll, Ch, Cl, M);
-  turn_moves_sl(s, dh, dl, Ch, Cl, M, hl0, w, bs != 0u, low, flip_always, o);
+  if (bs != 0u) turn_c0_pair_bound_w(s, dh, dl, bs, fw, Lh, Ll, Ch, Cl, M);
+  turn_moves_sl(s, dh, dl, Ch, Cl, M, hl0, w, bs != 0u, fw, flip_always, o);
 }
 
 // hc_full4_batch through turn_device_sl
@@ -408,6 +409,177 @@ extern "C" int64_t hc_step_sl_random(int64_t n, uint32_t seed, int64_t* bound) {
     nb += (uint32_t)__builtin_popcount(die_candidates(s.O, s.P, d0 > d1 ? d0 : d1)) != (uint32_t)__builtin_popcount(l.L[0]);
   }
   *bound = nb;
+  return bad;
+}
+
+// ---- block-bound two-dice turns from the failing windows (round 4) --------
+// the reference: env_turn_full's bound two-dice branch (die_filter lists, the
+// sure-pair masks, f4_keep_pair's child checks)
+static void c0_pair_bound_ref(const Side& s, uint32_t low, int dh, int dl, uint32_t hs, uint32_t& Lh, uint32_t& Ll,
+                              uint32_t& Ch, uint32_t& Cl, int& M) {
+  const Blocks bl = block_info_low(s.O, low);
+  Lh = die_filter(s.O, s.S1o, bl, die_candidates(s.O, s.P, dh), dh);
+  Ll = die_filter(s.O, s.S1o, bl, die_candidates(s.O, s.P, dl), dl);
+  const uint32_t sh = f4_sure_pair(s.O, s.P, dl, Lh, hs), sl = f4_sure_pair(s.O, s.P, dh, Ll, hs);
+  const uint32_t kh = sh | f4_keep_pair(s, low, dh, dl, Lh & ~sh, false);
+  const uint32_t kl = sl | f4_keep_pair(s, low, dl, dh, Ll & ~sl, false);
+  const bool pair = (kh | kl) != 0u;
+  Ch = pair ? kh : Lh;
+  Cl = pair ? kl : (Lh ? 0u : Ll);
+  M = pair ? 2 : ((Lh | Ll) ? 1 : 0);
+}
+
+// On n random block-bound two-dice positions (run-heavy boards, few
+// opponent points below): turn_c0_pair_bound_w equals the reference, and at
+// every child of the turn (each first move of either die) the other die's
+// list filtered by block_reject_w equals die_filter's.  Returns mismatches;
+// *cut = child lists the block rule shortened.
+extern "C" int64_t hc_pair_bound_w_random(int64_t n, uint32_t seed, int64_t* cut) {
+  uint64_t x = 0xA0761D6478BD642Full ^ ((uint64_t)seed << 20);
+  auto rnd = [&x](uint32_t m) {
+    x ^= x >> 12; x ^= x << 25; x ^= x >> 27;
+    return (uint32_t)(((x * 0x2545F4914F6CDD1Dull) >> 32) % m);
+  };
+  int64_t bad = 0, nc = 0;
+  for (int64_t done = 0; done < n;) {
+    Side s = side_start(0u);
+    for (int k = 0; k < 3; ++k) { s.own.w[k] = 0u; s.opp.w[k] = 0u; }
+    // a run of 4-7 own points somewhere, the rest scattered
+    const int r0 = (int)rnd(18), rl = 4 + (int)rnd(4);
+    int left = 15;
+    uint32_t used = 0u;
+    for (int p = r0; p < r0 + rl && p < 24 && left > 0; ++p) {
+      const int c = 1 + (int)rnd(left < 3 ? left : 3);
+      for (int j = 0; j < c; ++j) nib_inc(s.own, p);
+      used |= 1u << p;
+      left -= c;
+    }
+    while (left > 0) {
+      const int p = (int)rnd(24);
+      nib_inc(s.own, p);
+      used |= 1u << p;
+      --left;
+    }
+    int lo = 15;
+    for (int tries = 0; lo > 0 && tries < 1000; ++tries) {  // opponent mostly above the run
+      const int p = rnd(3) == 0 ? (int)rnd(24) : r0 + (int)rnd(24 - r0);
+      if (p > 23 || ((used >> p) & 1u)) continue;
+      nib_inc(s.opp, p);
+      --lo;
+    }
+    if (lo > 0) continue;
+    s.ft_own = rnd(4) == 0;
+    side_masks(s);
+    const int a = 1 + (int)rnd(6), b = 1 + (int)rnd(6);
+    if (a == b) continue;
+    const int dh = a > b ? a : b, dl = a > b ? b : a;
+    const uint32_t low = block_lowmask(s.P);
+    uint32_t fw;
+    const uint32_t bs = turn_block_set_sl(s.O, s.S1o, s.P, low, dh, dl, fw);
+    if (bs == 0u) continue;
+    ++done;
+    uint32_t Lh, Ll, Ch, Cl, Lh2, Ll2, Ch2, Cl2;
+    int M, M2;
+    c0_pair_bound_ref(s, low, dh, dl, bs, Lh, Ll, Ch, Cl, M);
+    turn_c0_pair_bound_w(s, dh, dl, bs, fw, Lh2, Ll2, Ch2, Cl2, M2);
+    bad += Lh != Lh2 || Ll != Ll2 || Ch != Ch2 || Cl != Cl2 || M != M2;
+    for (int w = 0; w < 2; ++w) {
+      const int u = w ? dl : dh, v = w ? dh : dl;
+      for (uint32_t m = w ? Ll : Lh; m; m &= m - 1u) {
+        const int p = __builtin_ctz(m);
+        Side c = s;
+        apply_die(c, p, u);
+        const uint32_t C = die_candidates(c.O, c.P, v);
+        const uint32_t ref = die_filter(c.O, c.S1o, block_info_low(c.O, low), C, v);
+        bad += ref != (C & ~block_reject_w(c.O, c.S1o, fw, C, v));
+        nc += ref != C;
+      }
+    }
+  }
+  *cut = nc;
+  return bad;
+}
+
+// On n random block-bound doubles positions: block_reject_w equals
+// die_filter at every node of the turn up to depth 3 (the lists the search
+// and the later sub-moves read), and f4_depth_w<3> equals f4_depth<3, 0> for
+// every root source.  Returns mismatches; *cut = node lists the rule cut.
+extern "C" int64_t hc_dbl_bound_w_random(int64_t n, uint32_t seed, int64_t* cut) {
+  uint64_t x = 0xE7037ED1A0B428DBull ^ ((uint64_t)seed << 21);
+  auto rnd = [&x](uint32_t m) {
+    x ^= x >> 12; x ^= x << 25; x ^= x >> 27;
+    return (uint32_t)(((x * 0x2545F4914F6CDD1Dull) >> 32) % m);
+  };
+  int64_t bad = 0, nc = 0;
+  for (int64_t done = 0; done < n;) {
+    Side s = side_start(0u);
+    for (int k = 0; k < 3; ++k) { s.own.w[k] = 0u; s.opp.w[k] = 0u; }
+    const int r0 = (int)rnd(18), rl = 3 + (int)rnd(5);
+    int left = 15;
+    uint32_t used = 0u;
+    for (int p = r0; p < r0 + rl && p < 24 && left > 0; ++p) {
+      const int c = 1 + (int)rnd(left < 3 ? left : 3);
+      for (int j = 0; j < c; ++j) nib_inc(s.own, p);
+      used |= 1u << p;
+      left -= c;
+    }
+    while (left > 0) {
+      const int p = (int)rnd(24);
+      nib_inc(s.own, p);
+      used |= 1u << p;
+      --left;
+    }
+    int lo = 15;
+    for (int tries = 0; lo > 0 && tries < 1000; ++tries) {
+      const int p = rnd(3) == 0 ? (int)rnd(24) : r0 + (int)rnd(24 - r0);
+      if (p > 23 || ((used >> p) & 1u)) continue;
+      nib_inc(s.opp, p);
+      --lo;
+    }
+    if (lo > 0) continue;
+    s.ft_own = rnd(3) == 0;
+    side_masks(s);
+    const int d = 1 + (int)rnd(6);
+    const int hl = (s.ft_own && (d == 3 || d == 4 || d == 6)) ? 2 : 1;
+    const uint32_t low = block_lowmask(s.P);
+    uint32_t fw;
+    if (turn_block_set_sl(s.O, s.S1o, s.P, low, d, d, fw) == 0u) continue;
+    ++done;
+    // every node to depth 3 (breadth-first over the plain search tree)
+    Side q[1 + 24 + 576];
+    int depth[1 + 24 + 576], hls[1 + 24 + 576], nq = 1, head = 0;
+    q[0] = s; depth[0] = 0; hls[0] = hl;
+    while (head < nq) {
+      const Side c = q[head];
+      const int dep = depth[head], h = hls[head];
+      ++head;
+      const uint32_t C = die_candidates(c.O, c.P, d);
+      const uint32_t ref = die_filter(c.O, c.S1o, block_info_low(c.O, low), C, d);
+      bad += ref != (C & ~block_reject_w(c.O, c.S1o, fw, C, d));
+      nc += ref != C;
+      if (dep >= 3) continue;
+      uint32_t L = ref & (h <= 0 ? ~HEAD : ~0u);
+      while (L && nq < (int)(sizeof(q) / sizeof(q[0]))) {
+        const int p = __builtin_ctz(L);
+        L &= L - 1u;
+        q[nq] = c;
+        apply_die(q[nq], p, d);
+        depth[nq] = dep + 1;
+        hls[nq] = h - (p == 23 ? 1 : 0);
+        ++nq;
+      }
+    }
+    uint32_t L = die_filter(s.O, s.S1o, block_info_low(s.O, low), die_candidates(s.O, s.P, d), d);
+    if (hl <= 0) L &= ~HEAD;
+    for (; L; L &= L - 1u) {
+      const int p = __builtin_ctz(L);
+      Side c = s;
+      apply_die(c, p, d);
+      const int h2 = hl - (p == 23 ? 1 : 0);
+      bad += f4_depth<3, 0>(c, low, d, h2, false) != f4_depth_w<3>(c, fw, d, h2);
+    }
+  }
+  *cut = nc;
   return bad;
 }
 

@@ -344,3 +344,26 @@ def test_hostcheck_block_set_straight_line(hostcheck):
     nb = ctypes.c_int64(0)
     assert f(ctypes.c_int64(400000 // SAN_DIV), ctypes.c_uint32(11), ctypes.byref(nb)) == 0
     assert nb.value > 1000 // SAN_DIV
+
+
+def test_hostcheck_pair_bound_from_failing_windows(hostcheck):
+    """Block-bound two-dice turns: C_0 / M from the failing windows
+    (turn_c0_pair_bound_w: masks, block_reject_w) equal env_turn_full's bound
+    branch (die_filter, f4_keep_pair), and block_reject_w equals die_filter
+    at every child of the turn."""
+    f = hostcheck.hc_pair_bound_w_random
+    f.restype = ctypes.c_int64
+    cut = ctypes.c_int64(0)
+    assert f(ctypes.c_int64(200000 // SAN_DIV), ctypes.c_uint32(3), ctypes.byref(cut)) == 0
+    assert cut.value > 1000 // SAN_DIV
+
+
+def test_hostcheck_doubles_bound_from_failing_windows(hostcheck):
+    """Block-bound doubles turns: block_reject_w (the turn's failing windows)
+    equals die_filter at every node to depth 3, and the search over those
+    lists (f4_depth_w) equals f4_depth for every first sub-move."""
+    f = hostcheck.hc_dbl_bound_w_random
+    f.restype = ctypes.c_int64
+    cut = ctypes.c_int64(0)
+    assert f(ctypes.c_int64(20000 // SAN_DIV), ctypes.c_uint32(9), ctypes.byref(cut)) == 0
+    assert cut.value > 1000 // SAN_DIV

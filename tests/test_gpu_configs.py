@@ -359,8 +359,8 @@ def test_rollout_launch_totals_rows(rules, plies, n):
     """narde_rollout_timed(totals=...): the launch writes its envs'
     statistics after it, summed per 256 envs -- equal to stats() of the same
     handle grouped the same way (and .sum(0) to totals()), for every rollout
-    kernel (REF2 producer/consumer, FULL4 one-wave below 48 plies and
-    rule/helper waves above) and ragged env counts."""
+    kernel (REF2 producer/consumer at both store policies, FULL4
+    k_rollout_wave) and ragged env counts."""
     from gym_narde import _lib
 
     env = vec(n, seed=13, rules=rules)

@@ -126,12 +126,10 @@ def test_full4_selfplay_trajectory_vs_oracle(dice_mode, max_steps):
 
 @pytest.mark.parametrize("max_steps", [1000, 30])
 def test_full4_rollout_equals_steps(max_steps):
-    """narde_rollout_full over launch boundaries == per-ply k_step<full>: 1 and
-    29 plies take k_rollout_wave, 70 and 100 k_rollout_full (rule + helper
-    waves, lanes drifting up to 16 plies, the per-ply rows through the LDS
-    ring), ragged odd n (the last workgroup partly empty, odd plies' rows not
-    64-B aligned); with TimeLimit 30 every env truncates several times
-    inside the launches (the truncated flag through the ring)."""
+    """narde_rollout_full over launch boundaries == per-ply k_step<full>:
+    launches of 1, 29, 70 and 100 plies (k_rollout_wave), ragged odd n (the
+    last workgroup partly empty, odd plies' rows not 64-B aligned); with
+    TimeLimit 30 every env truncates several times inside the launches."""
     n, seed = 2048 + 77, 31337
     a = vec(n, seed=seed, max_episode_steps=max_steps)
     b = vec(n, seed=seed, max_episode_steps=max_steps)
@@ -157,8 +155,8 @@ def test_full4_rollout_equals_steps(max_steps):
 
 @pytest.mark.parametrize("plies", [120, 20])
 def test_full4_full_batch_window_and_invariants(plies):
-    """B = 65,536 (the bench shape; 120 plies: k_rollout_full, 20:
-    k_rollout_wave, the driver's launch): a 2,048-env window equals the
+    """B = 65,536 (the bench shape; 120-ply launches, and the driver's 20-ply
+    launch; k_rollout_wave): a 2,048-env window equals the
     oracle run on those global ids; checker conservation and played == max
     dice everywhere."""
     n, seed = 65536, 7
@@ -191,8 +189,8 @@ def test_full4_full_batch_window_and_invariants(plies):
 def test_tiny_batches_both_rules_both_kernels(n):
     """One env, one wave less one lane, one wave plus one lane: REF2 rollouts
     of 20 plies (k_rollout_pc<true, true>: non-temporal stores) and 60 plies
-    (<true, false>), FULL4 rollouts of 20 (k_rollout_wave) and 60
-    (k_rollout_full: rule + helper waves) equal the oracle ply for ply."""
+    (<true, false>), FULL4 rollouts of 20 and 60 plies (k_rollout_wave)
+    equal the oracle ply for ply."""
     from gym_narde.vector import VecNardeEnv
 
     seed, env0 = 4242, 3

@@ -41,7 +41,7 @@ timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
         -d "$OUT/pmc_full/write" -o pmc -- python3 "$ROOT/tools/pmc_target.py" --rules full4 --plies 1000 --launches 3 \
         > "$OUT/pmc_full_write.log" 2>&1) \
   && python3 tools/pmc_summary.py --fetch "$OUT/pmc_full/fetch" --write "$OUT/pmc_full/write" \
-        --kernel "k_rollout_full<true>" --bytes-per-ply 118 --plies 1000 --out "$OUT/pmc_k_rollout_full.json" \
+        --kernel "k_rollout_wave<true>" --bytes-per-ply 118 --plies 1000 --out "$OUT/pmc_k_rollout_full.json" \
   && echo "[gpu_round] $(date +%T) bench --rules full4" \
   && timeout -k 10 300 python bench.py --rules full4 --no-cpu-baseline > "$OUT/bench_full4.json" 2> "$OUT/bench_full4.err" \
   && echo "[gpu_round] $(date +%T) rocprof kernel trace full4" \
