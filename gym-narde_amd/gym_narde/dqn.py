@@ -690,6 +690,12 @@ class BatchedDQNDriver:
         (post-move); greedy="reference": over act()'s own candidate sets
         (narde_act_masks: list #1's codes, then the pre-move second list of
         that move 1, :520-560).
+        Ties (parity unpinned): the policy kernels break an exact Q tie by
+        the LOWEST code; act()'s torch.argmax over valid_first_moves' keys
+        breaks it by insertion order (list #1: the higher die's sources
+        first, then the lower die's, :527-539), so on tied or NaN Q-values
+        move 1 may differ from the reference.  The 2,500-decision golden
+        (act_greedy.npz, random fixed Q) has no ties.
         Exploring rows (one shared draw per row and step): explore="plays"
         draws one of act()'s (move1, move2) combinations uniformly
         (k_explore_plays), as random.choice(valid_move_combinations)."""

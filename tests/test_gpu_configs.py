@@ -353,6 +353,55 @@ def test_rccl_world1_process_group_gathers_device_stats():
     assert r.returncode == 0 and "RCCL_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
 
+_NCCL_RANK = r"""
+import os, sys
+sys.path[:0] = [os.path.join(sys.argv[1], "gym-narde_amd")]
+import torch
+import torch.distributed as dist
+from gym_narde import distributed as D, _lib
+from gym_narde.vector import VecNardeEnv
+r, w, local = D.init_from_env(backend="nccl", force=True)
+assert w == 2 and dist.get_backend() == "nccl"
+n = 4096
+env = VecNardeEnv(n, device=f"cuda:{local}", seed=3, env_id_offset=r * n)
+rows = torch.empty((_lib.wg_rows(n), 3), dtype=torch.int64, device=env.device)
+L = env.rollout_launcher(20, env.rollout_buffers(20), totals=rows)
+L()
+G = D.RcclGather(rows)
+out = G()
+torch.cuda.synchronize()
+mine = env.totals().sum(0)
+allt = [torch.empty_like(mine) for _ in range(w)]
+dist.all_gather(allt, mine)  # every rank's env.totals(), by the torch collective
+assert out.shape == (w,) + tuple(rows.shape)
+for k in range(w):
+    assert torch.equal(out[k].sum(0), allt[k]), (k, out[k].sum(0), allt[k])
+G.close()
+dist.barrier()
+dist.destroy_process_group()
+env.close()
+print("RCCL2_OK", r)
+"""
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="two ranks over RCCL need two GPUs")
+def test_rccl_two_ranks_gather_equals_every_rank_totals():
+    """the N > 1 timed-region gather (D.RcclGather, RCCL's
+    ncclAllGather through its C API) at world size 2 on two GPUs: the
+    gathered per-256-env rows of rank k sum to rank k's env.totals(), and
+    both ranks exit cleanly."""
+    port = str(_free_port())
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=port, RANK=str(r), WORLD_SIZE="2",
+                   LOCAL_RANK=str(r), LOCAL_WORLD_SIZE="2")
+        procs.append(subprocess.Popen([sys.executable, "-c", _NCCL_RANK, ROOT], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=240) for p in procs]
+    for r, (p, (o, e)) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0 and f"RCCL2_OK {r}" in o, o[-2000:] + e[-4000:]
+
+
 @pytest.mark.parametrize("rules,plies,n", [("ref2", 20, 65536), ("ref2", 1000, 1000), ("full4", 20, 4099),
                                            ("full4", 60, 65536), ("ref2", 7, 300)])
 def test_rollout_launch_totals_rows(rules, plies, n):

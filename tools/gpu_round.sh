@@ -18,13 +18,13 @@ pmc_pair() {  # rules plies kernel bytes_per_ply name
   local rules=$1 plies=$2 kernel=$3 bpp=$4 name=$5 launches=3
   [ "$plies" -lt 100 ] && launches=5
   echo "[gpu_round] $(date +%T) pmc $name" \
-  && (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_$name/fetch" -o pmc \
+  && (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/$name/fetch" -o pmc \
         -- python3 "$ROOT/tools/pmc_target.py" --rules "$rules" --plies "$plies" --launches $launches \
-        > "$OUT/pmc_${name}_fetch.log" 2>&1) \
-  && (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_$name/write" -o pmc \
+        > "$OUT/${name}_fetch.log" 2>&1) \
+  && (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/$name/write" -o pmc \
         -- python3 "$ROOT/tools/pmc_target.py" --rules "$rules" --plies "$plies" --launches $launches \
-        > "$OUT/pmc_${name}_write.log" 2>&1) \
-  && python3 tools/pmc_summary.py --fetch "$OUT/pmc_$name/fetch" --write "$OUT/pmc_$name/write" \
+        > "$OUT/${name}_write.log" 2>&1) \
+  && python3 tools/pmc_summary.py --fetch "$OUT/$name/fetch" --write "$OUT/$name/write" \
         --kernel "$kernel" --bytes-per-ply "$bpp" --plies "$plies" --out "$OUT/$name.json"
 }
 
@@ -32,10 +32,10 @@ sq_pass() {  # rules plies kernel name
   local rules=$1 plies=$2 kernel=$3 name=$4 launches=3
   [ "$plies" -lt 100 ] && launches=5
   echo "[gpu_round] $(date +%T) sq $name" \
-  && (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/sq_$name" -o sq \
+  && (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc $SQ --output-format csv -d "$OUT/$name" -o sq \
         -- python3 "$ROOT/tools/pmc_target.py" --rules "$rules" --plies "$plies" --launches $launches \
-        > "$OUT/sq_$name.log" 2>&1) \
-  && python3 tools/sq_summary.py --dir "$OUT/sq_$name" --kernel "$kernel" --plies "$plies" --out "$OUT/$name.json"
+        > "$OUT/$name.log" 2>&1) \
+  && python3 tools/sq_summary.py --dir "$OUT/$name" --kernel "$kernel" --plies "$plies" --out "$OUT/$name.json"
 }
 
 if [ "$PHASE" = run ]; then
