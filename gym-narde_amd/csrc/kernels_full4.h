@@ -293,15 +293,21 @@ __device__ void coop_depth_w(const Side& s, uint32_t fw, int d, int hl, uint32_t
     const uint32_t ofw = rl(fw, ow), om = rl(m0, ow);
     const int od = (int)rl((uint32_t)d, ow), ohl = (int)rl((uint32_t)hl, ow), oneed = (int)rl((uint32_t)need, ow);
     const bool has = lane < 24 && ((om >> lane) & 1u);
-    bool k0 = false, k1 = false, k2 = false;
-    if (has) {
-      Side cc = c;
-      apply_die(cc, lane, od);
-      const int hl2 = ohl - (lane == 23 ? 1 : 0);
-      const int dep = oneed == 1 ? f4_depth_w<1>(cc, ofw, od, hl2)
-                                 : (oneed == 2 ? f4_depth_w<2>(cc, ofw, od, hl2) : f4_depth_w<3>(cc, ofw, od, hl2));
-      k0 = dep >= 1; k1 = dep >= 2; k2 = dep >= 3;
+    // below each source: the search's first path straight-line
+    // (f4_probe_w), the search itself only where that path falls short
+    const int src = has ? lane : 0;
+    Side cc = c;
+    apply_move_if(cc, src, src - od < 0 ? OFF : src - od, has);
+    const int hl2 = ohl - ((has && src == 23) ? 1 : 0);
+    int dep = oneed == 1 ? f4_probe_w<1>(cc, ofw, od, hl2)
+                         : (oneed == 2 ? f4_probe_w<2>(cc, ofw, od, hl2) : f4_probe_w<3>(cc, ofw, od, hl2));
+    const bool miss = has && dep < oneed;
+    if (__ballot(miss) != 0ull) {  // wave-uniform
+      if (miss)
+        dep = oneed == 1 ? f4_depth_w<1>(cc, ofw, od, hl2)
+                         : (oneed == 2 ? f4_depth_w<2>(cc, ofw, od, hl2) : f4_depth_w<3>(cc, ofw, od, hl2));
     }
+    const bool k0 = has && dep >= 1, k1 = has && dep >= 2, k2 = has && dep >= 3;
     const uint32_t r0 = (uint32_t)__ballot(k0), r1 = (uint32_t)__ballot(k1), r2 = (uint32_t)__ballot(k2);
     out[0] = lane == ow ? r0 : out[0];
     out[1] = lane == ow ? r1 : out[1];

@@ -1636,6 +1636,31 @@ NARDE_FN int f4_depth_w(const Side& s, uint32_t fw, int d, int hl) {
   }
 }
 
+// The first path f4_depth_w<N> walks (the lowest listed source at every
+// node), straight-line: its depth, which is f4_depth_w's whenever it reaches
+// N (the search stops there) -- so only a lane whose probe falls short needs
+// the search.  (Doubles searches end at depth N along this path in ~90 % of
+// the block-bound turns that f4_safe_bound leaves)
+template <int N>
+NARDE_FN int f4_probe_w(Side c, uint32_t fw, int d, int hl) {
+  int dep = 0;
+  bool alive = true;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    uint32_t L = die_candidates_sl(c.O, c.P, d);
+    L &= ~block_reject_w(c.O, c.S1o, fw, L, d);
+    L &= hl <= 0 ? ~HEAD : ~0u;
+    alive = alive && L != 0u;
+    dep += alive ? 1 : 0;
+    if (k + 1 < N) {
+      const int p = (int)__builtin_ctz(L | 0x800000u);  // 23 when L is empty (nothing applied then)
+      apply_move_if(c, p, p - d < 0 ? OFF : p - d, alive);
+      hl -= (alive && p == 23) ? 1 : 0;
+    }
+  }
+  return dep;
+}
+
 // turn_block_set without its early exit and with both kinds' per-window
 // tests computed (a wave holds both kinds of turn)
 // fw (out): the failing windows' start points (bit i = points i..i+5): the

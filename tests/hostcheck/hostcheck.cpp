@@ -577,6 +577,12 @@ extern "C" int64_t hc_dbl_bound_w_random(int64_t n, uint32_t seed, int64_t* cut)
       apply_die(c, p, d);
       const int h2 = hl - (p == 23 ? 1 : 0);
       bad += f4_depth<3, 0>(c, low, d, h2, false) != f4_depth_w<3>(c, fw, d, h2);
+      // the straight-line probe: never deeper than the search, and equal to
+      // it whenever it reaches the bound
+      const int e1 = f4_depth_w<1>(c, fw, d, h2), e2 = f4_depth_w<2>(c, fw, d, h2), e3 = f4_depth_w<3>(c, fw, d, h2);
+      const int q1 = f4_probe_w<1>(c, fw, d, h2), q2 = f4_probe_w<2>(c, fw, d, h2), q3 = f4_probe_w<3>(c, fw, d, h2);
+      bad += q1 > e1 || q2 > e2 || q3 > e3 || (q1 == 1 && e1 != 1) || (q2 == 2 && e2 != 2) || (q3 == 3 && e3 != 3);
+      bad += q1 != e1;  // depth 1: the probe is the search
     }
   }
   *cut = nc;

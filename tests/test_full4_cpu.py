@@ -361,7 +361,9 @@ def test_hostcheck_pair_bound_from_failing_windows(hostcheck):
 def test_hostcheck_doubles_bound_from_failing_windows(hostcheck):
     """Block-bound doubles turns: block_reject_w (the turn's failing windows)
     equals die_filter at every node to depth 3, and the search over those
-    lists (f4_depth_w) equals f4_depth for every first sub-move."""
+    lists (f4_depth_w) equals f4_depth for every first sub-move, and the
+    straight-line probe of its first path (f4_probe_w, the device's
+    coop_depth_w) is never deeper and equals it whenever it reaches N."""
     f = hostcheck.hc_dbl_bound_w_random
     f.restype = ctypes.c_int64
     cut = ctypes.c_int64(0)
