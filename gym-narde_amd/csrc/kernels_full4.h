@@ -297,7 +297,7 @@ __device__ void coop_depth_w(const Side& s, uint32_t fw, int d, int hl, uint32_t
     // (f4_probe_w), the search itself only where that path falls short
     const int src = has ? lane : 0;
     Side cc = c;
-    apply_move_if(cc, src, src - od < 0 ? OFF : src - od, has);
+    apply_die_if(cc, src, od, has);
     const int hl2 = ohl - ((has && src == 23) ? 1 : 0);
     int dep = oneed == 1 ? f4_probe_w<1>(cc, ofw, od, hl2)
                          : (oneed == 2 ? f4_probe_w<2>(cc, ofw, od, hl2) : f4_probe_w<3>(cc, ofw, od, hl2));
@@ -358,7 +358,7 @@ __device__ __forceinline__ void ply_bound_turn(Side& s, int dh, int dl, uint32_t
   const int d0 = hi ? dh : dl;
   const int p0 = select_bit(hi ? Ch : Cl, hi ? idx : idx - nh);
   const bool go = M >= 1;
-  apply_move_if(s, p0, p0 - d0 < 0 ? OFF : p0 - d0, go);
+  apply_die_if(s, p0, d0, go);
   uint32_t pl0 = go ? (0xFFFF0000u | ((uint32_t)d0 << 8) | (uint32_t)p0) : 0xFFFFFFFFu, pl1 = 0xFFFFFFFFu;
   int hl = hl0 - ((go && p0 == 23) ? 1 : 0);
   const int d1 = dbl ? dh : (d0 == dh ? dl : dh);
@@ -382,7 +382,7 @@ __device__ __forceinline__ void ply_bound_turn(Side& s, int dh, int dl, uint32_t
     }
     const uint32_t wk = k == 1 ? w[1] : (k == 2 ? w[2] : w[3]);
     const int p = select_bit(Lk, (int)mulhi_u32(wk, (uint32_t)__builtin_popcount(Lk)));
-    apply_move_if(s, p, p - dk < 0 ? OFF : p - dk, act);
+    apply_die_if(s, p, dk, act);
     const uint32_t v = ((uint32_t)dk << 8) | (uint32_t)p;
     if (k == 1) pl0 = act ? ((pl0 & 0xFFFFu) | (v << 16)) : pl0;
     if (k == 2) pl1 = act ? ((pl1 & 0xFFFF0000u) | v) : pl1;

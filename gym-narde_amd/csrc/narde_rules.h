@@ -1380,6 +1380,29 @@ NARDE_FN void apply_move_if(Side& s, int f, int t, bool en) {
   s.ft_own = en ? 0u : s.ft_own;
 }
 
+// apply_move_if(s, p, p - d < 0 ? OFF : p - d, en) with the landing as
+// max(p - d, 0) and the bear-off test as its sign (no OFF round trip)
+NARDE_FN void apply_die_if(Side& s, int p, int d, bool en) {
+  const int t = p - d;
+  const bool off = t < 0;
+  const int tq = t > 0 ? t : 0;
+  const uint32_t cf = nib_get(s.own, p);
+  const bool land = en && !off;
+  const uint32_t bf = en ? (1u << p) : 0u;
+  const uint32_t bt = land ? (1u << tq) : 0u;
+  const uint32_t vf = en ? (0xFFFFFFFFu << (4 * (p & 7))) : 0u;
+  const uint32_t vt = (land ? 1u : 0u) << (4 * (tq & 7));
+  const int kf = p >> 3, kt = tq >> 3;
+  s.own.w[0] += (kf == 0 ? vf : 0u) + (kt == 0 ? vt : 0u);
+  s.own.w[1] += (kf == 1 ? vf : 0u) + (kt == 1 ? vt : 0u);
+  s.own.w[2] += (kf == 2 ? vf : 0u) + (kt == 2 ? vt : 0u);
+  const uint32_t t01 = bt & (~s.O | s.S1o);
+  s.O = (s.O & (cf == 1u ? ~bf : ~0u)) | bt;
+  s.S1o ^= (cf - 1u < 2u ? bf : 0u) ^ t01;
+  s.off_own += (en && off) ? 1u : 0u;
+  s.ft_own = en ? 0u : s.ft_own;
+}
+
 // f4_keep_pair_bf with the home test as masks
 NARDE_FN uint32_t f4_keep_pair_bf_sl(uint32_t O, uint32_t S1, uint32_t P, int a, int b, uint32_t L) {
   const uint32_t G = ~(P << b) & (MASK24 << b) & MASK24;
@@ -1488,7 +1511,7 @@ NARDE_FN void turn_moves_sl(Side& s, int dh, int dl, uint32_t Ch, uint32_t Cl, i
   const int d0 = hi ? dh : dl;
   const int p0 = select_bit(hi ? Ch : Cl, hi ? idx : idx - nh);
   const bool go = M >= 1;
-  apply_move_if(s, p0, p0 - d0 < 0 ? OFF : p0 - d0, go);
+  apply_die_if(s, p0, d0, go);
   // the played word as two 32-bit halves (sub-moves 0-1, 2-3)
   uint32_t pl0 = go ? (0xFFFF0000u | ((uint32_t)d0 << 8) | (uint32_t)p0) : 0xFFFFFFFFu, pl1 = 0xFFFFFFFFu;
   hl -= (go && p0 == 23) ? 1 : 0;
@@ -1502,7 +1525,7 @@ NARDE_FN void turn_moves_sl(Side& s, int dh, int dl, uint32_t Ch, uint32_t Cl, i
     Lk &= hl <= 0 ? ~HEAD : ~0u;
     const uint32_t wk = k == 1 ? w[1] : (k == 2 ? w[2] : w[3]);
     const int p = select_bit(Lk, (int)mulhi_u32(wk, (uint32_t)__builtin_popcount(Lk)));
-    apply_move_if(s, p, p - dk < 0 ? OFF : p - dk, act);
+    apply_die_if(s, p, dk, act);
     const uint32_t v = ((uint32_t)dk << 8) | (uint32_t)p;
     if (k == 1) pl0 = act ? ((pl0 & 0xFFFFu) | (v << 16)) : pl0;
     if (k == 2) pl1 = act ? ((pl1 & 0xFFFF0000u) | v) : pl1;
@@ -1654,7 +1677,7 @@ NARDE_FN int f4_probe_w(Side c, uint32_t fw, int d, int hl) {
     dep += alive ? 1 : 0;
     if (k + 1 < N) {
       const int p = (int)__builtin_ctz(L | 0x800000u);  // 23 when L is empty (nothing applied then)
-      apply_move_if(c, p, p - d < 0 ? OFF : p - d, alive);
+      apply_die_if(c, p, d, alive);
       hl -= (alive && p == 23) ? 1 : 0;
     }
   }
