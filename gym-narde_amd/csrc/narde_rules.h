@@ -677,16 +677,13 @@ NARDE_FN uint32_t land_step(uint32_t S, uint32_t P, int d) { return (S >> d) & ~
 // are not own: a bit-sliced count of the holes over the six shifted masks
 NARDE_FN uint32_t windows_few_holes(uint32_t O, int k) {
   const uint32_t h = ~O & MASK24;
-  uint32_t s0 = 0u, s1 = 0u, s2 = 0u;  // 3-bit counter per window start
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    const uint32_t x = h >> j;
-    const uint32_t c0 = s0 & x;
-    s0 ^= x;
-    const uint32_t c1 = s1 & c0;
-    s1 ^= c0;
-    s2 |= c1;
-  }
+  // the count of the six shifted hole masks per window start, bit-sliced
+  // through two carry-save adders (xor3 / majority: one v_bitop3 each)
+  const uint32_t x0 = h, x1 = h >> 1, x2 = h >> 2, x3 = h >> 3, x4 = h >> 4, x5 = h >> 5;
+  const uint32_t sa = x0 ^ x1 ^ x2, ca = (x0 & x1) | (x2 & (x0 ^ x1));
+  const uint32_t sb = x3 ^ x4 ^ x5, cb = (x3 & x4) | (x5 & (x3 ^ x4));
+  const uint32_t s0 = sa ^ sb, c0 = sa & sb;
+  const uint32_t s1 = ca ^ cb ^ c0, s2 = (ca & cb) | (c0 & (ca ^ cb));
   return k >= 4 ? ~(s2 & (s1 | s0)) : ~s2 & ~(s1 & s0);
 }
 

@@ -991,3 +991,25 @@ extern "C" int64_t hc_sure_pair_random(int64_t n, uint32_t seed, int64_t* sure, 
   *total = tot;
   return bad;
 }
+
+// windows_few_holes (two carry-save adders) against the plain bit-sliced
+// counter it replaced, over every 24-bit own mask; returns mismatches
+static uint32_t wfh_ref(uint32_t O, int k) {
+  const uint32_t h = ~O & MASK24;
+  uint32_t s0 = 0u, s1 = 0u, s2 = 0u;
+  for (int j = 0; j < 6; ++j) {
+    const uint32_t x = h >> j;
+    const uint32_t c0 = s0 & x;
+    s0 ^= x;
+    const uint32_t c1 = s1 & c0;
+    s1 ^= c0;
+    s2 |= c1;
+  }
+  return k >= 4 ? ~(s2 & (s1 | s0)) : ~s2 & ~(s1 & s0);
+}
+extern "C" int64_t hc_windows_few_holes_all() {
+  int64_t bad = 0;
+  for (uint32_t O = 0; O < (1u << 24); ++O)
+    bad += (wfh_ref(O, 2) != windows_few_holes(O, 2)) + (wfh_ref(O, 4) != windows_few_holes(O, 4));
+  return bad;
+}

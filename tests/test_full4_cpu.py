@@ -377,3 +377,12 @@ def test_hostcheck_block_reject_loop_free(hostcheck):
     f = hostcheck.hc_block_reject_bp_random
     f.restype = ctypes.c_int64
     assert f(ctypes.c_int64(2000000 // SAN_DIV), ctypes.c_uint32(17)) == 0
+
+
+def test_hostcheck_windows_few_holes_exhaustive(hostcheck):
+    """windows_few_holes (the block test's hole count per 6-window, two
+    carry-save adders) equals the plain bit-sliced counter on every one of
+    the 2^24 own-point masks, for both hole limits (2: two dice, 4: doubles)."""
+    f = hostcheck.hc_windows_few_holes_all
+    f.restype = ctypes.c_int64
+    assert f() == 0
