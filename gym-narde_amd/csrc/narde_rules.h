@@ -1746,41 +1746,6 @@ NARDE_FN uint32_t block_reject_w(uint32_t O, uint32_t S1, uint32_t fw, uint32_t 
   return rej;
 }
 
-// block_reject_w without the loop: every failing window at once.  Full
-// ones (FF = runs6(O) & fw) reject every candidate but a single checker in
-// all of them (their intersection is [max start, min start + 5]); a window
-// with one hole h at offset o = h - start rejects a candidate landing on h
-// unless it is a single checker inside the window -- one landing at h + d
-// lies outside it iff o >= 6 - d.  (Equal to block_reject_w:
-// tests/hostcheck hc_block_reject_bp_random.)
-NARDE_FN uint32_t block_reject_bp(uint32_t O, uint32_t S1, uint32_t fw, uint32_t C, int d) {
-  const uint32_t FF = runs6(O) & fw;
-  const int mins = __builtin_ctz(FF | HEAD), maxs = 31 - __builtin_clz(FF | 1u);  // (no shift past 31 below)
-  const uint32_t inter = maxs <= mins + 5 ? (((2u << (mins + 5)) - 1u) & ~((1u << maxs) - 1u)) : 0u;
-  const uint32_t rej_full = FF ? (C & ~(S1 & inter)) : 0u;
-  // windows with exactly one hole: a bit-sliced count of the holes
-  const uint32_t Z = ~O & MASK24;
-  uint32_t s0 = 0u, s1 = 0u, s2 = 0u;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) {
-    const uint32_t x = Z >> j;
-    const uint32_t c0 = s0 & x;
-    s0 ^= x;
-    const uint32_t c1 = s1 & c0;
-    s1 ^= c0;
-    s2 |= c1;
-  }
-  const uint32_t OH = fw & s0 & ~s1 & ~s2;
-  uint32_t H1 = 0u, Hs = 0u;
-#pragma unroll
-  for (int o = 0; o < 6; ++o) {
-    const uint32_t h = (OH & (Z >> o)) << o;  // the hole of each one-hole window whose hole is at offset o
-    H1 |= h;
-    Hs |= o >= 6 - d ? h : 0u;
-  }
-  return rej_full | (C & ~S1 & (H1 << d)) | (C & S1 & (Hs << d));
-}
-
 // after first move p of die a (a two-dice turn with failing windows fw):
 // does die b still have a move (head rule: not a second head move)?
 NARDE_FN bool pair_child_ok_w(const Side& s, uint32_t fw, int p, int a, int b) {

@@ -589,27 +589,6 @@ extern "C" int64_t hc_dbl_bound_w_random(int64_t n, uint32_t seed, int64_t* cut)
   return bad;
 }
 
-// block_reject_bp (every failing window at once) against block_reject_w
-// (a loop over them) on random boards, window sets and candidate masks
-extern "C" int64_t hc_block_reject_bp_random(int64_t n, uint32_t seed) {
-  uint64_t x = 0x94D049BB133111EBull ^ ((uint64_t)seed << 13);
-  auto rnd = [&x]() {
-    x ^= x >> 12; x ^= x << 25; x ^= x >> 27;
-    return (uint32_t)((x * 0x2545F4914F6CDD1Dull) >> 32);
-  };
-  int64_t bad = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    // dense own masks (runs and near-runs are what the windows test)
-    const uint32_t O = (rnd() | rnd() | (rnd() & rnd())) & MASK24;
-    const uint32_t S1 = O & rnd();
-    const uint32_t fw = rnd() & rnd() & (MASK24 >> 5) & (runs6(O | (rnd() & rnd())) | (rnd() & rnd() & rnd()));
-    const uint32_t C = O & rnd();
-    const int d = 1 + (int)(rnd() % 6);
-    bad += block_reject_w(O, S1, fw, C, d) != block_reject_bp(O, S1, fw, C, d);
-  }
-  return bad;
-}
-
 // turn_block_set_sl (no early exit, both kinds' window tests) against
 // turn_block_set on n random positions (hc_pair_bf_random's boards, both
 // kinds of roll).  Returns mismatches; *bound = block-bound cases.

@@ -371,14 +371,6 @@ def test_hostcheck_doubles_bound_from_failing_windows(hostcheck):
     assert cut.value > 1000 // SAN_DIV
 
 
-def test_hostcheck_block_reject_loop_free(hostcheck):
-    """block_reject_bp (every failing window at once) equals block_reject_w
-    (a loop over the windows) on random boards, window sets and dice."""
-    f = hostcheck.hc_block_reject_bp_random
-    f.restype = ctypes.c_int64
-    assert f(ctypes.c_int64(2000000 // SAN_DIV), ctypes.c_uint32(17)) == 0
-
-
 def test_hostcheck_windows_few_holes_exhaustive(hostcheck):
     """windows_few_holes (the block test's hole count per 6-window, two
     carry-save adders) equals the plain bit-sliced counter on every one of
