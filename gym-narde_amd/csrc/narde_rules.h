@@ -1692,25 +1692,28 @@ NARDE_FN int f4_probe_w(Side c, uint32_t fw, int d, int hl) {
 // turn (a wave holds both): the windows that can fill, then one loop per
 // kind over its lanes' windows (a wave pays a kind's loop only where a lane
 // of that kind has a window; round 3's single loop computed both kinds'
-// tests in every iteration).  Two dice, a window with two holes needs both
-// one step from an own point (each sub-move fills one hole), so only those
-// enter its loop: 1.46 -> 0.94 + 0.62 iterations per wave-ply (host
-// statistics of random self-play).
+// tests in every iteration).  Windows whose holes are too far from the own
+// points for the turn's steps never enter a loop: 1.46 -> 0.94 + 0.36
+// iterations per wave-ply (host statistics of random self-play).
 // fw (out): the failing windows' start points (bit i = points i..i+5): the
 // only windows that can be full at a node of the turn (block_reject_w)
 NARDE_FN uint32_t turn_block_set_sl(uint32_t O, uint32_t S1, uint32_t P, uint32_t low, int dh, int dl,
                                     uint32_t& fw) {
   const bool dbl = dh == dl;
-  const uint32_t A = O | land_step(O, P, dh) | land_step(O, P, dl);
-  uint32_t U = A | land_step(A, P, dh) | land_step(A, P, dl);
-  const uint32_t V = land_step(U, P, dh);
-  U |= dbl ? (V | land_step(V, P, dh)) : 0u;
+  const uint32_t A = O | land_step(O, P, dh) | land_step(O, P, dl);  // one step
+  const uint32_t U2 = A | land_step(A, P, dh) | land_step(A, P, dl);  // two
+  const uint32_t V = land_step(U2, P, dh);
+  const uint32_t U = U2 | (dbl ? (V | land_step(V, P, dh)) : 0u);     // doubles: four
   uint32_t s0, s1, s2;
   window_hole_count(O, s0, s1, s2);
-  const uint32_t le1 = ~s2 & ~s1, eq2 = s1 & ~s0 & ~s2, le4 = ~(s2 & (s1 | s0));
-  const uint32_t rU = runs6(U) & low;
-  uint32_t win2 = dbl ? 0u : ((le1 & rU) | (eq2 & runs6(A) & low));
-  uint32_t wind = dbl ? (le4 & rU) : 0u;
+  const uint32_t le1 = ~s2 & ~s1, le2 = ~s2 & ~(s1 & s0), eq2 = s1 & ~s0 & ~s2;
+  const uint32_t eq3 = s1 & s0 & ~s2, eq4 = s2 & ~s1 & ~s0;
+  const uint32_t rU = runs6(U) & low, rA = runs6(A) & low;
+  // the landings' steps to a window's holes sum to at most 4 (doubles) or
+  // each hole takes one sub-move (two dice): three or four holes need every
+  // hole within two / one steps, two holes with two dice one step each
+  uint32_t win2 = dbl ? 0u : ((le1 & rU) | (eq2 & rA));
+  uint32_t wind = dbl ? ((le2 & rU) | (eq3 & runs6(U2) & low) | (eq4 & rA)) : 0u;
   uint32_t out = 0u;
   bool full = false;
   fw = 0u;
