@@ -185,6 +185,30 @@ def test_full4_full_batch_window_and_invariants(plies):
     assert (M == 4).mean() > 0.08
 
 
+def test_full4_steady_state_window_after_selfplay():
+    """The driver's 20-ply launch at B = 65,536 in the steady state (300
+    plies of stats-only self-play first: the envs spread over every game
+    phase, so block-bound two-dice and doubles turns, the failing-window
+    loops per kind and the doubles search all occur in every launch,
+    tools/diag/wave_kinds.cpp): a 2,048-env window of the launch's outputs
+    and final boards equals the oracle."""
+    n, seed, pre, plies, lo = 65536, 11, 300, 20, 20000
+    env = vec(n, seed=seed)
+    env.selfplay(pre)
+    bufs = env.rollout_buffers(plies)
+    env.rollout(plies, bufs)
+    ref = O.SelfPlay(2048, seed=seed, env0=lo)
+    ref.reset(0)
+    ref.run_full(pre, record=False)
+    rec = ref.run_full(plies)
+    sl = slice(lo, lo + 2048)
+    assert np.array_equal(np_(bufs["obs"][:, sl]), rec["obs"].astype(np.int32))
+    assert np.array_equal(np_(bufs["legal"][:, sl]).view(np.uint64), rec["legal"])
+    assert np.array_equal(np_(bufs["actions"][:, sl]).view(np.uint64), rec["played"])
+    assert np.array_equal(np_(bufs["reward"][:, sl]), rec["reward"].astype(np.int32))
+    assert np.array_equal(np_(env.get_state()["board"])[sl], ref.board)
+
+
 @pytest.mark.parametrize("n", [1, 63, 65])
 def test_tiny_batches_both_rules_both_kernels(n):
     """One env, one wave less one lane, one wave plus one lane: REF2 rollouts
