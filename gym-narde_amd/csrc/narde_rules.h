@@ -1793,8 +1793,19 @@ NARDE_FN bool pair_child_ok_w(const Side& s, uint32_t fw, int p, int a, int b) {
 NARDE_FN void turn_c0_pair_bound_w(const Side& s, int dh, int dl, uint32_t hs, uint32_t fw, uint32_t& Lh,
                                    uint32_t& Ll, uint32_t& Ch, uint32_t& Cl, int& M) {
   const uint32_t Chc = die_candidates_sl(s.O, s.P, dh), Clc = die_candidates_sl(s.O, s.P, dl);
-  Lh = Chc & ~block_reject_w(s.O, s.S1o, fw, Chc, dh);
-  Ll = Clc & ~block_reject_w(s.O, s.S1o, fw, Clc, dl);
+  // both dice's lists through one loop over the failing windows
+  // (block_reject_w twice, the window masks shared)
+  uint32_t rh = 0u, rl = 0u;
+  for (uint32_t f = fw; f; f &= f - 1u) {
+    const uint32_t W = 0x3Fu << __builtin_ctz(f);
+    const uint32_t H = W & ~s.O;
+    const bool one = (H & (H - 1u)) == 0u;
+    const uint32_t keep = ~(W & s.S1o);
+    rh |= H == 0u ? (Chc & keep) : (Chc & keep & (one ? (H << dh) : 0u) & MASK24);
+    rl |= H == 0u ? (Clc & keep) : (Clc & keep & (one ? (H << dl) : 0u) & MASK24);
+  }
+  Lh = Chc & ~rh;
+  Ll = Clc & ~rl;
   uint32_t kh = f4_sure_pair(s.O, s.P, dl, Lh, hs), kl = f4_sure_pair(s.O, s.P, dh, Ll, hs);
   uint32_t mh = Lh & ~kh, ml = Ll & ~kl;
   while (mh | ml) {
