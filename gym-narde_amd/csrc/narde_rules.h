@@ -1765,15 +1765,18 @@ NARDE_FN uint32_t turn_block_set_sl(uint32_t O, uint32_t S1, uint32_t P, uint32_
 // failing window W full -- W full already (no hole) and x not a single
 // checker of W, or W's one hole is the landing and x not a single checker of
 // W.  A loop over the failing windows (usually one), no per-source loop.
+NARDE_FN uint32_t block_reject_w1(uint32_t O, uint32_t S1, uint32_t W, uint32_t C, int d) {
+  const uint32_t H = W & ~O;
+  const uint32_t stay = C & ~(W & S1);  // moving it does not open a hole in W
+  const uint32_t one = (H & (H - 1u)) == 0u ? (H << d) : 0u;  // landing on the one hole
+  return H == 0u ? stay : (stay & one & MASK24);
+}
 NARDE_FN uint32_t block_reject_w(uint32_t O, uint32_t S1, uint32_t fw, uint32_t C, int d) {
-  uint32_t rej = 0u;
-  for (uint32_t f = fw; f; f &= f - 1u) {
-    const uint32_t W = 0x3Fu << __builtin_ctz(f);
-    const uint32_t H = W & ~O;
-    const uint32_t stay = C & ~(W & S1);  // moving it does not open a hole in W
-    const uint32_t one = (H & (H - 1u)) == 0u ? (H << d) : 0u;  // landing on the one hole
-    rej |= H == 0u ? stay : (stay & one & MASK24);
-  }
+  // the lowest window outside the loop (usually the only one): no loop
+  // iteration's branches when there is one window
+  uint32_t rej = block_reject_w1(O, S1, (0x3Fu << (__builtin_ctz(fw | 0x80000000u) & 31)) & MASK24, C, d);
+  rej &= msk(fw != 0u);
+  for (uint32_t f = fw & (fw - 1u); f; f &= f - 1u) rej |= block_reject_w1(O, S1, 0x3Fu << __builtin_ctz(f), C, d);
   return rej;
 }
 
