@@ -173,6 +173,8 @@ def load_issue(full4, envs, plies, kernel_ms):
         return None
     if d.get("envs") != envs or d.get("plies") != plies or not d.get("valu_per_launch") or not kernel_ms:
         return None
+    if d.get("kernel", "") not in kernel_name(full4, plies):  # a summary of another kernel
+        return None
     achieved = d["valu_per_launch"] / (kernel_ms * 1e-3)
     return {
         "bound": "valu-issue",
@@ -205,13 +207,46 @@ def spawn_ranks(n, argv, cpu=None):
     exec), and rank 0's JSON line reaches our stdout.  `cpu`: the CPU
     baseline this process measured before starting them (rank 0 reports it
     instead of measuring it again)."""
+    port = _free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
     env = dict(os.environ)
+    env.pop(CPU_BASELINE_ENV, None)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL on this host driver)
     if cpu is not None:
-        env[CPU_BASELINE_ENV] = json.dumps(cpu)
+        # marked for this launch only: rank 0 accepts it when the marker's
+        # port is its MASTER_PORT and the marker's pid one of its ancestors
+        env[CPU_BASELINE_ENV] = json.dumps({"launcher_pid": os.getpid(), "master_port": port, "cpu": cpu})
     return subprocess.call(cmd, env=env)
+
+
+def _ancestors(depth=4):
+    """pids of this process's parent, grandparent, ... (Linux /proc)."""
+    out, pid = [], os.getpid()
+    for _ in range(depth):
+        try:
+            with open(f"/proc/{pid}/stat") as f:
+                pid = int(f.read().rsplit(")", 1)[1].split()[1])
+        except (OSError, ValueError, IndexError):
+            break
+        out.append(pid)
+    return out
+
+
+def handed_cpu_baseline():
+    """The CPU baseline spawn_ranks measured for THIS launch, or None: a
+    value inherited from an outer shell or another launch is ignored (and
+    then rank 0 measures its own)."""
+    raw = os.environ.get(CPU_BASELINE_ENV)
+    if not raw:
+        return None
+    try:
+        d = json.loads(raw)
+        ok = (str(d["master_port"]) == os.environ.get("MASTER_PORT")
+              and int(d["launcher_pid"]) in _ancestors())
+    except (ValueError, KeyError, TypeError):
+        return None
+    return d["cpu"] if ok else None
 
 
 def measure_cpu_baseline(args):
@@ -358,8 +393,9 @@ def main():
     # outside launcher the other ranks wait in the rendezvous meanwhile)
     cpu = None
     if rank_env == 0 and not args.no_cpu_baseline:
-        handed = os.environ.get(CPU_BASELINE_ENV)
-        cpu = json.loads(handed) if handed else measure_cpu_baseline(args)
+        cpu = handed_cpu_baseline()
+        if cpu is None:
+            cpu = measure_cpu_baseline(args)
 
     import torch
     import torch.distributed as dist

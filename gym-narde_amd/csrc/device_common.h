@@ -24,6 +24,17 @@ __device__ __forceinline__ void draw(const Rng& g, uint32_t t, uint32_t i, uint3
   philox4x32_10(t, g.env0 + i, 0u, stream, g.k0, g.k1, r);
 }
 
+// Hand-over of a wave's own LDS writes to other lanes of the same wave: the
+// LDS ops of one wave retire in issue order, so no hardware wait is needed,
+// but the wave barrier alone is not a memory fence in the IR -- the
+// wavefront-scope release/acquire pair makes the cross-lane read-after-write
+// explicit to the compiler (no instruction on gfx950).
+__device__ __forceinline__ void wave_lds_handoff() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // the four words of ply t of env i (narde_rules.h ply_words: one Philox
 // block per two plies; a kernel that runs consecutive plies keeps the block)
 __device__ __forceinline__ void ply_draw(const Rng& g, uint32_t t, uint32_t i, uint32_t r[4]) {

@@ -135,7 +135,7 @@ __global__ void __launch_bounds__(kBlock) k_tesauro198_rows(Planes pl, int n, fl
     for (int k = 0; k < 26; ++k)
       if (2 * k < nf) *reinterpret_cast<float2*>(row + c0 + 2 * k) = make_float2(f[2 * k], f[2 * k + 1]);
   }
-  __builtin_amdgcn_wave_barrier();  // the wave reads only its own rows: LDS ops of one wave retire in issue order
+  wave_lds_handoff();  // the wave reads only its own rows
   // the wave's rows: [e0, min(e0 + 16, n)) -> 16-B pieces, lane-major
   const int rows_here = max(0, min(kTesEnvs, n - e0));
   const uint32_t bytes = (uint32_t)rows_here * kTesRowB;

@@ -105,11 +105,11 @@ __device__ __forceinline__ void store_obs_wave(int32_t* __restrict__ obs, size_t
   lds[lane * 6 + 3] = obs_quad<3>(s);
   lds[lane * 6 + 4] = obs_quad<4>(s);
   lds[lane * 6 + 5] = obs_quad<5>(s);
-  __builtin_amdgcn_wave_barrier();  // LDS ops of one wave retire in issue order
+  wave_lds_handoff();
   int4* dst = reinterpret_cast<int4*>(obs + (ix - lane) * 24);
 #pragma unroll
   for (int q = 0; q < 6; ++q) st_out(dst + q * 64 + lane, lds[q * 64 + lane]);
-  __builtin_amdgcn_wave_barrier();
+  wave_lds_handoff();  // the slice's next writes stay behind these reads
 }
 
 // obs rows through the wave's LDS slice (whole 1-KiB store instructions) or

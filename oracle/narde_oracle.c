@@ -73,10 +73,12 @@ int or_violates_block_rule(const int32_t *board) {
     return 0;
 }
 
-/* narde.py:58-92 (+ :94-106 and :127-137).  roll has n <= 4 dice. */
-int or_get_valid_moves(const int32_t *abs_board, int ft_w, int ft_b,
-                       const int32_t *roll_in, int n, int player,
-                       int32_t (*out)[2]) {
+/* narde.py:58-92 (+ :94-106 and :127-137).  roll has n <= 4 dice.
+ * grp (optional): for each returned entry, the index into the sorted roll of
+ * the die whose loop iteration (narde.py:64) produced it. */
+static int or_get_valid_moves_g(const int32_t *abs_board, int ft_w, int ft_b,
+                                const int32_t *roll_in, int n, int player,
+                                int32_t (*out)[2], int8_t *grp) {
     int32_t roll[4];
     for (int i = 0; i < n; ++i) roll[i] = roll_in[i];
     /* sorted(roll, reverse=True): insertion sort, descending */
@@ -89,6 +91,7 @@ int or_get_valid_moves(const int32_t *abs_board, int ft_w, int ft_b,
     else or_rotate_board(abs_board, board);
 
     int32_t moves[OR_MAXM * 2][2];
+    int8_t mg[OR_MAXM * 2];
     int nm = 0;
     for (int di = 0; di < n; ++di) {
         int die = roll[di];
@@ -96,23 +99,24 @@ int or_get_valid_moves(const int32_t *abs_board, int ft_w, int ft_b,
             if (board[pos] <= 0) continue;
             int np_ = pos - die;
             if (np_ >= 0 && np_ < 24) {
-                if (board[np_] >= 0) { moves[nm][0] = pos; moves[nm][1] = np_; nm++; }
+                if (board[np_] >= 0) { moves[nm][0] = pos; moves[nm][1] = np_; mg[nm] = (int8_t)di; nm++; }
             } else if (np_ < 0) {
                 int32_t s = 0;
                 for (int k = 6; k < 24; ++k) s += board[k] > 0 ? board[k] : 0;
-                if (s == 0 && die >= pos + 1) { moves[nm][0] = pos; moves[nm][1] = OR_OFF; nm++; }
+                if (s == 0 && die >= pos + 1) { moves[nm][0] = pos; moves[nm][1] = OR_OFF; mg[nm] = (int8_t)di; nm++; }
             }
         }
     }
     /* block-rule filter (narde.py:78-89) */
     int32_t filt[OR_MAXM * 2][2];
+    int8_t fg[OR_MAXM * 2];
     int nf = 0;
     for (int m = 0; m < nm; ++m) {
         int32_t bc[24];
         memcpy(bc, board, sizeof bc);
         bc[moves[m][0]] -= 1;
         if (moves[m][1] != OR_OFF) bc[moves[m][1]] += 1;
-        if (!or_violates_block_rule(bc)) { filt[nf][0] = moves[m][0]; filt[nf][1] = moves[m][1]; nf++; }
+        if (!or_violates_block_rule(bc)) { filt[nf][0] = moves[m][0]; filt[nf][1] = moves[m][1]; fg[nf] = mg[m]; nf++; }
     }
     /* _validate_head_moves: sorted(roll) in [[3,3],[4,4],[6,6]] */
     int first_turn = player == 1 ? ft_w : ft_b;
@@ -123,12 +127,35 @@ int or_get_valid_moves(const int32_t *abs_board, int ft_w, int ft_b,
     int cnt = 0, head = 0;
     for (int m = 0; m < nf; ++m) {
         if (filt[m][0] == 23) {
-            if (head < max_head) { out[cnt][0] = filt[m][0]; out[cnt][1] = filt[m][1]; cnt++; head++; }
+            if (head < max_head) {
+                if (grp) grp[cnt] = fg[m];
+                out[cnt][0] = filt[m][0]; out[cnt][1] = filt[m][1]; cnt++; head++;
+            }
         } else {
+            if (grp) grp[cnt] = fg[m];
             out[cnt][0] = filt[m][0]; out[cnt][1] = filt[m][1]; cnt++;
         }
     }
     return cnt;
+}
+
+int or_get_valid_moves(const int32_t *abs_board, int ft_w, int ft_b,
+                       const int32_t *roll_in, int n, int player,
+                       int32_t (*out)[2]) {
+    return or_get_valid_moves_g(abs_board, ft_w, ft_b, roll_in, n, player, out, NULL);
+}
+
+/* The build's compact form of a two-dice list,
+ * computed from the list itself: bit `from` of word 0 for an entry of the
+ * higher die's loop, of word 1 for the lower die's (grp from
+ * or_get_valid_moves_g), | d_hi<<48 | d_lo<<52.  The decoding (entries in
+ * die-major, ascending-source order, to = from - die or 'off') reproduces
+ * the list exactly, so equal words are equal lists. */
+static uint64_t or_compact2(const int32_t (*list)[2], const int8_t *grp, int cnt, const int32_t dice[2]) {
+    uint32_t L[2] = {0u, 0u};
+    for (int k = 0; k < cnt; ++k) L[grp[k]] |= 1u << list[k][0];
+    uint32_t hi = dice[0] > dice[1] ? dice[0] : dice[1], lo = dice[0] > dice[1] ? dice[1] : dice[0];
+    return (uint64_t)L[0] | ((uint64_t)L[1] << 24) | ((uint64_t)hi << 48) | ((uint64_t)lo << 52);
 }
 
 /* narde.py:108-125 */
@@ -192,6 +219,7 @@ typedef struct {
     int32_t list2[OR_MAXM][2];
     int32_t roll2;
     int32_t code1, code2; /* actions actually used (policy mode) */
+    uint64_t legal1;      /* or_compact2 of list1 */
 } or_step_out;
 
 /*
@@ -204,8 +232,10 @@ static void or_step_core(or_state *s, const int32_t dice[2], int code1, int code
                          int policy, uint32_t r1, uint32_t r2, or_step_out *o) {
     o->count2 = -1;
     o->roll2 = 0;
-    int n1 = or_get_valid_moves(s->board, s->ft_w, s->ft_b, dice, 2, s->player, o->list1);
+    int8_t g1[OR_MAXM];
+    int n1 = or_get_valid_moves_g(s->board, s->ft_w, s->ft_b, dice, 2, s->player, o->list1, g1);
     o->count1 = n1;
+    o->legal1 = or_compact2((const int32_t (*)[2])o->list1, g1, n1, dice);
     if (policy) {
         code1 = 0; code2 = 0;
         if (n1 >= 2) {
@@ -318,7 +348,8 @@ void or_apply_batch(int64_t n, int8_t *board, uint8_t *off, uint8_t *ft,
 void or_step_batch(int64_t n, int8_t *board, uint8_t *off, uint8_t *ft, int8_t *player,
                    const uint8_t *dice, const int16_t *action,
                    int8_t *obs, int8_t *reward, uint8_t *terminated,
-                   int8_t *list1, int16_t *count1, int8_t *list2, int16_t *count2, uint8_t *roll2) {
+                   int8_t *list1, int16_t *count1, int8_t *list2, int16_t *count2, uint8_t *roll2,
+                   uint64_t *legal1) {
     for (int64_t i = 0; i < n; ++i) {
         or_state s;
         or_step_out o;
@@ -340,6 +371,7 @@ void or_step_batch(int64_t n, int8_t *board, uint8_t *off, uint8_t *ft, int8_t *
             count2[i] = (int16_t)o.count2;
             roll2[i] = (uint8_t)o.roll2;
         }
+        if (legal1) legal1[i] = o.legal1;
     }
 }
 
@@ -586,7 +618,8 @@ void or_reset_batch(int64_t n, int64_t env0, uint64_t seed, uint32_t epoch,
  * Run `plies` lockstep plies t0..t0+plies-1 of random-legal self-play over n
  * envs.  Per-ply outputs (optional, NULL to skip) are [plies][n][...]:
  * obs int8[24] (next mover's perspective, after auto-reset), reward,
- * terminated, truncated, dice[2], action codes[2], count1.
+ * terminated, truncated, dice[2], action codes[2], count1, legal1 (list #1
+ * in the build's compact form, or_compact2).
  * stats[n][3] accumulates {games, white points, black points}.
  */
 void or_selfplay(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int plies,
@@ -594,7 +627,7 @@ void or_selfplay(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int plies,
                  int8_t *board, uint8_t *off, uint8_t *ft, int8_t *player, uint16_t *elapsed,
                  int32_t *stats,
                  int8_t *obs, int8_t *reward, uint8_t *terminated, uint8_t *truncated,
-                 uint8_t *dice_out, int16_t *action_out, int16_t *count1_out) {
+                 uint8_t *dice_out, int16_t *action_out, int16_t *count1_out, uint64_t *legal_out) {
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
     for (int64_t i = 0; i < n; ++i) {
         or_state s;
@@ -630,6 +663,7 @@ void or_selfplay(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int plies,
             if (dice_out) { dice_out[ix * 2] = (uint8_t)d[0]; dice_out[ix * 2 + 1] = (uint8_t)d[1]; }
             if (action_out) { action_out[ix * 2] = (int16_t)o.code1; action_out[ix * 2 + 1] = (int16_t)o.code2; }
             if (count1_out) count1_out[ix] = (int16_t)o.count1;
+            if (legal_out) legal_out[ix] = o.legal1;
         }
         store_state(&s, board + i * 24, off + i * 2, ft + i * 2, player + i);
         elapsed[i] = (uint16_t)s.elapsed;

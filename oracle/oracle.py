@@ -96,12 +96,13 @@ def step(board, off, ft, player, dice, action, with_lists=True):
         roll2 = np.empty(n, np.uint8)
     else:
         list1 = list2 = count1 = count2 = roll2 = None
+    legal1 = np.empty(n, np.uint64)
     lib().or_step_batch(ctypes.c_int64(n), _p(board), _p(off), _p(ft), _p(player), _p(dice),
                         _p(action), _p(obs), _p(reward), _p(term), _p(list1), _p(count1),
-                        _p(list2), _p(count2), _p(roll2))
+                        _p(list2), _p(count2), _p(roll2), _p(legal1))
     return dict(board=board, off=off, first_turn=ft, player=player, obs=obs, reward=reward,
                 terminated=term, list1=list1, count1=count1, list2=list2, count2=count2,
-                roll2=roll2)
+                roll2=roll2, legal1=legal1)
 
 
 def full4_turn(board, off, ft, player, dice, words):
@@ -123,6 +124,35 @@ def full4_turn(board, off, ft, player, dice, words):
                          _p(played), _p(reward), _p(done))
     return dict(board=board, off=off, first_turn=ft, max_dice=M, cmask=cm, played=played,
                 reward=reward, done=done)
+
+
+def expand_compact(words):
+    """Compact two-dice legal words (u64[N]) -> (moves int8[N,64,2] padded with
+    -1, count int16[N]) in the reference's list order: the higher die's
+    entries, then the lower die's, ascending source, to = from - die or 24
+    ('off').  Vectorised (numpy); the inverse of or_compact2."""
+    w = np.ascontiguousarray(words, dtype=np.uint64).reshape(-1)
+    n = w.shape[0]
+    pos = np.arange(24, dtype=np.uint64)
+    Lh = ((w[:, None] >> pos) & np.uint64(1)).astype(bool)
+    Ll = ((w[:, None] >> (pos + np.uint64(24))) & np.uint64(1)).astype(bool)
+    dh = ((w >> np.uint64(48)) & np.uint64(0xF)).astype(np.int16)
+    dl = ((w >> np.uint64(52)) & np.uint64(0xF)).astype(np.int16)
+    bits = np.concatenate([Lh, Ll], axis=1)                      # [N, 48] group-major
+    src = np.tile(np.arange(24, dtype=np.int16), 2)[None, :]      # [1, 48]
+    die = np.concatenate([np.repeat(dh[:, None], 24, 1), np.repeat(dl[:, None], 24, 1)], 1)
+    dst = src - die
+    dst = np.where(dst < 0, OFF, dst)
+    order = np.argsort(~bits, axis=1, kind="stable")             # set bits first, in order
+    cnt = bits.sum(1).astype(np.int16)
+    rows = np.arange(n)[:, None]
+    f = np.broadcast_to(src, (n, 48))[rows, order]
+    t = dst[rows, order]
+    keep = np.arange(48)[None, :] < cnt[:, None]
+    moves = np.full((n, MAXM, 2), -1, np.int8)
+    moves[:, :48, 0] = np.where(keep, f, -1)
+    moves[:, :48, 1] = np.where(keep, t, -1)
+    return moves, cnt
 
 
 def tesauro198(board, off, player):
@@ -173,17 +203,20 @@ class SelfPlay:
             dice = np.empty((plies, n, 2), np.uint8)
             action = np.empty((plies, n, 2), np.int16)
             count1 = np.empty((plies, n), np.int16)
+            legal = np.empty((plies, n), np.uint64)
         else:
-            obs = reward = term = trunc = dice = action = count1 = None
+            obs = reward = term = trunc = dice = action = count1 = legal = None
         lib().or_selfplay(ctypes.c_int64(n), ctypes.c_int64(self.env0), ctypes.c_uint64(self.seed),
                           ctypes.c_uint32(self.t), ctypes.c_int(plies), ctypes.c_int(self.dice_mode),
                           ctypes.c_int(self.max_steps), _p(self.board), _p(self.off), _p(self.ft),
                           _p(self.player), _p(self.elapsed), _p(self.stats), _p(obs), _p(reward),
-                          _p(term), _p(trunc), _p(dice), _p(action), _p(count1))
+                          _p(term), _p(trunc), _p(dice), _p(action), _p(count1), _p(legal))
         self.t += plies
         if record:
+            # legal: list #1 of each ply in the build's compact form, built by
+            # the oracle from its own list (or_compact2)
             return dict(obs=obs, reward=reward, terminated=term, truncated=trunc, dice=dice,
-                        action=action, count1=count1)
+                        action=action, count1=count1, legal=legal)
         return None
 
 

@@ -64,7 +64,7 @@ class HostVecEnv:
                              ctypes.c_uint32(self.t), ctypes.c_int(plies), ctypes.c_int(0),
                              ctypes.c_int(self.max_steps), _p(self.board), _p(self.off), _p(self.ft),
                              _p(self.player), _p(self.elapsed), _p(self.stats),
-                             None, None, None, None, None, None, None)
+                             None, None, None, None, None, None, None, None)
         self.t += plies
         return bufs
 

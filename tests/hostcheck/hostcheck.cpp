@@ -143,10 +143,16 @@ void hc_reset_batch(int64_t n, int64_t env0, uint64_t seed, uint32_t epoch, int8
   }
 }
 
+// the compact list-#1 word the rollouts store (kernels_state.h compact_legal)
+static uint64_t compact2(const Legal& l) {
+  return (uint64_t)l.L[0] | ((uint64_t)l.L[1] << 24) | ((uint64_t)l.d[0] << 48) | ((uint64_t)l.d[1] << 52);
+}
+
 void hc_selfplay(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int plies, int dice_mode,
                  int max_steps, int8_t* board, uint8_t* off, uint8_t* ft, int8_t* player,
                  uint16_t* elapsed, int32_t* stats, int8_t* obs, int8_t* reward, uint8_t* term,
-                 uint8_t* trunc, uint8_t* dice_out, int16_t* action_out, int16_t* count1_out) {
+                 uint8_t* trunc, uint8_t* dice_out, int16_t* action_out, int16_t* count1_out,
+                 uint64_t* legal_out) {
   for (int64_t i = 0; i < n; ++i) {
     Side s = load(board + i * 24, off + 2 * i, ft + 2 * i, player[i], elapsed[i]);
     int4 st = make_int4(0, 0, 0, 0);
@@ -167,6 +173,7 @@ void hc_selfplay(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int plies,
       if (dice_out) { dice_out[2 * ix] = (uint8_t)d0; dice_out[2 * ix + 1] = (uint8_t)d1; }
       if (action_out) { action_out[2 * ix] = (int16_t)o.code1; action_out[2 * ix + 1] = (int16_t)o.code2; }
       if (count1_out) count1_out[ix] = (int16_t)o.l1.count;
+      if (legal_out) legal_out[ix] = compact2(o.l1);
     }
     stats[3 * i] += st.x;
     stats[3 * i + 1] += st.y;
@@ -244,7 +251,8 @@ void hc_selfplay_full(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int p
 void hc_selfplay_sl(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int plies, int dice_mode,
                     int max_steps, int8_t* board, uint8_t* off, uint8_t* ft, int8_t* player,
                     uint16_t* elapsed, int32_t* stats, int8_t* obs, int8_t* reward, uint8_t* term,
-                    uint8_t* trunc, uint8_t* dice_out, int16_t* action_out, int16_t* count1_out) {
+                    uint8_t* trunc, uint8_t* dice_out, int16_t* action_out, int16_t* count1_out,
+                    uint64_t* legal_out) {
   for (int64_t i = 0; i < n; ++i) {
     Side s = load(board + i * 24, off + 2 * i, ft + 2 * i, player[i], elapsed[i]);
     int4 st = make_int4(0, 0, 0, 0);
@@ -265,6 +273,7 @@ void hc_selfplay_sl(int64_t n, int64_t env0, uint64_t seed, uint32_t t0, int pli
       if (dice_out) { dice_out[2 * ix] = (uint8_t)d0; dice_out[2 * ix + 1] = (uint8_t)d1; }
       if (action_out) { action_out[2 * ix] = (int16_t)o.code1; action_out[2 * ix + 1] = (int16_t)o.code2; }
       if (count1_out) count1_out[ix] = (int16_t)o.l1.count;
+      if (legal_out) legal_out[ix] = compact2(o.l1);
     }
     stats[3 * i] += st.x;
     stats[3 * i + 1] += st.y;

@@ -41,7 +41,7 @@ def _shard_selfplay(lib, first, per):
                        P(b), P(off), P(ft), P(pl), P(el))
     lib.hc_selfplay(ctypes.c_int64(per), ctypes.c_int64(first), ctypes.c_uint64(SEED), ctypes.c_uint32(0),
                     ctypes.c_int(PLIES), ctypes.c_int(0), ctypes.c_int(1000), P(b), P(off), P(ft), P(pl), P(el),
-                    P(st), None, None, None, None, None, None, None)
+                    P(st), None, None, None, None, None, None, None, None)
     return st
 
 

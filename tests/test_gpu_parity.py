@@ -46,8 +46,10 @@ def test_legal_moves_golden():
     from gym_narde.vector import decode_compact
 
     c = np_(compact).view(np.uint64)
-    two = np.nonzero(d["nroll"] == 2)[0][:3000]
-    for i in two:
+    two = np.nonzero(d["nroll"] == 2)[0]
+    m2, c2 = O.expand_compact(c[two])  # every two-dice case, entry by entry
+    assert np.array_equal(c2, d["count"][two]) and np.array_equal(m2, d["moves"][two])
+    for i in two[:200]:  # the product's own decoder agrees
         ref = [(int(f), "off" if t == 24 else int(t)) for f, t in d["moves"][i][: d["count"][i]]]
         assert decode_compact(c[i]) == ref, i
 
@@ -67,12 +69,14 @@ def test_step_golden():
     assert np.array_equal(np_(st["off"]), s["post_off"])
     assert np.array_equal(np_(st["first_turn"]), s["post_first_turn"])
     assert np.array_equal(np_(st["player"]), s["post_player"])
-    from gym_narde.vector import decode_compact
-
+    # list #1 of all 44,004 golden steps, entry by entry (vectorised expansion
+    # of the compact words), and the words equal the oracle's own (or_compact2)
     c = np_(info["legal"]).view(np.uint64)
-    for i in np.random.RandomState(0).choice(n, 3000, replace=False):
-        ref = [(int(f), "off" if t == 24 else int(t)) for f, t in s["list1"][i][: s["count1"][i]]]
-        assert decode_compact(c[i]) == ref, i
+    moves, count = O.expand_compact(c)
+    assert np.array_equal(count, s["count1"])
+    assert np.array_equal(moves, s["list1"])
+    ref = O.step(s["board"], s["off"], s["first_turn"], s["player"], s["dice"], s["action"], with_lists=False)
+    assert np.array_equal(c, ref["legal1"])
 
 
 def test_apply_golden():
@@ -118,10 +122,7 @@ def test_selfplay_trajectory_vs_oracle(dice_mode, max_steps):
         assert np.array_equal(np_(term), rec["terminated"][p]), p
         assert np.array_equal(np_(trunc), rec["truncated"][p]), p
         assert np.array_equal(np_(info["actions"]), rec["action"][p]), p
-        c = np_(info["legal"]).view(np.uint64)
-        cnt = np.array([bin(int(x) & 0xFFFFFF).count("1") + bin((int(x) >> 24) & 0xFFFFFF).count("1")
-                        for x in c])
-        assert np.array_equal(cnt, rec["count1"][p]), p
+        assert np.array_equal(np_(info["legal"]).view(np.uint64), rec["legal"][p]), p
     st = env.get_state()
     assert np.array_equal(np_(st["board"]), ref.board)
     assert np.array_equal(np_(st["elapsed"]).view(np.uint16), ref.elapsed)
@@ -177,9 +178,8 @@ def test_rollout_vs_oracle_and_step(n):
         assert np.array_equal(np_(bufs["terminated"]), rec["terminated"])
         assert np.array_equal(np_(bufs["truncated"]), rec["truncated"])
         assert np.array_equal(np_(bufs["actions"]), rec["action"])
-        lg = np_(bufs["legal"]).view(np.uint64)
-        cnt = (np.vectorize(lambda x: bin(int(x) & 0xFFFFFFFFFFFF).count("1"))(lg)).astype(np.int16)
-        assert np.array_equal(cnt, rec["count1"])
+        # list #1 of every ply against the oracle's own list, word for word
+        assert np.array_equal(np_(bufs["legal"]).view(np.uint64), rec["legal"])
     assert np.array_equal(np_(env.stats()), ref.stats)
     assert env.ply == 320
 
@@ -273,8 +273,8 @@ def test_full_batch_subset_and_invariants():
 def test_bench_launch_window_and_invariants():
     """The launches bench.py times (k_rollout_pc<true, *>: B = 65,536, 1,000
     plies, every output), then a 100-ply one and the driver's 20-ply one
-    (non-temporal stores): a 2,048-env window of every
-    output equals the oracle on those global ids; over the whole batch the
+    (non-temporal stores): a 2,048-env window of every output -- the legal
+    sets included -- equals the oracle on those global ids; over the whole batch the
     outputs obey the rules' invariants (at most 15 checkers a side, reward
     only on a finished game (1 or 2), no truncation: no random game lasts
     1,000 plies)."""
@@ -292,6 +292,9 @@ def test_bench_launch_window_and_invariants():
         assert np.array_equal(np_(bufs["terminated"][:, sl]), rec["terminated"])
         assert np.array_equal(np_(bufs["truncated"][:, sl]), rec["truncated"])
         assert np.array_equal(np_(bufs["actions"][:, sl]), rec["action"])
+        # the metric's "legal-move bit-exact vs CPU": list #1 of every ply of the
+        # window, word for word against the oracle's (or_compact2 of its list)
+        assert np.array_equal(np_(bufs["legal"][:, sl]).view(np.uint64), rec["legal"])
         obs = bufs["obs"]
         assert int(obs.abs().max()) <= 15
         assert bool((obs.clamp(min=0).sum(-1) <= 15).all()) and bool(((-obs).clamp(min=0).sum(-1) <= 15).all())

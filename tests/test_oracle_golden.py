@@ -78,6 +78,27 @@ def test_oracle_step_golden():
     assert (s["ncalls"] == 2).any()
 
 
+def test_oracle_compact_legal_is_the_reference_list():
+    """The oracle's compact list-#1 word (or_compact2, built from its own list
+    and the die loop each entry came from) expands back to the reference's
+    list #1 for every golden step, entry by entry: comparing the device's
+    compact words with the oracle's is comparing the lists themselves."""
+    s = golden("steps.npz")
+    r = O.step(s["board"], s["off"], s["first_turn"], s["player"], s["dice"], s["action"])
+    moves, count = O.expand_compact(r["legal1"])
+    assert np.array_equal(count, s["count1"])
+    assert np.array_equal(moves, s["list1"])
+    # the self-play driver records the same word
+    sp = O.SelfPlay(512, seed=77)
+    sp.reset(0)
+    rec = sp.run(300)
+    m, c = O.expand_compact(rec["legal"])
+    assert np.array_equal(c.reshape(300, 512), rec["count1"])
+    # doubles lists (duplicate entries, the head filter on the second die) are covered
+    dice = rec["dice"]
+    assert ((dice[..., 0] == dice[..., 1]) & (rec["count1"] >= 2)).any()
+
+
 def _port_state(b, off, ft, pl):
     e = port.PortEnv()
     g = e.game
@@ -156,7 +177,7 @@ def test_hostcheck_step_golden(hostcheck):
 def test_hostcheck_selfplay_vs_oracle(hostcheck, dice_mode, fn, max_steps):
     """The host build of the device's REF2 ply -- env_ply, and the rollouts'
     straight-line env_ply_policy_sl (round 4) -- equals the oracle's
-    self-play on every per-ply output."""
+    self-play on every per-ply output, the compact list-#1 words included."""
     n, plies, seed, env0 = 512, 400, 0xDEADBEEF12345, 1000
     sp = O.SelfPlay(n, seed=seed, env0=env0, dice_mode=dice_mode, max_steps=max_steps)
     sp.reset(0)
@@ -174,7 +195,7 @@ def test_hostcheck_selfplay_vs_oracle(hostcheck, dice_mode, fn, max_steps):
                           ctypes.c_uint32(0), ctypes.c_int(plies), ctypes.c_int(dice_mode),
                           ctypes.c_int(max_steps), P(b), P(off), P(ft), P(pl), P(el), P(st),
                           P(out["obs"]), P(out["reward"]), P(out["terminated"]), P(out["truncated"]),
-                          P(out["dice"]), P(out["action"]), P(out["count1"]))
+                          P(out["dice"]), P(out["action"]), P(out["count1"]), P(out["legal"]))
     for k in ro:
         assert np.array_equal(out[k], ro[k]), k
     assert np.array_equal(st, sp.stats) and np.array_equal(b, sp.board)

@@ -32,3 +32,42 @@ def test_roofline_check_recomputes_a_line(tmp_path):
     line["roofline"]["frac"] = round(frac * 1.1, 5)
     p.write_text(json.dumps(line) + "\n")
     assert _run(str(p)).returncode == 1
+
+
+def test_summaries_apply_only_to_their_kernel():
+    """A PMC/SQ summary of another kernel (e.g. the retired k_rollout_full<true>)
+    is never combined with a launch's timings, in bench.py and in the checker
+    alike."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    sys.path.insert(0, ROOT)
+    import bench
+    import roofline_check as rc
+
+    for full in (False, True):
+        for plies in (1, 20, 32, 33, 1000):
+            assert rc.launched_kernel(full, plies) == bench.kernel_name(full, plies)
+    k = bench.kernel_name(True, 20)
+    assert rc.matches({"envs": 65536, "plies": 20, "kernel": "k_rollout_wave"}, 65536, 20, k)
+    assert not rc.matches({"envs": 65536, "plies": 20, "kernel": "k_rollout_full<true>"}, 65536, 20, k)
+    assert not rc.matches({"envs": 65536, "plies": 20, "kernel": "k_rollout_pc"}, 65536, 20, k)
+
+
+def test_cpu_baseline_handover_needs_this_launchs_marker(monkeypatch):
+    """bench.py rank 0 takes a handed-over CPU baseline only when the marker
+    names its own MASTER_PORT and an ancestor pid."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    cpu = {"value": 1.0}
+    monkeypatch.setenv("MASTER_PORT", "29611")
+    monkeypatch.setenv(bench.CPU_BASELINE_ENV, json.dumps(cpu))  # unmarked: an outer shell's
+    assert bench.handed_cpu_baseline() is None
+    mark = {"launcher_pid": os.getppid(), "master_port": 29611, "cpu": cpu}
+    monkeypatch.setenv(bench.CPU_BASELINE_ENV, json.dumps(mark))
+    assert bench.handed_cpu_baseline() == cpu
+    monkeypatch.setenv("MASTER_PORT", "29612")  # another launch
+    assert bench.handed_cpu_baseline() is None
+    mark["launcher_pid"] = 1 << 30  # not an ancestor
+    monkeypatch.setenv("MASTER_PORT", "29611")
+    monkeypatch.setenv(bench.CPU_BASELINE_ENV, json.dumps(mark))
+    assert bench.handed_cpu_baseline() is None

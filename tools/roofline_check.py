@@ -33,15 +33,30 @@ def profile(name):
         return None
 
 
+def launched_kernel(full, plies):
+    """The kernel a launch of this shape runs (bench.py kernel_name)."""
+    if not full:
+        return "k_rollout_pc<true, true>" if plies <= 32 else "k_rollout_pc<true, false>"
+    return "k_rollout_wave<true>"
+
+
+def matches(summary, envs, plies, kernel):
+    """A PMC/SQ summary applies only if it was measured at this shape on this
+    kernel (its `kernel` filter is a prefix of the launched kernel's name)."""
+    return (summary is not None and summary.get("envs") == envs and summary.get("plies") == plies
+            and summary.get("kernel", "") in kernel)
+
+
 def check(label, full, envs, plies, kernel_ms, line_frac, line_issue):
     nbytes = bytes_per_launch(envs, plies, full)
     frac = nbytes / (kernel_ms * 1e-3) / HBM_PEAK
     stem = "k_rollout_full" if full else "k_rollout"
+    kernel = launched_kernel(full, plies)
     pmc = profile(f"pmc_{stem}_p{plies}.json") or profile(f"pmc_{stem}.json")
-    traffic = pmc["hbm_bytes_per_launch"] if pmc and pmc.get("plies") == plies and pmc.get("envs") == envs else None
+    traffic = pmc["hbm_bytes_per_launch"] if matches(pmc, envs, plies, kernel) else None
     sq = profile(f"sq_{stem}_p{plies}.json")
     issue = None
-    if sq and sq.get("envs") == envs and sq.get("plies") == plies:
+    if matches(sq, envs, plies, kernel):
         issue = sq["valu_per_launch"] / (kernel_ms * 1e-3) / ISSUE_PEAK
     out = {"leg": label, "rules": "full4" if full else "ref2", "plies": plies, "kernel_ms": kernel_ms,
            "hbm_frac": round(frac, 5), "line_hbm_frac": line_frac,
