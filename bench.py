@@ -134,11 +134,11 @@ def cpu_baseline(seconds, cores, how):
 
 def kernel_name(full4, plies):
     """The kernel narde_rollout[_full] launches for this shape (narde.hip):
-    REF2 stores non-temporally up to 32 plies per launch (kPcNtMaxPlies);
-    FULL4 takes k_rollout_wave (one wave per 64 envs) at every length."""
-    if not full4:
-        return "k_rollout_pc<true, true>" if plies <= 32 else "k_rollout_pc<true, false>"
-    return "k_rollout_wave<true>"
+    both store non-temporally up to 32 plies per launch (kPcNtMaxPlies);
+    REF2 is the producer/consumer workgroup k_rollout_pc, FULL4 the pairwise
+    producer/consumer k_rollout_pp_full."""
+    nt = "true" if plies <= 32 else "false"
+    return f"k_rollout_pc<true, {nt}>" if not full4 else f"k_rollout_pp_full<true, {nt}>"
 
 
 def load_traffic(path, envs, plies, kernel):
@@ -496,8 +496,10 @@ def main():
         gather = lambda: D.gather_total_rows(rows_buf)  # noqa: E731
         gather_impl = "ProcessGroup all_gather_into_tensor"
         if dist.get_backend() == "nccl":
-            # RcclGather agrees across ranks at every stage: it either builds
-            # on every rank or raises on every rank, so the fallback is common
+            # RcclGather agrees across ranks at every stage: when every rank's
+            # RCCL calls return, it either builds on every rank or raises on
+            # every rank, so the fallback is common (an init that never
+            # returns on some rank ends with the launcher's timeout)
             try:
                 rccl = D.RcclGather(rows_buf)
                 gather, gather_impl = rccl, "ncclAllGather (RCCL C API, launching stream)"

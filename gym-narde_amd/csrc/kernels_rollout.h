@@ -218,13 +218,13 @@ __device__ __forceinline__ void ply_free_turn(Side& s, int dh, int dl, uint32_t 
   turn_moves_sl(s, dh, dl, Ch, Cl, M, hl0, w, b2, fw, flip_always, o);
 }
 
-__device__ __forceinline__ void ply_policy_full(Side& s, int4& st, const Rng& g, uint32_t i, int max_steps,
-                                                bool autoreset, TurnOut& o, int& term, int& trunc,
-                                                uint32_t R[4], int p, int par) {
-  uint32_t r[4];
-  ply_draw_wave(g, s.t, i, R, p, par, r);
+// the ply with its words r already drawn (ply_words); every lane of the wave
+// must call it
+__device__ __forceinline__ void ply_full_words(Side& s, int4& st, const uint32_t r[4], int dice_mode,
+                                               int max_steps, bool autoreset, TurnOut& o, int& term,
+                                               int& trunc) {
   int d0, d1;
-  dice_from(r[0], g.dice_mode, d0, d1);
+  dice_from(r[0], dice_mode, d0, d1);
   const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
   const uint32_t low = block_lowmask(s.P);
   uint32_t fw;
@@ -244,6 +244,14 @@ __device__ __forceinline__ void ply_policy_full(Side& s, int4& st, const Rng& g,
   }
   if (autoreset) ply_close_sl(s, st, o.term, o.reward, mover_black, r[3], max_steps, term, trunc);
   else ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, false, term, trunc);
+}
+
+__device__ __forceinline__ void ply_policy_full(Side& s, int4& st, const Rng& g, uint32_t i, int max_steps,
+                                                bool autoreset, TurnOut& o, int& term, int& trunc,
+                                                uint32_t R[4], int p, int par) {
+  uint32_t r[4];
+  ply_draw_wave(g, s.t, i, R, p, par, r);
+  ply_full_words(s, st, r, g.dice_mode, max_steps, autoreset, o, term, trunc);
 }
 
 // one FULL4 ply (a whole turn per step), the turn
@@ -455,7 +463,8 @@ __device__ __forceinline__ void pc_put(PcLds& L, int slot, int k, int le, const 
 // obs quad qq (points 4qq .. 4qq + 3) of workgroup-local env le from the ply
 // results in LDS: only the two words it needs -- own word wi is dword wi of
 // nib0, opponent word wi is dword 3 of nib0 or wi - 1 of nib1
-__device__ __forceinline__ int4 pc_obs_quad(const PcLds& L, int slot, int k, int le, int qq) {
+template <class Lds>
+__device__ __forceinline__ int4 pc_obs_quad(const Lds& L, int slot, int k, int le, int qq) {
   const int wi = qq >> 1, sh = (qq & 1) * 16;
   const uint32_t* n0w = reinterpret_cast<const uint32_t*>(&L.nib0[slot][k][le]);
   const uint32_t* n1w = reinterpret_cast<const uint32_t*>(&L.nib1[slot][k][le]);
@@ -669,6 +678,368 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
     pl.p1[i] = rb;
     cum = stats_after(pl.stats, i, st, out.totals != nullptr);
   }
+  if (out.totals) wg_totals(cum, out.totals);
+}
+
+
+// ---------------------------------------------------------------------------
+// k_rollout_pc_full: the FULL4 rollout (whole turns)
+// in k_rollout_pc's producer/consumer shape.  Waves 0-3 play the turns
+// (ply_full_words, wave-cooperative: every lane of a producer wave plays,
+// lanes past n on a dummy state) with the record in VGPRs; waves 4-7 draw
+// the next block's Philox words and store the previous block's outputs,
+// every wave-wide obs store one contiguous 1 KiB.  The one-wave kernel
+// (k_rollout_wave) stores its own 96-B obs rows and draws its own words, and
+// those stores stall its turn: with no turn at all it still took 0.208 ms
+// per 100 plies of 20-ply launches.
+struct PcFullLds {
+  uint2 draw[kPcSlots][kPcR][kPcEnvs];     // the ply's (wa, wb) per env and ply
+  uint4 nib0[kPcSlots][kPcR][kPcEnvs];     // {own w0, own w1, own w2, opp w0} (next mover's view)
+  uint2 nib1[kPcSlots][kPcR][kPcEnvs];     // {opp w1, opp w2}
+  uint2 legal[kPcSlots][kPcR][kPcEnvs];    // C_0 word (lo, hi)
+  uint2 played[kPcSlots][kPcR][kPcEnvs];   // played sub-moves word (lo, hi)
+  uint32_t rtt[kPcSlots][kPcR][kPcEnvs];   // reward | term << 8 | trunc << 16
+};
+
+__device__ __forceinline__ void pc_put_full(PcFullLds& L, int slot, int k, int le, const Side& s,
+                                            const TurnOut& o, int term, int trunc) {
+  L.nib0[slot][k][le] = make_uint4(s.own.w[0], s.own.w[1], s.own.w[2], s.opp.w[0]);
+  L.nib1[slot][k][le] = make_uint2(s.opp.w[1], s.opp.w[2]);
+  L.legal[slot][k][le] = make_uint2((uint32_t)o.legal, (uint32_t)(o.legal >> 32));
+  L.played[slot][k][le] = make_uint2((uint32_t)o.played, (uint32_t)(o.played >> 32));
+  L.rtt[slot][k][le] = (uint32_t)o.reward | ((uint32_t)term << 8) | ((uint32_t)trunc << 16);
+}
+
+// consumer: the outputs of ply p for the 64 envs of consumer wave cw, in
+// pc_emit_ply's two forms (kNt: raw non-temporal buffer stores, the
+// resource's extent dropping rows past n; else global stores behind bounds
+// checks)
+template <bool kNt>
+__device__ __forceinline__ void pc_emit_ply_full(const PcFullLds& L, int slot, int k, int p, int n, int wg_env0,
+                                                 int cw, int lane, const Outs& out) {
+  const int e0 = cw * 64;
+  if constexpr (kNt) {
+    const int g0 = wg_env0 + __builtin_amdgcn_readfirstlane(cw) * 64;
+    const size_t row0 = (size_t)p * n + g0;
+    const uint32_t nw = (uint32_t)max(0, min(64, n - g0));
+    if (out.obs) {
+      const __amdgpu_buffer_rsrc_t r = pc_rsrc(out.obs + row0 * 24, nw * 96u);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const int j = lane + 64 * q;
+        const int el = j / 6, qq = j - 6 * el;
+        pc_st16(r, (uint32_t)j * 16u, pc_obs_quad(L, slot, k, e0 + el, qq));
+      }
+    }
+    const uint32_t c = L.rtt[slot][k][e0 + lane];
+    const uint32_t l = (uint32_t)lane;
+    if (out.reward) pc_st4(pc_rsrc(out.reward + row0, nw * 4u), 4u * l, c & 0xFFu);
+    if (out.term) pc_st1(pc_rsrc(out.term + row0, nw), l, (uint8_t)((c >> 8) & 1u));
+    if (out.trunc) pc_st1(pc_rsrc(out.trunc + row0, nw), l, (uint8_t)((c >> 16) & 1u));
+    if (out.legal) {
+      const uint2 lg = L.legal[slot][k][e0 + lane];
+      pc_st8(pc_rsrc(out.legal + row0, nw * 8u), 8u * l, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
+    }
+    if (out.played) {
+      const uint2 pw = L.played[slot][k][e0 + lane];
+      pc_st8(pc_rsrc(out.played + row0, nw * 8u), 8u * l, (uint64_t)pw.x | ((uint64_t)pw.y << 32));
+    }
+  } else {
+    const int g0 = wg_env0 + e0;
+    const size_t row0 = (size_t)p * n + g0;
+    if (out.obs) {
+      int4* dst = reinterpret_cast<int4*>(out.obs + row0 * 24);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const int j = lane + 64 * q;
+        const int el = j / 6, qq = j - 6 * el;
+        if (g0 + el >= n) continue;
+        st_out(dst + j, pc_obs_quad(L, slot, k, e0 + el, qq));
+      }
+    }
+    if (g0 + lane < n) {
+      const uint32_t c = L.rtt[slot][k][e0 + lane];
+      const size_t ix = row0 + lane;
+      if (out.reward) st_out(out.reward + ix, (int32_t)(c & 0xFFu));
+      if (out.term) st_out(out.term + ix, (uint8_t)((c >> 8) & 1u));
+      if (out.trunc) st_out(out.trunc + ix, (uint8_t)((c >> 16) & 1u));
+      if (out.legal) {
+        const uint2 lg = L.legal[slot][k][e0 + lane];
+        st_out(out.legal + ix, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
+      }
+      if (out.played) {
+        const uint2 pw = L.played[slot][k][e0 + lane];
+        st_out(out.played + ix, (uint64_t)pw.x | ((uint64_t)pw.y << 32));
+      }
+    }
+  }
+}
+
+template <bool kOut, bool kNt>
+__global__ void __launch_bounds__(kPcThreads) k_rollout_pc_full(Planes pl, int n, Rng g, int plies,
+                                                                int max_steps, Outs out) {
+  __shared__ PcFullLds L;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool producer = wave < kPcGroups;
+  const int cw = wave % kPcGroups;
+  const int le = cw * 64 + lane;
+  const int wg_env0 = blockIdx.x * kPcEnvs;
+  const int i = wg_env0 + le;
+  const bool valid = i < n;
+  const int nb = pc_nblocks(plies);
+
+  Side s = side_start(0u);
+  int4 st = make_int4(0, 0, 0, 0);
+  uint32_t t0 = 0;
+  if (producer) {
+    if (valid) s = side_from_record(pl.p0[i], pl.p1[i]);
+  } else if (valid) {
+    t0 = pl.p1[i].w;
+  }
+  auto draw_block = [&](int b) {
+    int p0, np;
+    pc_block(b, plies, p0, np);
+    uint32_t R[4];
+    for (int k = 0; k < np; ++k) {
+      const uint32_t t = t0 + (uint32_t)(p0 + k);
+      if (k == 0 || (t & 1u) == 0u) ply_block(t, g.env0 + (uint32_t)i, g.k0, g.k1, R);
+      const bool odd = (t & 1u) != 0u;
+      L.draw[b % kPcSlots][k][le] = odd ? make_uint2(R[2], R[3]) : make_uint2(R[0], R[1]);
+    }
+  };
+  if (!producer) draw_block(0);
+  __syncthreads();
+  for (int b = 0; b < nb; ++b) {
+    int p0, np;
+    pc_block(b, plies, p0, np);
+    if (producer) {
+      for (int k = 0; k < np; ++k) {  // every lane: the turn is wave-cooperative
+        const uint2 rv = L.draw[b % kPcSlots][k][le];
+        uint32_t r[4];
+        ply_words(rv.x, rv.y, g.dice_mode, r);
+        TurnOut o;
+        int term, trunc;
+        ply_full_words(s, st, r, g.dice_mode, max_steps, true, o, term, trunc);
+        if (kOut) pc_put_full(L, b % kPcSlots, k, le, s, o, term, trunc);
+      }
+    } else {
+      if (b + 1 < nb) draw_block(b + 1);
+      if (kOut && b > 0) {
+        int q0, nq;
+        pc_block(b - 1, plies, q0, nq);
+        for (int k = 0; k < nq; ++k) pc_emit_ply_full<kNt>(L, (b - 1) % kPcSlots, k, q0 + k, n, wg_env0, cw, lane, out);
+      }
+    }
+    __syncthreads();
+  }
+  if (kOut && !producer && nb > 0) {
+    int p0, np;
+    pc_block(nb - 1, plies, p0, np);
+    for (int k = 0; k < np; ++k) pc_emit_ply_full<kNt>(L, (nb - 1) % kPcSlots, k, p0 + k, n, wg_env0, cw, lane, out);
+  }
+  int4 cum = make_int4(0, 0, 0, 0);
+  if (producer && valid) {
+    uint4 ra, rb;
+    side_to_record(s, ra, rb);
+    pl.p0[i] = ra;
+    pl.p1[i] = rb;
+    cum = stats_after(pl.stats, i, st, out.totals != nullptr);
+  }
+  if (out.totals) wg_totals(cum, out.totals);
+}
+
+
+// ---------------------------------------------------------------------------
+// k_rollout_pp_full: the FULL4 rollout with a pairwise hand-over.  Each
+// producer wave (waves 0-3) has its own consumer wave (waves 4-7) and a ring
+// of kPpR ply slots in LDS (draws and results); the pair hands plies over
+// through three LDS counters instead of workgroup barriers, so a producer
+// never waits for the other producers of its workgroup -- FULL4's turns vary
+// several-fold in cost from ply to ply (block-bound plies, DESIGN.md
+// section 10), and k_rollout_pc_full's one barrier per block of plies made
+// every producer wait for the slowest of four.
+//   producer, ply p: wait until drawn > p and emitted + kPpR > p, play the
+//     turn with the words of draw slot p % kPpR, leave the results in result
+//     slot p % kPpR, then produced = p + 1;
+//   consumer: draws plies 0 .. kPpR - 1 ahead; for each ply p: wait until
+//     produced > p, store ply p's outputs, then emitted = p + 1 (the result
+//     slot is free), draw ply p + kPpR into the draw slot ply p used (read
+//     before ply p was produced), then drawn = p + kPpR + 1.
+// Counters are wave-uniform LDS words; a release fence (workgroup scope)
+// orders each side's slot accesses before its counter store, an acquire
+// fence after the counter load orders the other side's.
+constexpr int kPpR = 8;  // ring depth in plies
+
+struct PpLds {
+  uint2 draw[kPcGroups][kPpR][64];
+  uint4 nib0[kPcGroups][kPpR][64];
+  uint2 nib1[kPcGroups][kPpR][64];
+  uint2 legal[kPcGroups][kPpR][64];
+  uint2 played[kPcGroups][kPpR][64];
+  uint32_t rtt[kPcGroups][kPpR][64];
+  uint32_t drawn[kPcGroups], produced[kPcGroups], emitted[kPcGroups];
+};
+
+__device__ __forceinline__ uint32_t pp_load(const uint32_t* c) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void pp_publish(uint32_t* c, uint32_t v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __hip_atomic_store(c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// spin until f(counter value) holds (wave-uniform), then acquire
+template <class F>
+__device__ __forceinline__ void pp_wait(const uint32_t* c, F ok) {
+  while (!ok(pp_load(c))) __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// obs quad qq of env el of pair cw, ring slot sl (pc_obs_quad's layout)
+__device__ __forceinline__ int4 pp_obs_quad(const PpLds& L, int cw, int sl, int el, int qq) {
+  const int wi = qq >> 1, sh = (qq & 1) * 16;
+  const uint32_t* n0w = reinterpret_cast<const uint32_t*>(&L.nib0[cw][sl][el]);
+  const uint32_t* n1w = reinterpret_cast<const uint32_t*>(&L.nib1[cw][sl][el]);
+  const uint32_t own = n0w[wi];
+  const uint32_t opp = wi == 0 ? n0w[3] : n1w[wi - 1];
+  int4 v;
+  v.x = nib_at(own, sh) - nib_at(opp, sh);
+  v.y = nib_at(own, sh + 4) - nib_at(opp, sh + 4);
+  v.z = nib_at(own, sh + 8) - nib_at(opp, sh + 8);
+  v.w = nib_at(own, sh + 12) - nib_at(opp, sh + 12);
+  return v;
+}
+
+// consumer: ply p's outputs of pair cw's 64 envs from ring slot sl
+// (pc_emit_ply_full's two store forms)
+template <bool kNt>
+__device__ __forceinline__ void pp_emit_ply(const PpLds& L, int cw, int sl, int p, int n, int g0, int lane,
+                                            const Outs& out) {
+  const size_t row0 = (size_t)p * n + g0;
+  if constexpr (kNt) {
+    const uint32_t nw = (uint32_t)max(0, min(64, n - g0));
+    if (out.obs) {
+      const __amdgpu_buffer_rsrc_t r = pc_rsrc(out.obs + row0 * 24, nw * 96u);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const int j = lane + 64 * q;
+        const int el = j / 6, qq = j - 6 * el;
+        pc_st16(r, (uint32_t)j * 16u, pp_obs_quad(L, cw, sl, el, qq));
+      }
+    }
+    const uint32_t c = L.rtt[cw][sl][lane];
+    const uint32_t l = (uint32_t)lane;
+    if (out.reward) pc_st4(pc_rsrc(out.reward + row0, nw * 4u), 4u * l, c & 0xFFu);
+    if (out.term) pc_st1(pc_rsrc(out.term + row0, nw), l, (uint8_t)((c >> 8) & 1u));
+    if (out.trunc) pc_st1(pc_rsrc(out.trunc + row0, nw), l, (uint8_t)((c >> 16) & 1u));
+    if (out.legal) {
+      const uint2 lg = L.legal[cw][sl][lane];
+      pc_st8(pc_rsrc(out.legal + row0, nw * 8u), 8u * l, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
+    }
+    if (out.played) {
+      const uint2 pw = L.played[cw][sl][lane];
+      pc_st8(pc_rsrc(out.played + row0, nw * 8u), 8u * l, (uint64_t)pw.x | ((uint64_t)pw.y << 32));
+    }
+  } else {
+    if (out.obs) {
+      int4* dst = reinterpret_cast<int4*>(out.obs + row0 * 24);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const int j = lane + 64 * q;
+        const int el = j / 6, qq = j - 6 * el;
+        if (g0 + el >= n) continue;
+        st_out(dst + j, pp_obs_quad(L, cw, sl, el, qq));
+      }
+    }
+    if (g0 + lane < n) {
+      const uint32_t c = L.rtt[cw][sl][lane];
+      const size_t ix = row0 + lane;
+      if (out.reward) st_out(out.reward + ix, (int32_t)(c & 0xFFu));
+      if (out.term) st_out(out.term + ix, (uint8_t)((c >> 8) & 1u));
+      if (out.trunc) st_out(out.trunc + ix, (uint8_t)((c >> 16) & 1u));
+      if (out.legal) {
+        const uint2 lg = L.legal[cw][sl][lane];
+        st_out(out.legal + ix, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
+      }
+      if (out.played) {
+        const uint2 pw = L.played[cw][sl][lane];
+        st_out(out.played + ix, (uint64_t)pw.x | ((uint64_t)pw.y << 32));
+      }
+    }
+  }
+}
+
+template <bool kOut, bool kNt>
+__global__ void __launch_bounds__(kPcThreads) k_rollout_pp_full(Planes pl, int n, Rng g, int plies,
+                                                                int max_steps, Outs out) {
+  __shared__ PpLds L;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const bool producer = wave < kPcGroups;
+  const int cw = __builtin_amdgcn_readfirstlane(wave % kPcGroups);
+  const int g0 = blockIdx.x * kPcEnvs + cw * 64;  // the pair's first env (global)
+  const int i = g0 + lane;
+  const bool valid = i < n;
+  if (threadIdx.x < kPcGroups) {
+    L.drawn[threadIdx.x] = 0u;
+    L.produced[threadIdx.x] = 0u;
+    L.emitted[threadIdx.x] = 0u;
+  }
+  __syncthreads();
+  int4 st = make_int4(0, 0, 0, 0);
+  if (producer) {
+    Side s = valid ? side_from_record(pl.p0[i], pl.p1[i]) : side_start(0u);
+    for (int p = 0; p < plies; ++p) {
+      const uint32_t up = (uint32_t)p;
+      const int sl = p % kPpR;
+      pp_wait(&L.drawn[cw], [&](uint32_t v) { return v > up; });
+      if (kOut && p >= kPpR) pp_wait(&L.emitted[cw], [&](uint32_t v) { return v + (uint32_t)kPpR > up; });
+      const uint2 rv = L.draw[cw][sl][lane];
+      uint32_t r[4];
+      ply_words(rv.x, rv.y, g.dice_mode, r);
+      TurnOut o;
+      int term, trunc;
+      ply_full_words(s, st, r, g.dice_mode, max_steps, true, o, term, trunc);
+      if (kOut) {
+        L.nib0[cw][sl][lane] = make_uint4(s.own.w[0], s.own.w[1], s.own.w[2], s.opp.w[0]);
+        L.nib1[cw][sl][lane] = make_uint2(s.opp.w[1], s.opp.w[2]);
+        L.legal[cw][sl][lane] = make_uint2((uint32_t)o.legal, (uint32_t)(o.legal >> 32));
+        L.played[cw][sl][lane] = make_uint2((uint32_t)o.played, (uint32_t)(o.played >> 32));
+        L.rtt[cw][sl][lane] = (uint32_t)o.reward | ((uint32_t)term << 8) | ((uint32_t)trunc << 16);
+      }
+      pp_publish(&L.produced[cw], up + 1u);
+    }
+    if (valid) {
+      uint4 ra, rb;
+      side_to_record(s, ra, rb);
+      pl.p0[i] = ra;
+      pl.p1[i] = rb;
+    }
+  } else {
+    const uint32_t t0 = valid ? pl.p1[i].w : 0u;
+    uint32_t R[4];  // the Philox block of the last ply drawn (one block per ply pair)
+    auto draw = [&](int p) {
+      const uint32_t t = t0 + (uint32_t)p;
+      if (p == 0 || (t & 1u) == 0u) ply_block(t, g.env0 + (uint32_t)i, g.k0, g.k1, R);
+      L.draw[cw][p % kPpR][lane] = (t & 1u) ? make_uint2(R[2], R[3]) : make_uint2(R[0], R[1]);
+    };
+    const int ahead = min(kPpR, plies);
+    for (int p = 0; p < ahead; ++p) draw(p);
+    pp_publish(&L.drawn[cw], (uint32_t)ahead);
+    for (int p = 0; p < plies; ++p) {
+      const uint32_t up = (uint32_t)p;
+      pp_wait(&L.produced[cw], [&](uint32_t v) { return v > up; });
+      if (kOut) {
+        pp_emit_ply<kNt>(L, cw, p % kPpR, p, n, g0, lane, out);
+        pp_publish(&L.emitted[cw], up + 1u);
+      }
+      if (p + kPpR < plies) {  // ply p's draw slot was read before ply p was produced
+        draw(p + kPpR);
+        pp_publish(&L.drawn[cw], up + (uint32_t)kPpR + 1u);
+      }
+    }
+  }
+  __syncthreads();
+  int4 cum = make_int4(0, 0, 0, 0);
+  if (producer && valid) cum = stats_after(pl.stats, i, st, out.totals != nullptr);
   if (out.totals) wg_totals(cum, out.totals);
 }
 

@@ -335,14 +335,15 @@ int launch_rollout_ref2(narde_env* e, int plies, const Outs& out, bool any, hipS
 }
 
 int launch_rollout_full(narde_env* e, int plies, const Outs& out, bool any, hipStream_t stream) {
-  // one wave per 64 envs at every length (round 4: faster than round 3's
-  // rule + helper waves from 100 plies up)
-  const dim3 g((unsigned)grid(e->n)), b(kBlock);
-  if (any)
-    k_rollout_wave<true><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
+  // producer/consumer pairs (k_rollout_pp_full)
+  const dim3 g((unsigned)((e->n + kPcEnvs - 1) / kPcEnvs)), b(kPcThreads);
+  if (any && plies <= kPcNtMaxPlies)
+    k_rollout_pp_full<true, true><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
+  else if (any)
+    k_rollout_pp_full<true, false><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
   else
-    k_rollout_wave<false><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
-  return check_launch("k_rollout_wave");
+    k_rollout_pp_full<false, false><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
+  return check_launch("k_rollout_pp_full");
 }
 
 }  // namespace

@@ -147,11 +147,18 @@ class RcclGather:
     broadcast through it); the same bytes as gather_total_rows.
 
     Every stage ends with the ranks agreeing (`agree`, or rank 0's status
-    byte riding with the unique id), so either every rank gets a
-    communicator or every rank raises RuntimeError -- a caller that falls
-    back to the process group's collective on that error falls back on every
-    rank alike (a rank deciding alone would leave the others in
-    a broadcast, or in a different collective, forever)."""
+    byte riding with the unique id), so when every rank's calls RETURN,
+    either every rank gets a communicator or every rank raises RuntimeError
+    -- a caller that falls back to the process group's collective on that
+    error falls back on every rank alike (a rank deciding alone
+    would leave the others in a broadcast, or in a different collective,
+    forever).  ncclCommInitRank itself is collective and blocking: a rank
+    whose init never returns (a peer that died inside its own init) leaves
+    the others inside theirs, and no agreement can follow; that case ends
+    with the launcher's timeout, not with the fallback.  (The non-blocking
+    init, ncclCommInitRankConfig with blocking = 0, would make every later
+    call on the communicator -- the timed ncclAllGather included -- liable
+    to return ncclInProgress and need polling, so it is not used.)"""
 
     def __init__(self, rows):
         self.comm = ctypes.c_void_p()

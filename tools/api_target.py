@@ -3,7 +3,10 @@
 k_step<false> (REF2 VecNardeEnv.step), k_step<true> (FULL4 step),
 k_observe's 198-float Tesauro observation and its int32[24] one.  Each runs
 `--warm` untimed then `--reps` timed calls back to back; HIP events around
-each run give microseconds per call, and the same command under
+each run give microseconds per eager call (`us`: the host's call rate when
+the kernel is shorter than the call, as k_observe's is), and the same calls
+replayed from a CUDA graph give the device time per call (`graph_us`: the
+kernel plus the gap between dispatches).  The same command under
 `rocprofv3 --kernel-trace --stats` gives the per-dispatch durations
 (tools/gpu_round.sh commits that summary).  Prints one JSON line.
 
@@ -38,6 +41,33 @@ def timed(fn, warm, reps):
     return s.elapsed_time(e) * 1e3 / reps
 
 
+def graphed(fn, reps, per_graph=50):
+    """Device time per call: `per_graph` calls captured in one CUDA graph,
+    replayed until `reps` calls ran, HIP events around the replays -- no
+    host launch cost between kernels (an eager call of a ~4-us kernel is
+    bound by the host's ~6-us call, so HIP events around eager calls measure
+    the host, not the kernel)."""
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(g, stream=side):
+            for _ in range(per_graph):
+                fn()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    R = max(1, reps // per_graph)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(R):
+        g.replay()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1e3 / (R * per_graph)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=65536)
@@ -49,8 +79,10 @@ def main():
     for rules, per_env in (("ref2", 64 + 114), ("full4", 64 + 118)):
         env = VecNardeEnv(n, device="cuda:0", seed=0, rules=rules)
         us = timed(env.step, a.warm, a.reps)
-        out[f"k_step_{rules}"] = {"us": round(us, 2), "bytes": n * per_env,
-                                  "frac": round(n * per_env / (us * 1e-6) / HBM_PEAK, 4)}
+        gus = graphed(env.step, a.reps)
+        out[f"k_step_{rules}"] = {"us": round(us, 2), "graph_us": round(gus, 2), "bytes": n * per_env,
+                                  "frac": round(n * per_env / (us * 1e-6) / HBM_PEAK, 4),
+                                  "graph_frac": round(n * per_env / (gus * 1e-6) / HBM_PEAK, 4)}
         env.close()
     env = VecNardeEnv(n, device="cuda:0", seed=0)
     env.selfplay(100)
@@ -58,8 +90,10 @@ def main():
     for kind, per_env, fn in (("tesauro198", 32 + 792, lambda: env.tesauro198(out=obs198)),
                               ("observe_int24", 32 + 96, env.observe)):
         us = timed(fn, a.warm, a.reps)
-        out[kind] = {"us": round(us, 2), "bytes": n * per_env,
-                     "frac": round(n * per_env / (us * 1e-6) / HBM_PEAK, 4)}
+        gus = graphed(fn, a.reps)
+        out[kind] = {"us": round(us, 2), "graph_us": round(gus, 2), "bytes": n * per_env,
+                     "frac": round(n * per_env / (us * 1e-6) / HBM_PEAK, 4),
+                     "graph_frac": round(n * per_env / (gus * 1e-6) / HBM_PEAK, 4)}
     env.close()
     print(json.dumps(out), flush=True)
 

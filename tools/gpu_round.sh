@@ -68,12 +68,12 @@ if [ "$PHASE" = run ]; then
 else
   pmc_pair ref2 20 "k_rollout_pc<true, true>" 114 pmc_k_rollout_p20 \
     && pmc_pair ref2 1000 "k_rollout_pc<true, false>" 114 pmc_k_rollout \
-    && pmc_pair full4 20 "k_rollout_wave<true>" 118 pmc_k_rollout_full_p20 \
-    && pmc_pair full4 1000 "k_rollout_wave<true>" 118 pmc_k_rollout_full \
+    && pmc_pair full4 20 "k_rollout_pp_full<true, true>" 118 pmc_k_rollout_full_p20 \
+    && pmc_pair full4 1000 "k_rollout_pp_full<true, false>" 118 pmc_k_rollout_full \
     && sq_pass ref2 20 "k_rollout_pc<true, true>" sq_k_rollout_p20 \
-    && sq_pass full4 20 "k_rollout_wave<true>" sq_k_rollout_full_p20 \
+    && sq_pass full4 20 "k_rollout_pp_full<true, true>" sq_k_rollout_full_p20 \
     && sq_pass ref2 1000 "k_rollout_pc<true, false>" sq_k_rollout_p1000 \
-    && sq_pass full4 1000 "k_rollout_wave<true>" sq_k_rollout_full_p1000 \
+    && sq_pass full4 1000 "k_rollout_pp_full<true, false>" sq_k_rollout_full_p1000 \
     && echo "[gpu_round] $(date +%T) api kernels (timed, traced)" \
     && timeout -k 10 120 python3 tools/api_target.py > "$OUT/api.json" \
     && (cd /tmp && timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/api_trace" -o api \

@@ -35,9 +35,8 @@ def profile(name):
 
 def launched_kernel(full, plies):
     """The kernel a launch of this shape runs (bench.py kernel_name)."""
-    if not full:
-        return "k_rollout_pc<true, true>" if plies <= 32 else "k_rollout_pc<true, false>"
-    return "k_rollout_wave<true>"
+    nt = "true" if plies <= 32 else "false"
+    return f"k_rollout_pc<true, {nt}>" if not full else f"k_rollout_pp_full<true, {nt}>"
 
 
 def matches(summary, envs, plies, kernel):
