@@ -157,8 +157,12 @@ def load_traffic(path, envs, plies, kernel):
 # SURVEY.md 8(d)'s secondary figure: VALU wave-instructions per launch (a
 # committed SQ-counter summary at the launch shape, tools/sq_summary.py)
 # against the chip's integer VALU issue peak -- one VALU wave-instruction per
-# 4 cycles per SIMD (tools/sq_summary.py's docstring)
+# 4 cycles per SIMD: what one wave issues of any kind, and two waves of the
+# slow kinds; two waves issue the fast kinds every 2 cycles
+# (profiles/r05/issue_probe/summary.json, tools/sq_summary.py's docstring)
 ISSUE_PEAK = 1024 * 2.4e9 / 4
+ISSUE_BASIS = ("1,024 SIMDs x 2.4 GHz / 4 cycles per VALU wave-instruction: one wave's rate (any kind) "
+               "and two waves' rate on the slow kinds, measured in profiles/r05/issue_probe/summary.json")
 
 
 def load_issue(full4, envs, plies, kernel_ms):
@@ -185,6 +189,8 @@ def load_issue(full4, envs, plies, kernel_ms):
         "peak": round(ISSUE_PEAK / 1e9, 2),
         "unit": "G VALU wave-instructions/s",
         "frac": round(achieved / ISSUE_PEAK, 4),
+        "basis": ISSUE_BASIS,
+        "frac_of_two_wave_fast_peak": round(achieved / (2 * ISSUE_PEAK), 4),
         "valu_busy_of_wave_cycles": d.get("valu_busy_of_wave_cycles"),
         "source": os.path.relpath(path, ROOT),
     }

@@ -1,4 +1,4 @@
-// kernels_rollout.h -- the timed path: per-ply outputs, k_step, k_rollout and the producer/consumer k_rollout_pc
+// kernels_rollout.h -- the timed path: per-ply outputs, k_step, the producer/consumer rollouts k_rollout_pc (REF2) and k_rollout_pp_full (FULL4) (DESIGN.md sections 5, 10)
 // Part of the one translation unit narde.hip (included there, in order);
 // not a standalone header.
 #pragma once
@@ -29,13 +29,33 @@ struct StepArgs {
   Outs out;
 };
 
-// Every per-ply output is a plain store.  Measured against non-temporal
-// stores on sustained 1,000-ply REF2 rollouts (one box): plain 0.1265 ms
-// per 100 plies, non-temporal obs rows 0.135 (the narrow outputs' policy
-// did not matter).
+// The rollouts' long launches store plainly (the consumers' global-store
+// form): measured against non-temporal stores on sustained 1,000-ply REF2
+// rollouts (one box), plain 0.1265 ms per 100 plies, non-temporal obs rows
+// 0.135 (the narrow outputs' policy did not matter).  Short launches store
+// through non-temporal raw buffer stores (pc_st*), the API kernels through
+// st_nt below.
 template <class T>
 __device__ __forceinline__ void st_out(T* p, T v) {
   *p = v;
+}
+
+// The per-call API kernels (k_step, k_observe) store non-temporally: a
+// launch's outputs are all it writes, and their L2 write-back is otherwise
+// on the call's critical path (with the straight-line REF2 ply below,
+// k_step<false> 5.25 -> 5.09-5.12 us and k_observe 2.88 -> 2.71 us per
+// graph-replayed call; the rollouts' long launches keep plain stores, see
+// st_out; profiles/r05/ab/api_kstep_variants.log)
+template <class T>
+__device__ __forceinline__ void st_nt(T* p, T v) {
+  if constexpr (sizeof(T) == 16) {
+    typedef int v4nt __attribute__((ext_vector_type(4)));
+    v4nt x;
+    __builtin_memcpy(&x, &v, 16);
+    __builtin_nontemporal_store(x, reinterpret_cast<v4nt*>(p));
+  } else {
+    __builtin_nontemporal_store(v, p);
+  }
 }
 
 // the nibble of x at bit `off` (a multiple of 4, below 32) as one v_bfe_u32:
@@ -86,12 +106,12 @@ __device__ __forceinline__ int4 obs_quad(const Side& s) {
 
 __device__ __forceinline__ void store_obs(int32_t* __restrict__ obs, size_t ix, const Side& s) {
   int4* o = reinterpret_cast<int4*>(obs + ix * 24);
-  st_out(o + 0, obs_quad<0>(s));
-  st_out(o + 1, obs_quad<1>(s));
-  st_out(o + 2, obs_quad<2>(s));
-  st_out(o + 3, obs_quad<3>(s));
-  st_out(o + 4, obs_quad<4>(s));
-  st_out(o + 5, obs_quad<5>(s));
+  st_nt(o + 0, obs_quad<0>(s));
+  st_nt(o + 1, obs_quad<1>(s));
+  st_nt(o + 2, obs_quad<2>(s));
+  st_nt(o + 3, obs_quad<3>(s));
+  st_nt(o + 4, obs_quad<4>(s));
+  st_nt(o + 5, obs_quad<5>(s));
 }
 
 // whole-wave obs store through the wave's 6-KiB LDS slice (all 64 lanes
@@ -108,7 +128,7 @@ __device__ __forceinline__ void store_obs_wave(int32_t* __restrict__ obs, size_t
   wave_lds_handoff();
   int4* dst = reinterpret_cast<int4*>(obs + (ix - lane) * 24);
 #pragma unroll
-  for (int q = 0; q < 6; ++q) st_out(dst + q * 64 + lane, lds[q * 64 + lane]);
+  for (int q = 0; q < 6; ++q) st_nt(dst + q * 64 + lane, lds[q * 64 + lane]);
   wave_lds_handoff();  // the slice's next writes stay behind these reads
 }
 
@@ -124,18 +144,18 @@ __device__ __forceinline__ void store_common(const Outs& out, size_t ix, const S
     if (via_lds) store_obs_wave(out.obs, ix, s, lds);
     else store_obs(out.obs, ix, s);
   }
-  if (out.reward) st_out(out.reward + ix, (int32_t)reward);
-  if (out.term) st_out(out.term + ix, (uint8_t)term);
-  if (out.trunc) st_out(out.trunc + ix, (uint8_t)trunc);
+  if (out.reward) st_nt(out.reward + ix, (int32_t)reward);
+  if (out.term) st_nt(out.term + ix, (uint8_t)term);
+  if (out.trunc) st_nt(out.trunc + ix, (uint8_t)trunc);
 }
 
 __device__ __forceinline__ void store_outs(const Outs& out, size_t ix, const Side& s,
                                            const StepOut& o, int term, int trunc, int4* lds,
                                            bool wave_full) {
   store_common(out, ix, s, o.reward, term, trunc, lds, wave_full);
-  if (out.legal) st_out(out.legal + ix, (uint64_t)compact_legal(o.l1));
+  if (out.legal) st_nt(out.legal + ix, (uint64_t)compact_legal(o.l1));
   if (out.act_out)
-    st_out(reinterpret_cast<uint32_t*>(out.act_out) + ix,
+    st_nt(reinterpret_cast<uint32_t*>(out.act_out) + ix,
            ((uint32_t)(uint16_t)o.code1) | ((uint32_t)(uint16_t)o.code2 << 16));
 }
 
@@ -144,8 +164,8 @@ __device__ __forceinline__ void store_outs(const Outs& out, size_t ix, const Sid
                                            bool wave_full) {
   (void)wave_full;
   store_common(out, ix, s, o.reward, term, trunc, lds, false);
-  if (out.legal) st_out(out.legal + ix, o.legal);
-  if (out.played) st_out(out.played + ix, o.played);
+  if (out.legal) st_nt(out.legal + ix, o.legal);
+  if (out.played) st_nt(out.played + ix, o.played);
 }
 
 // this wave's slice of the block's obs staging buffer (6 KiB per wave)
@@ -172,8 +192,11 @@ __device__ __forceinline__ void ply(Side& s, int4& st, const Rng& g, uint32_t i,
   int d0 = 0, d1 = 0, c1 = 0, c2 = 0;
   if (dice) { d0 = dice[2 * i]; d1 = dice[2 * i + 1]; }
   if (actions) { c1 = actions[2 * i]; c2 = actions[2 * i + 1]; }
-  env_ply(s, st, r, dice != nullptr, d0, d1, g.dice_mode, actions == nullptr, c1, c2, max_steps,
-          autoreset, o, term, trunc);
+  // self-play with auto-reset (every argument a kernel argument: a
+  // wave-uniform branch): the rollouts' straight-line ply
+  if (!dice && !actions && autoreset) env_ply_policy_sl(s, st, r, g.dice_mode, max_steps, o, term, trunc);
+  else env_ply(s, st, r, dice != nullptr, d0, d1, g.dice_mode, actions == nullptr, c1, c2, max_steps,
+               autoreset, o, term, trunc);
 }
 
 // the words of ply p of a launch (env counter t): the Philox block on the
@@ -209,13 +232,34 @@ __device__ __forceinline__ int wave_parity(bool valid, uint32_t t) {
 // straight-line (turn_moves_sl)
 template <bool kFilt>
 __device__ __forceinline__ void ply_free_turn(Side& s, int dh, int dl, uint32_t bs, uint32_t fw, const uint32_t w[4],
-                                              bool flip_always, TurnOut& o) {
-  uint32_t Lh, Ll, Ch, Cl;
-  int M, hl0;
-  turn_c0_free(s, dh, dl, Lh, Ll, Ch, Cl, M, hl0);
+                                              bool flip_always, TurnOut& o, const TurnC0& c) {
+  uint32_t Lh = c.Lh, Ll = c.Ll, Ch = c.Ch, Cl = c.Cl;
+  int M = c.M;
   const bool b2 = kFilt && bs != 0u;
   if (kFilt && b2) turn_c0_pair_bound_w(s, dh, dl, bs, fw, Lh, Ll, Ch, Cl, M);
-  turn_moves_sl(s, dh, dl, Ch, Cl, M, hl0, w, b2, fw, flip_always, o);
+  turn_moves_sl(s, dh, dl, Ch, Cl, M, c.hl0, w, b2, fw, flip_always, o);
+}
+
+// the turn and the end of the ply once the block test (bs, fw) and
+// turn_c0_free's results (c) are known; every lane of the wave must call it
+__device__ __forceinline__ void ply_full_turn(Side& s, int4& st, int dh, int dl, uint32_t bs, uint32_t fw,
+                                              const TurnC0& c, const uint32_t r[4], int max_steps, bool autoreset,
+                                              TurnOut& o, int& term, int& trunc) {
+  uint32_t w[4];
+  turn_words(r, w);
+  const uint32_t mover_black = s.black;
+  // three kinds of wave (one instruction stream each): no block-bound
+  // lane, block-bound two-dice lanes only, a block-bound doubles lane
+  // (one copy of the turn for all three: 0.448 against 0.437 ms per 100
+  // plies of 20-ply launches, tools/diag/gpu_ab_f4.sh)
+  if (__ballot(bs != 0u && dh == dl) == 0ull) {
+    if (__ballot(bs != 0u) == 0ull) ply_free_turn<false>(s, dh, dl, bs, fw, w, autoreset, o, c);
+    else ply_free_turn<true>(s, dh, dl, bs, fw, w, autoreset, o, c);
+  } else {
+    ply_bound_turn_c0(s, dh, dl, bs, fw, w, autoreset, o, (int)(threadIdx.x & 63), c);
+  }
+  if (autoreset) ply_close_sl(s, st, o.term, o.reward, mover_black, r[3], max_steps, term, trunc);
+  else ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, false, term, trunc);
 }
 
 // the ply with its words r already drawn (ply_words); every lane of the wave
@@ -229,21 +273,9 @@ __device__ __forceinline__ void ply_full_words(Side& s, int4& st, const uint32_t
   const uint32_t low = block_lowmask(s.P);
   uint32_t fw;
   const uint32_t bs = turn_block_set_sl(s.O, s.S1o, s.P, low, dh, dl, fw);
-  uint32_t w[4];
-  turn_words(r, w);
-  const uint32_t mover_black = s.black;
-  // three kinds of wave (one instruction stream each): no block-bound
-  // lane, block-bound two-dice lanes only, a block-bound doubles lane
-  // (one copy of the turn for all three: 0.448 against 0.437 ms per 100
-  // plies of 20-ply launches, tools/diag/gpu_ab_f4.sh)
-  if (__ballot(bs != 0u && dh == dl) == 0ull) {
-    if (__ballot(bs != 0u) == 0ull) ply_free_turn<false>(s, dh, dl, bs, fw, w, autoreset, o);
-    else ply_free_turn<true>(s, dh, dl, bs, fw, w, autoreset, o);
-  } else {
-    ply_bound_turn(s, dh, dl, bs, fw, w, autoreset, o, (int)(threadIdx.x & 63));
-  }
-  if (autoreset) ply_close_sl(s, st, o.term, o.reward, mover_black, r[3], max_steps, term, trunc);
-  else ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, false, term, trunc);
+  TurnC0 c;
+  turn_c0_free(s, dh, dl, c.Lh, c.Ll, c.Ch, c.Cl, c.M, c.hl0);
+  ply_full_turn(s, st, dh, dl, bs, fw, c, r, max_steps, autoreset, o, term, trunc);
 }
 
 __device__ __forceinline__ void ply_policy_full(Side& s, int4& st, const Rng& g, uint32_t i, int max_steps,
@@ -356,50 +388,14 @@ __global__ void __launch_bounds__(kBlock) k_step(StepArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_rollout_wave: the FULL4 rollout, one wave per 64 envs (ply_policy_full):
-// `plies` whole turns of random-legal self-play with auto-reset, the record
-// in VGPRs, every ply's outputs stored straight from registers (the lanes
-// play in lockstep, so a wave's rows of a ply go out together).  Round 3's
-// k_rollout_full -- rule waves playing the block-free turns and parking
-// block-bound envs with a helper wave on the same SIMD, lanes drifting up
-// to 16 plies apart, the narrow rows through an LDS ring -- was the faster
-// kernel from 48 plies per launch; with the straight-line turn this one is
-// faster at every length (100 plies 0.414 -> 0.353, 1,000 plies 0.349 ->
-// 0.319 ms per 100 plies; stats only 0.375 -> 0.306 / 0.306 -> 0.274;
-// tools/diag/gpu_ab_len.sh, one box) and k_rollout_full is retired
-// (DESIGN.md section 10, Appendix M.10).
-template <bool kOut>
-__global__ void __launch_bounds__(kBlock, 1) k_rollout_wave(Planes pl, int n, Rng g, int plies, int max_steps,
-                                                            Outs out) {
-  const int i = blockIdx.x * kBlock + threadIdx.x;
-  const bool valid = i < n;  // lanes past n stay: the turn is wave-cooperative
-  Side s = valid ? side_from_record(pl.p0[i], pl.p1[i]) : side_start(0u);
-  int4 st = make_int4(0, 0, 0, 0);
-  uint32_t R[4];  // the Philox block of the current ply pair
-  const int par = wave_parity(valid, s.t);
-  for (int p = 0; p < plies; ++p) {
-    TurnOut o;
-    int term, trunc;
-    ply_policy_full(s, st, g, (uint32_t)i, max_steps, true, o, term, trunc, R, p, par);
-    if (kOut && valid) store_outs(out, (size_t)p * n + i, s, o, term, trunc, nullptr, false);
-  }
-  int4 cum = make_int4(0, 0, 0, 0);
-  if (valid) {
-    uint4 ra, rb;
-    side_to_record(s, ra, rb);
-    pl.p0[i] = ra;
-    pl.p1[i] = rb;
-    cum = stats_after(pl.stats, i, st, out.totals != nullptr);
-  }
-  if (out.totals) wg_totals(cum, out.totals);
-}
-
-// ---------------------------------------------------------------------------
 // k_rollout_pc: the REF2 rollout as a producer/consumer workgroup.
 //
 // At B = 65,536 one lane per env gives exactly one wave per SIMD, and one wave
-// alone issues a VALU instruction only every 4 cycles (MI355X_MICROARCH.md,
-// constants table) -- half of what the SIMD can issue.  So each workgroup
+// alone issues a VALU instruction only every 4 cycles, whatever the kind;
+// a second wave on the SIMD adds issue slots for the "fast" kinds (add/sub,
+// and/or/xor, bitop3, shift right: every 2 cycles across two waves) and
+// hides the first one's waits (profiles/r05/issue_probe/summary.json,
+// tools/issue_probe.hip).  So each workgroup
 // (one per CU) holds 256 envs on 8 waves, two per SIMD:
 //   waves 0-3 (producers, the older waves, which win VALU arbitration) run
 //     the rules for their env with the record in VGPRs;
@@ -683,181 +679,19 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
 
 
 // ---------------------------------------------------------------------------
-// k_rollout_pc_full: the FULL4 rollout (whole turns)
-// in k_rollout_pc's producer/consumer shape.  Waves 0-3 play the turns
-// (ply_full_words, wave-cooperative: every lane of a producer wave plays,
-// lanes past n on a dummy state) with the record in VGPRs; waves 4-7 draw
-// the next block's Philox words and store the previous block's outputs,
-// every wave-wide obs store one contiguous 1 KiB.  The one-wave kernel
-// (k_rollout_wave) stores its own 96-B obs rows and draws its own words, and
-// those stores stall its turn: with no turn at all it still took 0.208 ms
-// per 100 plies of 20-ply launches.
-struct PcFullLds {
-  uint2 draw[kPcSlots][kPcR][kPcEnvs];     // the ply's (wa, wb) per env and ply
-  uint4 nib0[kPcSlots][kPcR][kPcEnvs];     // {own w0, own w1, own w2, opp w0} (next mover's view)
-  uint2 nib1[kPcSlots][kPcR][kPcEnvs];     // {opp w1, opp w2}
-  uint2 legal[kPcSlots][kPcR][kPcEnvs];    // C_0 word (lo, hi)
-  uint2 played[kPcSlots][kPcR][kPcEnvs];   // played sub-moves word (lo, hi)
-  uint32_t rtt[kPcSlots][kPcR][kPcEnvs];   // reward | term << 8 | trunc << 16
-};
-
-__device__ __forceinline__ void pc_put_full(PcFullLds& L, int slot, int k, int le, const Side& s,
-                                            const TurnOut& o, int term, int trunc) {
-  L.nib0[slot][k][le] = make_uint4(s.own.w[0], s.own.w[1], s.own.w[2], s.opp.w[0]);
-  L.nib1[slot][k][le] = make_uint2(s.opp.w[1], s.opp.w[2]);
-  L.legal[slot][k][le] = make_uint2((uint32_t)o.legal, (uint32_t)(o.legal >> 32));
-  L.played[slot][k][le] = make_uint2((uint32_t)o.played, (uint32_t)(o.played >> 32));
-  L.rtt[slot][k][le] = (uint32_t)o.reward | ((uint32_t)term << 8) | ((uint32_t)trunc << 16);
-}
-
-// consumer: the outputs of ply p for the 64 envs of consumer wave cw, in
-// pc_emit_ply's two forms (kNt: raw non-temporal buffer stores, the
-// resource's extent dropping rows past n; else global stores behind bounds
-// checks)
-template <bool kNt>
-__device__ __forceinline__ void pc_emit_ply_full(const PcFullLds& L, int slot, int k, int p, int n, int wg_env0,
-                                                 int cw, int lane, const Outs& out) {
-  const int e0 = cw * 64;
-  if constexpr (kNt) {
-    const int g0 = wg_env0 + __builtin_amdgcn_readfirstlane(cw) * 64;
-    const size_t row0 = (size_t)p * n + g0;
-    const uint32_t nw = (uint32_t)max(0, min(64, n - g0));
-    if (out.obs) {
-      const __amdgpu_buffer_rsrc_t r = pc_rsrc(out.obs + row0 * 24, nw * 96u);
-#pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        const int j = lane + 64 * q;
-        const int el = j / 6, qq = j - 6 * el;
-        pc_st16(r, (uint32_t)j * 16u, pc_obs_quad(L, slot, k, e0 + el, qq));
-      }
-    }
-    const uint32_t c = L.rtt[slot][k][e0 + lane];
-    const uint32_t l = (uint32_t)lane;
-    if (out.reward) pc_st4(pc_rsrc(out.reward + row0, nw * 4u), 4u * l, c & 0xFFu);
-    if (out.term) pc_st1(pc_rsrc(out.term + row0, nw), l, (uint8_t)((c >> 8) & 1u));
-    if (out.trunc) pc_st1(pc_rsrc(out.trunc + row0, nw), l, (uint8_t)((c >> 16) & 1u));
-    if (out.legal) {
-      const uint2 lg = L.legal[slot][k][e0 + lane];
-      pc_st8(pc_rsrc(out.legal + row0, nw * 8u), 8u * l, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
-    }
-    if (out.played) {
-      const uint2 pw = L.played[slot][k][e0 + lane];
-      pc_st8(pc_rsrc(out.played + row0, nw * 8u), 8u * l, (uint64_t)pw.x | ((uint64_t)pw.y << 32));
-    }
-  } else {
-    const int g0 = wg_env0 + e0;
-    const size_t row0 = (size_t)p * n + g0;
-    if (out.obs) {
-      int4* dst = reinterpret_cast<int4*>(out.obs + row0 * 24);
-#pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        const int j = lane + 64 * q;
-        const int el = j / 6, qq = j - 6 * el;
-        if (g0 + el >= n) continue;
-        st_out(dst + j, pc_obs_quad(L, slot, k, e0 + el, qq));
-      }
-    }
-    if (g0 + lane < n) {
-      const uint32_t c = L.rtt[slot][k][e0 + lane];
-      const size_t ix = row0 + lane;
-      if (out.reward) st_out(out.reward + ix, (int32_t)(c & 0xFFu));
-      if (out.term) st_out(out.term + ix, (uint8_t)((c >> 8) & 1u));
-      if (out.trunc) st_out(out.trunc + ix, (uint8_t)((c >> 16) & 1u));
-      if (out.legal) {
-        const uint2 lg = L.legal[slot][k][e0 + lane];
-        st_out(out.legal + ix, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
-      }
-      if (out.played) {
-        const uint2 pw = L.played[slot][k][e0 + lane];
-        st_out(out.played + ix, (uint64_t)pw.x | ((uint64_t)pw.y << 32));
-      }
-    }
-  }
-}
-
-template <bool kOut, bool kNt>
-__global__ void __launch_bounds__(kPcThreads) k_rollout_pc_full(Planes pl, int n, Rng g, int plies,
-                                                                int max_steps, Outs out) {
-  __shared__ PcFullLds L;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const bool producer = wave < kPcGroups;
-  const int cw = wave % kPcGroups;
-  const int le = cw * 64 + lane;
-  const int wg_env0 = blockIdx.x * kPcEnvs;
-  const int i = wg_env0 + le;
-  const bool valid = i < n;
-  const int nb = pc_nblocks(plies);
-
-  Side s = side_start(0u);
-  int4 st = make_int4(0, 0, 0, 0);
-  uint32_t t0 = 0;
-  if (producer) {
-    if (valid) s = side_from_record(pl.p0[i], pl.p1[i]);
-  } else if (valid) {
-    t0 = pl.p1[i].w;
-  }
-  auto draw_block = [&](int b) {
-    int p0, np;
-    pc_block(b, plies, p0, np);
-    uint32_t R[4];
-    for (int k = 0; k < np; ++k) {
-      const uint32_t t = t0 + (uint32_t)(p0 + k);
-      if (k == 0 || (t & 1u) == 0u) ply_block(t, g.env0 + (uint32_t)i, g.k0, g.k1, R);
-      const bool odd = (t & 1u) != 0u;
-      L.draw[b % kPcSlots][k][le] = odd ? make_uint2(R[2], R[3]) : make_uint2(R[0], R[1]);
-    }
-  };
-  if (!producer) draw_block(0);
-  __syncthreads();
-  for (int b = 0; b < nb; ++b) {
-    int p0, np;
-    pc_block(b, plies, p0, np);
-    if (producer) {
-      for (int k = 0; k < np; ++k) {  // every lane: the turn is wave-cooperative
-        const uint2 rv = L.draw[b % kPcSlots][k][le];
-        uint32_t r[4];
-        ply_words(rv.x, rv.y, g.dice_mode, r);
-        TurnOut o;
-        int term, trunc;
-        ply_full_words(s, st, r, g.dice_mode, max_steps, true, o, term, trunc);
-        if (kOut) pc_put_full(L, b % kPcSlots, k, le, s, o, term, trunc);
-      }
-    } else {
-      if (b + 1 < nb) draw_block(b + 1);
-      if (kOut && b > 0) {
-        int q0, nq;
-        pc_block(b - 1, plies, q0, nq);
-        for (int k = 0; k < nq; ++k) pc_emit_ply_full<kNt>(L, (b - 1) % kPcSlots, k, q0 + k, n, wg_env0, cw, lane, out);
-      }
-    }
-    __syncthreads();
-  }
-  if (kOut && !producer && nb > 0) {
-    int p0, np;
-    pc_block(nb - 1, plies, p0, np);
-    for (int k = 0; k < np; ++k) pc_emit_ply_full<kNt>(L, (nb - 1) % kPcSlots, k, p0 + k, n, wg_env0, cw, lane, out);
-  }
-  int4 cum = make_int4(0, 0, 0, 0);
-  if (producer && valid) {
-    uint4 ra, rb;
-    side_to_record(s, ra, rb);
-    pl.p0[i] = ra;
-    pl.p1[i] = rb;
-    cum = stats_after(pl.stats, i, st, out.totals != nullptr);
-  }
-  if (out.totals) wg_totals(cum, out.totals);
-}
-
-
-// ---------------------------------------------------------------------------
 // k_rollout_pp_full: the FULL4 rollout with a pairwise hand-over.  Each
 // producer wave (waves 0-3) has its own consumer wave (waves 4-7) and a ring
 // of kPpR ply slots in LDS (draws and results); the pair hands plies over
 // through three LDS counters instead of workgroup barriers, so a producer
 // never waits for the other producers of its workgroup -- FULL4's turns vary
 // several-fold in cost from ply to ply (block-bound plies, DESIGN.md
-// section 10), and k_rollout_pc_full's one barrier per block of plies made
-// every producer wait for the slowest of four.
+// section 10), and k_rollout_pc's one barrier per block of plies made every
+// producer wait for the slowest of four (the same kernel with barrier
+// blocks: 0.412 / 0.307 ms per 100 plies at 20 / 1,000 plies against the
+// one-wave kernel's 0.405 / 0.290 and this one's 0.382 / 0.268,
+// profiles/r05/ab/sus_wave_pc_pp.log).  Round 4's one-wave kernel
+// (k_rollout_wave: each wave drew its own words and stored its own rows
+// at a 96-B lane stride) is retired; git history has it.
 //   producer, ply p: wait until drawn > p and emitted + kPpR > p, play the
 //     turn with the words of draw slot p % kPpR, leave the results in result
 //     slot p % kPpR, then produced = p + 1;
@@ -865,6 +699,11 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc_full(Planes pl, int n
 //     produced > p, store ply p's outputs, then emitted = p + 1 (the result
 //     slot is free), draw ply p + kPpR into the draw slot ply p used (read
 //     before ply p was produced), then drawn = p + kPpR + 1.
+// (Measured and not kept: the consumer running each ply's block test
+// (turn_block_set_sl on the masks the previous ply left) while the
+// producer computes C_0 -- the producer then waits for it: 20-ply launches
+// 0.382 -> 0.408, 1,000 plies 0.268 -> 0.287 ms per 100 plies,
+// profiles/r05/ab/.)
 // Counters are wave-uniform LDS words; a release fence (workgroup scope)
 // orders each side's slot accesses before its counter store, an acquire
 // fence after the counter load orders the other side's.
@@ -1022,8 +861,10 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pp_full(Planes pl, int n
       L.draw[cw][p % kPpR][lane] = (t & 1u) ? make_uint2(R[2], R[3]) : make_uint2(R[0], R[1]);
     };
     const int ahead = min(kPpR, plies);
-    for (int p = 0; p < ahead; ++p) draw(p);
-    pp_publish(&L.drawn[cw], (uint32_t)ahead);
+    for (int p = 0; p < ahead; ++p) {  // each ply's words published as drawn: ply 0 starts at once
+      draw(p);
+      pp_publish(&L.drawn[cw], (uint32_t)p + 1u);
+    }
     for (int p = 0; p < plies; ++p) {
       const uint32_t up = (uint32_t)p;
       pp_wait(&L.produced[cw], [&](uint32_t v) { return v > up; });

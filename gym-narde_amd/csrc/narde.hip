@@ -10,9 +10,11 @@
 //   device_common.h     build knobs, env planes, the device RNG draws
 //   kernels_state.h     reset, set/get state, peek dice, get_valid_moves
 //                       (k_legal), apply, statistics, block rule
-//   kernels_full4.h     the wave-cooperative FULL4 turn, k_legal_full
+//   kernels_full4.h     k_legal_full, with full4_wave.h: the
+//                       wave-cooperative FULL4 turn
 //   kernels_rollout.h   the timed path: per-ply outputs, k_step (API step),
-//                       k_rollout, the producer/consumer k_rollout_pc
+//                       the producer/consumer rollouts k_rollout_pc (REF2)
+//                       and k_rollout_pp_full (FULL4)
 //   kernels_agent.h     observations, move masks, the policy kernel, the DQN
 //                       transition
 // This file keeps the handle, the host-side checks and every C entry point.

@@ -1475,6 +1475,14 @@ NARDE_FN void turn_c0_free(const Side& s, int dh, int dl, uint32_t& Lh, uint32_t
   M = dbl ? (Lh != 0u ? Mx : 0) : M2;
 }
 
+// turn_c0_free's results (a block-free turn's C_0 and M, the root lists,
+// the head allowance), for callers that compute them before the block test
+// is known (k_rollout_pp_full: the consumer wave runs the block test)
+struct TurnC0 {
+  uint32_t Lh, Ll, Ch, Cl;
+  int M, hl0;
+};
+
 // the mover change as selects (no branch): when `flip`
 NARDE_FN void side_flip_if(Side& s, bool flip) {
   Side f = s;

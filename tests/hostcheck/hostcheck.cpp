@@ -1001,3 +1001,179 @@ extern "C" int64_t hc_windows_few_holes_all() {
     bad += (wfh_ref(O, 2) != windows_few_holes(O, 2)) + (wfh_ref(O, 4) != windows_few_holes(O, 4));
   return bad;
 }
+
+// ===========================================================================
+// ply_bound_turn (gym-narde_amd/csrc/full4_wave.h) on 64 emulated lanes
+// (ADVICE r04): the rollout's turn for a wave holding a block-bound doubles
+// lane, compiled for the CPU with its two cross-lane operations emulated --
+// every lane is a host thread, __ballot and __builtin_amdgcn_readlane meet
+// at a 64-thread barrier (each lane publishes its value, all read, all leave)
+// -- and held to env_turn_full (the host turn, itself held to the oracle and
+// full4.npz) lane by lane: C_0 | M, the played sub-moves, reward / done and
+// the post-turn state, on waves mixing block-bound doubles lanes (the
+// f4_safe_bound fast path and the searched ones), block-bound two-dice lanes
+// and free lanes.
+#include <atomic>
+#include <thread>
+#include <vector>
+
+namespace wave_emu {
+// a sense-counting barrier (atomics, yielding spin: 64 threads on a few cores)
+struct Wave {
+  std::atomic<int> arrived{0};
+  std::atomic<uint64_t> gen{0};
+  uint32_t v[64];
+  void sync() {
+    const uint64_t g = gen.load(std::memory_order_acquire);
+    if (arrived.fetch_add(1, std::memory_order_acq_rel) == 63) {
+      arrived.store(0, std::memory_order_relaxed);
+      gen.store(g + 1, std::memory_order_release);
+    } else {
+      while (gen.load(std::memory_order_acquire) == g) std::this_thread::yield();
+    }
+  }
+};
+Wave* g_wave = nullptr;
+thread_local int t_lane = 0;
+inline uint32_t readlane(uint32_t x, int l) {
+  g_wave->v[t_lane] = x;
+  g_wave->sync();
+  const uint32_t r = g_wave->v[l];
+  g_wave->sync();
+  return r;
+}
+inline uint64_t ballot(bool b) {
+  g_wave->v[t_lane] = b ? 1u : 0u;
+  g_wave->sync();
+  uint64_t r = 0;
+  for (int l = 0; l < 64; ++l) r |= (uint64_t)(g_wave->v[l] & 1u) << l;
+  g_wave->sync();
+  return r;
+}
+}  // namespace wave_emu
+
+#define __ballot(x) wave_emu::ballot(x)
+#define __builtin_amdgcn_readlane(x, l) ((int)wave_emu::readlane((uint32_t)(x), (l)))
+#include "../../gym-narde_amd/csrc/full4_wave.h"
+#undef __ballot
+#undef __builtin_amdgcn_readlane
+
+namespace {
+struct Rnd {
+  uint64_t x;
+  uint32_t operator()(uint32_t m) {
+    x ^= x >> 12; x ^= x << 25; x ^= x >> 27;
+    return (uint32_t)(((x * 0x2545F4914F6CDD1Dull) >> 32) % m);
+  }
+};
+
+// a run-heavy position (hc_dbl_bound_w_random's generator): a run of 3-7
+// own points from a random start, the rest of the 15 anywhere, the
+// opponent's 15 mostly above the run
+bool gen_position(Rnd& rnd, Side& s) {
+  s = side_start(0u);
+  for (int k = 0; k < 3; ++k) { s.own.w[k] = 0u; s.opp.w[k] = 0u; }
+  const int r0 = (int)rnd(18), rl = 3 + (int)rnd(5);
+  int left = 15;
+  uint32_t used = 0u;
+  for (int p = r0; p < r0 + rl && p < 24 && left > 0; ++p) {
+    const int c = 1 + (int)rnd(left < 3 ? left : 3);
+    for (int j = 0; j < c; ++j) nib_inc(s.own, p);
+    used |= 1u << p;
+    left -= c;
+  }
+  while (left > 0) {
+    const int p = (int)rnd(24);
+    nib_inc(s.own, p);
+    used |= 1u << p;
+    --left;
+  }
+  int lo = 15;
+  for (int tries = 0; lo > 0 && tries < 1000; ++tries) {
+    const int p = rnd(3) == 0 ? (int)rnd(24) : r0 + (int)rnd(24 - r0);
+    if (p > 23 || ((used >> p) & 1u)) continue;
+    nib_inc(s.opp, p);
+    --lo;
+  }
+  if (lo > 0) return false;
+  s.ft_own = rnd(3) == 0;
+  side_masks(s);
+  return true;
+}
+
+// a lane of the given kind: 0 block-bound doubles, 1 block-bound two dice,
+// 2 anything (random dice)
+void gen_lane(Rnd& rnd, int kind, Side& s, int& dh, int& dl) {
+  for (;;) {
+    if (!gen_position(rnd, s)) continue;
+    int a = 1 + (int)rnd(6), b = 1 + (int)rnd(6);
+    if (kind == 0) b = a;
+    if (kind == 1 && a == b) continue;
+    dh = a > b ? a : b;
+    dl = a > b ? b : a;
+    if (kind == 2) return;
+    uint32_t fw;
+    if (turn_block_set_sl(s.O, s.S1o, s.P, block_lowmask(s.P), dh, dl, fw) != 0u) return;
+  }
+}
+}  // namespace
+
+// `waves` waves of 64 lanes: returns the number of lanes whose result
+// differs; counts[0..3] = block-bound doubles lanes, of them with the full
+// search (not f4_safe_bound's fast path), block-bound two-dice lanes, lanes
+extern "C" int64_t hc_ply_bound_turn_random(int64_t waves, uint32_t seed, int64_t* counts) {
+  Rnd rnd{0x9E3779B97F4A7C15ull ^ ((uint64_t)seed << 17)};
+  int64_t bad = 0;
+  counts[0] = counts[1] = counts[2] = counts[3] = 0;
+  for (int64_t wv = 0; wv < waves; ++wv) {
+    Side s[64], got[64];
+    int dh[64], dl[64];
+    uint32_t w[64][4];
+    TurnOut o[64];
+    for (int l = 0; l < 64; ++l) {
+      const uint32_t u = rnd(8);
+      const int kind = l == 0 ? 0 : (u < 2 ? 0 : (u < 4 ? 1 : 2));
+      gen_lane(rnd, kind, s[l], dh[l], dl[l]);
+      for (int k = 0; k < 4; ++k) w[l][k] = (uint32_t)rnd(0xFFFFFFFFu) ^ ((uint32_t)rnd(65536) << 16);
+    }
+    wave_emu::Wave wave;
+    wave_emu::g_wave = &wave;
+    std::vector<std::thread> th;
+    for (int l = 0; l < 64; ++l) {
+      th.emplace_back([&, l] {
+        wave_emu::t_lane = l;
+        Side x = s[l];
+        uint32_t fw;
+        const uint32_t bs = turn_block_set_sl(x.O, x.S1o, x.P, block_lowmask(x.P), dh[l], dl[l], fw);
+        ply_bound_turn(x, dh[l], dl[l], bs, fw, w[l], false, o[l], l);
+        got[l] = x;
+      });
+    }
+    for (auto& t : th) t.join();
+    wave_emu::g_wave = nullptr;
+    for (int l = 0; l < 64; ++l) {
+      Side e = s[l];
+      TurnOut oe;
+      env_turn_full(e, dh[l], dl[l], false, 0ull, w[l], oe);
+      uint4 a1, b1, a2, b2;
+      side_to_record(got[l], a1, b1);
+      side_to_record(e, a2, b2);
+      const bool same = o[l].legal == oe.legal && o[l].played == oe.played && o[l].term == oe.term &&
+                        o[l].reward == oe.reward && o[l].max_dice == oe.max_dice && a1.x == a2.x &&
+                        a1.y == a2.y && a1.z == a2.z && a1.w == a2.w && b1.x == b2.x && b1.y == b2.y &&
+                        b1.z == b2.z && got[l].O == e.O && got[l].P == e.P && got[l].S1o == e.S1o &&
+                        got[l].S1p == e.S1p;
+      bad += same ? 0 : 1;
+      uint32_t fw;
+      const uint32_t bs = turn_block_set_sl(s[l].O, s[l].S1o, s[l].P, block_lowmask(s[l].P), dh[l], dl[l], fw);
+      const int hl = (s[l].ft_own && (dh[l] == 3 || dh[l] == 4 || dh[l] == 6)) ? 2 : 1;
+      if (bs && dh[l] == dl[l]) {
+        ++counts[0];
+        counts[1] += f4_safe_bound(s[l], dh[l], hl, bs) < 4;
+      }
+      counts[2] += bs && dh[l] != dl[l];
+      ++counts[3];
+    }
+  }
+  return bad;
+}

@@ -378,3 +378,21 @@ def test_hostcheck_windows_few_holes_exhaustive(hostcheck):
     f = hostcheck.hc_windows_few_holes_all
     f.restype = ctypes.c_int64
     assert f() == 0
+
+
+def test_hostcheck_ply_bound_turn_emulated_wave(hostcheck):
+    """ply_bound_turn (full4_wave.h: the rollout's turn for a wave holding a
+    block-bound doubles lane, with the f4_safe_bound fast path, the
+    cooperative search coop_depth_w and the per-sub-move checks) compiled for
+    the CPU with its ballots and readlanes emulated over 64 host threads,
+    lane by lane equal to env_turn_full (C_0 | M, played sub-moves, reward,
+    done, post-turn state) on waves mixing block-bound doubles, block-bound
+    two-dice and free lanes."""
+    f = hostcheck.hc_ply_bound_turn_random
+    f.restype = ctypes.c_int64
+    c = (ctypes.c_int64 * 4)()
+    waves = max(4, 160 // SAN_DIV)
+    assert f(ctypes.c_int64(waves), ctypes.c_uint32(11), c) == 0
+    bd, searched, b2, lanes = list(c)
+    assert lanes == 64 * waves
+    assert bd > 10 * waves and searched > 5 * waves and b2 > 10 * waves

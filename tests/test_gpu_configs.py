@@ -409,7 +409,7 @@ def test_rollout_launch_totals_rows(rules, plies, n):
     statistics after it, summed per 256 envs -- equal to stats() of the same
     handle grouped the same way (and .sum(0) to totals()), for every rollout
     kernel (REF2 producer/consumer at both store policies, FULL4
-    k_rollout_wave) and ragged env counts."""
+    k_rollout_pp_full) and ragged env counts."""
     from gym_narde import _lib
 
     env = vec(n, seed=13, rules=rules)

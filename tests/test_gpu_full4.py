@@ -127,7 +127,7 @@ def test_full4_selfplay_trajectory_vs_oracle(dice_mode, max_steps):
 @pytest.mark.parametrize("max_steps", [1000, 30])
 def test_full4_rollout_equals_steps(max_steps):
     """narde_rollout_full over launch boundaries == per-ply k_step<full>:
-    launches of 1, 29, 70 and 100 plies (k_rollout_wave), ragged odd n (the
+    launches of 1, 29, 70 and 100 plies (k_rollout_pp_full), ragged odd n (the
     last workgroup partly empty, odd plies' rows not 64-B aligned); with
     TimeLimit 30 every env truncates several times inside the launches."""
     n, seed = 2048 + 77, 31337
@@ -156,7 +156,7 @@ def test_full4_rollout_equals_steps(max_steps):
 @pytest.mark.parametrize("plies", [120, 20])
 def test_full4_full_batch_window_and_invariants(plies):
     """B = 65,536 (the bench shape; 120-ply launches, and the driver's 20-ply
-    launch; k_rollout_wave): a 2,048-env window equals the
+    launch; k_rollout_pp_full): a 2,048-env window equals the
     oracle run on those global ids; checker conservation and played == max
     dice everywhere."""
     n, seed = 65536, 7
@@ -213,7 +213,7 @@ def test_full4_steady_state_window_after_selfplay():
 def test_tiny_batches_both_rules_both_kernels(n):
     """One env, one wave less one lane, one wave plus one lane: REF2 rollouts
     of 20 plies (k_rollout_pc<true, true>: non-temporal stores) and 60 plies
-    (<true, false>), FULL4 rollouts of 20 and 60 plies (k_rollout_wave)
+    (<true, false>), FULL4 rollouts of 20 and 60 plies (k_rollout_pp_full)
     equal the oracle ply for ply."""
     from gym_narde.vector import VecNardeEnv
 

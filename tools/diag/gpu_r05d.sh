@@ -31,7 +31,9 @@ sq_pass() {  # rules plies kernel name
         > "$OUT/$name.log" 2>&1) \
   && python3 tools/sq_summary.py --dir "$OUT/$name" --kernel "$kernel" --plies "$plies" --out "$OUT/$name.json"
 }
-echo "[$TAG] $(date +%T) issue probe" \
+echo "[$TAG] $(date +%T) pytest -m gpu" \
+  && timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1 \
+  && echo "[$TAG] $(date +%T) issue probe" \
   && timeout -k 10 300 python3 tools/issue_probe.py --out $OUT/issue_probe.json > $OUT/issue_probe.log 2>&1 \
   && (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
         --output-format csv -d $OUT/issue_probe_sq -o sq -- python3 $ROOT/tools/issue_probe.py --iters 2000 \
@@ -45,7 +47,7 @@ echo "[$TAG] $(date +%T) issue probe" \
   && (cd /tmp && timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/api_trace" -o api \
         -- python3 "$ROOT/tools/api_target.py" > "$OUT/api_trace.log" 2>&1)
 rc=$?
-tail -1 $OUT/issue_probe.log | cut -c1-200; cat $OUT/api.json
+tail -3 $OUT/pytest_gpu.log; tail -1 $OUT/issue_probe.log | cut -c1-200; cat $OUT/api.json
 grep -ho '"traffic_over_algorithmic": [0-9.]*\|"valu_per_env_ply": [0-9.]*\|"frac_at_profiled_duration": [0-9.]*' $OUT/*.json
 echo "[$TAG] rc=$rc"
 exit $rc

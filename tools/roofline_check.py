@@ -8,7 +8,8 @@ recomputes, from profiles/:
     8 TB/s, and the PMC traffic of profiles/pmc_k_rollout[_full][_p<P>].json;
   * the issue figure: VALU wave-instructions per launch from
     profiles/sq_k_rollout[_full]_p<P>.json / kernel_ms / the 1,024-SIMD
-    integer issue peak (tools/sq_summary.py),
+    integer issue peak of one VALU wave-instruction per 4 cycles
+    (tools/sq_summary.py; measured in profiles/r05/issue_probe/),
 for the headline (`roofline`) and `other_rules`, and prints them beside
 the line's own numbers.  Exit status 1 if any recomputed fraction differs
 from the line's by more than 1e-3.
@@ -19,7 +20,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HBM_PEAK = 8.0e12
-ISSUE_PEAK = 1024 * 2.4e9 / 4
+ISSUE_PEAK = 1024 * 2.4e9 / 4  # basis: profiles/r05/issue_probe/summary.json (tools/sq_summary.py)
 
 
 def bytes_per_launch(envs, plies, full):

@@ -14,7 +14,8 @@ OUT=build/sanitize
 mkdir -p "$OUT"
 SAN="-fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g -O1"
 $CLANG $SAN -std=c99 -fPIC -shared -o "$OUT/libnarde_oracle_san.so" oracle/narde_oracle.c
-$HIPCC -std=c++17 -fPIC -shared -Xarch_host -fsanitize=address,undefined -Xarch_host -fno-sanitize-recover=undefined \
+$HIPCC -std=c++17 -fPIC -shared -x c++ -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include \
+  -Xarch_host -fsanitize=address,undefined -Xarch_host -fno-sanitize-recover=undefined \
   -fno-gpu-sanitize -fno-omit-frame-pointer -g -O1 -o "$OUT/libhostcheck_san.so" tests/hostcheck/hostcheck.cpp
 export NARDE_ORACLE_LIB=$PWD/$OUT/libnarde_oracle_san.so
 export NARDE_HOSTCHECK_LIB=$PWD/$OUT/libhostcheck_san.so

@@ -13,14 +13,24 @@ averages per launch.  SQ_INSTS_* count wave-instructions; SQ_WAVE_CYCLES,
 SQ_WAIT_* and SQ_ACTIVE_INST_* count quad-cycles (MI355X_MICROARCH.md,
 constants table).
 
-The issue peak: this integer code issues at most one vector instruction per
-4 cycles per SIMD -- one wave alone issues one per 4 cycles
-(MI355X_MICROARCH.md, row 'vector-instruction ISSUE cost'), and a second
-wave per SIMD added 7 % on independent integer chains
-(tools/diag/halfwave.hip) -- so
-  peak = 1,024 SIMDs x 2.4 GHz / 4 = 6.144e11 VALU wave-instructions/s,
-and bench.py's `roofline.issue.frac` = (VALU wave-instructions per launch,
-from this file) / (the launch's live duration) / peak.
+The issue peak (measured, profiles/r05/issue_probe/summary.json from
+tools/issue_probe.hip: every VALU kind the rules engine uses, at 1, 2 and 4
+waves per SIMD, shader-clock cycles per wave and SQ_BUSY_CYCLES):
+  * one wave alone issues a VALU instruction at most every 4 cycles,
+    whatever the kind -- the bound of every kernel's rule wave (one per
+    SIMD at B = 65,536: 64 envs a wave, 1,024 SIMDs);
+  * two or more waves on a SIMD share it at 4 cycles per instruction for the
+    "slow" kinds (shift left, bfe, add3, and_or / or3 / lshl_or, cndmask
+    e64, bcnt, ffbl, min / max, perm, SDWA, mul) and at 2 cycles for the
+    "fast" kinds (add / sub, and / or / xor / not, bitop3, shift right,
+    f32 add / fma) -- MI355X_MICROARCH.md's "2 cycles (SIMD-32)" holds for
+    the fast kinds only, and only across waves.
+So peak = 1,024 SIMDs x 2.4 GHz / 4 = 6.144e11 VALU wave-instructions/s
+(`issue_peak_basis`); a two-wave kernel (the producer/consumer rollouts)
+could go up to 2x that on fast-class instructions, which bench.py reports
+beside it (`roofline.issue.frac_of_two_wave_fast_peak`).  bench.py's
+`roofline.issue.frac` = (VALU wave-instructions per launch, from this file)
+/ (the launch's live duration) / peak.
 """
 import argparse
 import csv
@@ -68,7 +78,9 @@ def summarise(root, kernel, envs, plies):
         "salu_per_launch": round(salu),
         "valu_per_env_ply": round(valu / (envs * plies) * 64, 1) if valu else None,  # per 64-env wave-ply
         "issue_peak_valu_per_s": ISSUE_PEAK,
-        "issue_peak_basis": f"{SIMDS} SIMDs x {CLOCK_HZ / 1e9} GHz / {CYCLES_PER_VALU} cycles per VALU wave-instruction",
+        "issue_peak_basis": f"{SIMDS} SIMDs x {CLOCK_HZ / 1e9} GHz / {CYCLES_PER_VALU} cycles per VALU wave-instruction "
+                            "(one wave's rate, any kind; two waves' rate on the slow kinds: "
+                            "profiles/r05/issue_probe/summary.json)",
         "profiled_duration_us": round(sum(dur[1:]) / len(dur[1:]) / 1e3, 2),
     }
     if valu and wave_cycles:
