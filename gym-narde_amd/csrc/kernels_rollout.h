@@ -694,7 +694,8 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
 // at a 96-B lane stride) is retired; git history has it.
 //   producer, ply p: wait until drawn > p and emitted + kPpR > p, play the
 //     turn with the words of draw slot p % kPpR, leave the results in result
-//     slot p % kPpR, then produced = p + 1;
+//     slot p % kPpR; produced = p + 1 is published early in ply p + 1 (and
+//     after the last ply);
 //   consumer: draws plies 0 .. kPpR - 1 ahead; for each ply p: wait until
 //     produced > p, store ply p's outputs, then emitted = p + 1 (the result
 //     slot is free), draw ply p + kPpR into the draw slot ply p used (read
@@ -726,11 +727,17 @@ __device__ __forceinline__ void pp_publish(uint32_t* c, uint32_t v) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __hip_atomic_store(c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// spin until f(counter value) holds (wave-uniform), then acquire
-template <class F>
-__device__ __forceinline__ void pp_wait(const uint32_t* c, F ok) {
-  while (!ok(pp_load(c))) __builtin_amdgcn_s_sleep(1);
+// spin until f(counter value) holds (wave-uniform), then acquire; returns
+// the value seen.  kSleep: s_sleep units (64 cycles) between polls -- 1 for
+// the producer, longer for the consumer, whose polls would otherwise take
+// the producer's issue slots (both waves share a SIMD) while it waits a
+// whole turn
+template <int kSleep, class F>
+__device__ __forceinline__ uint32_t pp_wait(const uint32_t* c, F ok) {
+  uint32_t v;
+  while (!ok(v = pp_load(c))) __builtin_amdgcn_s_sleep(kSleep);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  return v;
 }
 
 // obs quad qq of env el of pair cw, ring slot sl (pc_obs_quad's layout)
@@ -826,14 +833,22 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pp_full(Planes pl, int n
   int4 st = make_int4(0, 0, 0, 0);
   if (producer) {
     Side s = valid ? side_from_record(pl.p0[i], pl.p1[i]) : side_start(0u);
+    // the counters as last seen: a poll (an LDS round trip) only when ply p
+    // is past them -- the consumer runs up to kPpR plies ahead
+    uint32_t dk = 0u, ek = 0u;
     for (int p = 0; p < plies; ++p) {
       const uint32_t up = (uint32_t)p;
       const int sl = p % kPpR;
-      pp_wait(&L.drawn[cw], [&](uint32_t v) { return v > up; });
-      if (kOut && p >= kPpR) pp_wait(&L.emitted[cw], [&](uint32_t v) { return v + (uint32_t)kPpR > up; });
+      if (up >= dk) dk = pp_wait<1>(&L.drawn[cw], [&](uint32_t v) { return v > up; });
+      if (kOut && up >= ek + (uint32_t)kPpR)
+        ek = pp_wait<1>(&L.emitted[cw], [&](uint32_t v) { return v + (uint32_t)kPpR > up; });
       const uint2 rv = L.draw[cw][sl][lane];
       uint32_t r[4];
       ply_words(rv.x, rv.y, g.dice_mode, r);
+      // ply p - 1's results, published here: its LDS writes are long done
+      // and the release's wait covers only this ply's draw read, which the
+      // words above waited for anyway
+      if (p > 0) pp_publish(&L.produced[cw], up);
       TurnOut o;
       int term, trunc;
       ply_full_words(s, st, r, g.dice_mode, max_steps, true, o, term, trunc);
@@ -844,8 +859,8 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pp_full(Planes pl, int n
         L.played[cw][sl][lane] = make_uint2((uint32_t)o.played, (uint32_t)(o.played >> 32));
         L.rtt[cw][sl][lane] = (uint32_t)o.reward | ((uint32_t)term << 8) | ((uint32_t)trunc << 16);
       }
-      pp_publish(&L.produced[cw], up + 1u);
     }
+    pp_publish(&L.produced[cw], (uint32_t)plies);
     if (valid) {
       uint4 ra, rb;
       side_to_record(s, ra, rb);
@@ -867,7 +882,7 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pp_full(Planes pl, int n
     }
     for (int p = 0; p < plies; ++p) {
       const uint32_t up = (uint32_t)p;
-      pp_wait(&L.produced[cw], [&](uint32_t v) { return v > up; });
+      pp_wait<8>(&L.produced[cw], [&](uint32_t v) { return v > up; });
       if (kOut) {
         pp_emit_ply<kNt>(L, cw, p % kPpR, p, n, g0, lane, out);
         pp_publish(&L.emitted[cw], up + 1u);
