@@ -683,7 +683,11 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
 // producer wave (waves 0-3) has its own consumer wave (waves 4-7) and a ring
 // of kPpR ply slots in LDS (draws and results); the pair hands plies over
 // through three LDS counters instead of workgroup barriers, so a producer
-// never waits for the other producers of its workgroup -- FULL4's turns vary
+// never waits for the other producers of its workgroup (REF2 stays with
+// k_rollout_pc: its plies are short and even, and the same pairwise kernel
+// playing REF2 plies ran 0.196 / 0.140 against k_rollout_pc's 0.160 / 0.126
+// ms per 100 plies at 20 / 1,000 plies, 44.1 against 37.6 us at the
+// driver's shape, profiles/r05/ab/*ref2_pc_vs_pairwise*) -- FULL4's turns vary
 // several-fold in cost from ply to ply (block-bound plies, DESIGN.md
 // section 10), and k_rollout_pc's one barrier per block of plies made every
 // producer wait for the slowest of four (the same kernel with barrier

@@ -6,7 +6,7 @@
 # so the first failure ends the call.  PMC / SQ passes are separate
 # rocprofv3 runs, never combined with tracing domains (MI355X_MICROARCH.md).
 set -o pipefail
-TAG=${1:-r04}
+TAG=${1:-r05}
 PHASE=${2:-run}
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out/$TAG
@@ -74,6 +74,10 @@ else
     && sq_pass full4 20 "k_rollout_pp_full<true, true>" sq_k_rollout_full_p20 \
     && sq_pass ref2 1000 "k_rollout_pc<true, false>" sq_k_rollout_p1000 \
     && sq_pass full4 1000 "k_rollout_pp_full<true, false>" sq_k_rollout_full_p1000 \
+    && echo "[gpu_round] $(date +%T) DQN driver (configs[3]) traced" \
+    && (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/dqn_trace" -o dqn \
+          -- python3 "$ROOT/tools/dqn_target.py" 65536 20 > "$OUT/dqn_trace.log" 2>&1) \
+    && python3 tools/dqn_breakdown.py "$OUT/dqn_trace" --out "$OUT/dqn_breakdown.json" \
     && echo "[gpu_round] $(date +%T) api kernels (timed, traced)" \
     && timeout -k 10 120 python3 tools/api_target.py > "$OUT/api.json" \
     && (cd /tmp && timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/api_trace" -o api \
