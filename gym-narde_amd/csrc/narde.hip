@@ -97,14 +97,18 @@ Rng rng_of(const narde_env* e) {
   return g;
 }
 
+// the handle's device for the call; the caller's restored after it (no
+// runtime call on the way out when they are the same -- the usual case, and
+// the timed launch's host path)
 struct DeviceGuard {
   int prev = -1;
+  bool switched = false;
   explicit DeviceGuard(int d) {
     if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-    if (prev != d) (void)hipSetDevice(d);
+    if (prev != d) switched = hipSetDevice(d) == hipSuccess;
   }
   ~DeviceGuard() {
-    if (prev >= 0) (void)hipSetDevice(prev);
+    if (switched && prev >= 0) (void)hipSetDevice(prev);
   }
 };
 
