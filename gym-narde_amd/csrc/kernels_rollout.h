@@ -486,6 +486,18 @@ typedef unsigned pc_v2u __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t pc_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
 }
+// pc_rsrc with the base and extent passed through v_readfirstlane: both are
+// wave-uniform, but where the compiler cannot prove it (k_rollout_pp_full's
+// consumer) it keeps the resource in VGPRs and wraps every store in a
+// readfirstlane / compare / exec loop (11 per ply there, ~80 VALU of the
+// kernel); k_rollout_pc's consumer needs no help (its form would add VALU)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pc_rsrc_u(const void* base, uint32_t bytes) {
+  const uint64_t a = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32));
+  void* ub = reinterpret_cast<void*>((uint64_t)lo | ((uint64_t)hi << 32));
+  return __builtin_amdgcn_make_buffer_rsrc(ub, (short)0, __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
+}
 __device__ __forceinline__ void pc_st16(__amdgpu_buffer_rsrc_t r, uint32_t off, int4 v) {
   const pc_v4i x = {v.x, v.y, v.z, v.w};
   __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)off, 0, 2);
@@ -768,7 +780,7 @@ __device__ __forceinline__ void pp_emit_ply(const PpLds& L, int cw, int sl, int 
   if constexpr (kNt) {
     const uint32_t nw = (uint32_t)max(0, min(64, n - g0));
     if (out.obs) {
-      const __amdgpu_buffer_rsrc_t r = pc_rsrc(out.obs + row0 * 24, nw * 96u);
+      const __amdgpu_buffer_rsrc_t r = pc_rsrc_u(out.obs + row0 * 24, nw * 96u);
 #pragma unroll
       for (int q = 0; q < 6; ++q) {
         const int j = lane + 64 * q;
@@ -778,16 +790,16 @@ __device__ __forceinline__ void pp_emit_ply(const PpLds& L, int cw, int sl, int 
     }
     const uint32_t c = L.rtt[cw][sl][lane];
     const uint32_t l = (uint32_t)lane;
-    if (out.reward) pc_st4(pc_rsrc(out.reward + row0, nw * 4u), 4u * l, c & 0xFFu);
-    if (out.term) pc_st1(pc_rsrc(out.term + row0, nw), l, (uint8_t)((c >> 8) & 1u));
-    if (out.trunc) pc_st1(pc_rsrc(out.trunc + row0, nw), l, (uint8_t)((c >> 16) & 1u));
+    if (out.reward) pc_st4(pc_rsrc_u(out.reward + row0, nw * 4u), 4u * l, c & 0xFFu);
+    if (out.term) pc_st1(pc_rsrc_u(out.term + row0, nw), l, (uint8_t)((c >> 8) & 1u));
+    if (out.trunc) pc_st1(pc_rsrc_u(out.trunc + row0, nw), l, (uint8_t)((c >> 16) & 1u));
     if (out.legal) {
       const uint2 lg = L.legal[cw][sl][lane];
-      pc_st8(pc_rsrc(out.legal + row0, nw * 8u), 8u * l, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
+      pc_st8(pc_rsrc_u(out.legal + row0, nw * 8u), 8u * l, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
     }
     if (out.played) {
       const uint2 pw = L.played[cw][sl][lane];
-      pc_st8(pc_rsrc(out.played + row0, nw * 8u), 8u * l, (uint64_t)pw.x | ((uint64_t)pw.y << 32));
+      pc_st8(pc_rsrc_u(out.played + row0, nw * 8u), 8u * l, (uint64_t)pw.x | ((uint64_t)pw.y << 32));
     }
   } else {
     if (out.obs) {
