@@ -241,12 +241,12 @@ __device__ __forceinline__ void ply_free_turn(Side& s, int dh, int dl, uint32_t 
 }
 
 // the turn and the end of the ply once the block test (bs, fw) and
-// turn_c0_free's results (c) are known; every lane of the wave must call it
+// turn_c0_free's results (c) are known; w = turn_words of the ply's words r,
+// rb = reset_black(r[3]) (auto-reset only); every lane of the wave must call
+// it
 __device__ __forceinline__ void ply_full_turn(Side& s, int4& st, int dh, int dl, uint32_t bs, uint32_t fw,
-                                              const TurnC0& c, const uint32_t r[4], int max_steps, bool autoreset,
-                                              TurnOut& o, int& term, int& trunc) {
-  uint32_t w[4];
-  turn_words(r, w);
+                                              const TurnC0& c, const uint32_t w[4], uint32_t rb, int max_steps,
+                                              bool autoreset, TurnOut& o, int& term, int& trunc) {
   const uint32_t mover_black = s.black;
   // three kinds of wave (one instruction stream each): no block-bound
   // lane, block-bound two-dice lanes only, a block-bound doubles lane
@@ -258,8 +258,31 @@ __device__ __forceinline__ void ply_full_turn(Side& s, int4& st, int dh, int dl,
   } else {
     ply_bound_turn_c0(s, dh, dl, bs, fw, w, autoreset, o, (int)(threadIdx.x & 63), c);
   }
-  if (autoreset) ply_close_sl(s, st, o.term, o.reward, mover_black, r[3], max_steps, term, trunc);
-  else ply_close(s, st, o.term, o.reward, mover_black, r[3], max_steps, false, term, trunc);
+  if (autoreset) ply_close_sl_b(s, st, o.term, o.reward, mover_black, rb, max_steps, term, trunc);
+  else ply_close(s, st, o.term, o.reward, mover_black, 0u, max_steps, false, term, trunc);
+}
+
+// the ply from what its words give (dice dh >= dl, the pick words w, the
+// auto-reset side rb); every lane of the wave must call it
+__device__ __forceinline__ void ply_full_dice(Side& s, int4& st, int dh, int dl, const uint32_t w[4], uint32_t rb,
+                                              int max_steps, bool autoreset, TurnOut& o, int& term, int& trunc) {
+  const uint32_t low = block_lowmask(s.P);
+  uint32_t fw;
+  const uint32_t bs = turn_block_set_sl(s.O, s.S1o, s.P, low, dh, dl, fw);
+  TurnC0 c;
+  turn_c0_free(s, dh, dl, c.Lh, c.Ll, c.Ch, c.Cl, c.M, c.hl0);
+  ply_full_turn(s, st, dh, dl, bs, fw, c, w, rb, max_steps, autoreset, o, term, trunc);
+}
+
+// what a ply's words r give ply_full_dice, packed: dh | dl << 4 | rb << 8
+// (and the pick words w) -- computed by the rollout's consumer wave, off the
+// turn's stream
+__device__ __forceinline__ uint32_t ply_dice_word(const uint32_t r[4], int dice_mode, uint32_t w[4]) {
+  int d0, d1;
+  dice_from(r[0], dice_mode, d0, d1);
+  const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
+  turn_words(r, w);
+  return (uint32_t)dh | ((uint32_t)dl << 4) | (reset_black(r[3]) << 8);
 }
 
 // the ply with its words r already drawn (ply_words); every lane of the wave
@@ -267,15 +290,10 @@ __device__ __forceinline__ void ply_full_turn(Side& s, int4& st, int dh, int dl,
 __device__ __forceinline__ void ply_full_words(Side& s, int4& st, const uint32_t r[4], int dice_mode,
                                                int max_steps, bool autoreset, TurnOut& o, int& term,
                                                int& trunc) {
-  int d0, d1;
-  dice_from(r[0], dice_mode, d0, d1);
-  const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
-  const uint32_t low = block_lowmask(s.P);
-  uint32_t fw;
-  const uint32_t bs = turn_block_set_sl(s.O, s.S1o, s.P, low, dh, dl, fw);
-  TurnC0 c;
-  turn_c0_free(s, dh, dl, c.Lh, c.Ll, c.Ch, c.Cl, c.M, c.hl0);
-  ply_full_turn(s, st, dh, dl, bs, fw, c, r, max_steps, autoreset, o, term, trunc);
+  uint32_t w[4];
+  const uint32_t dw = ply_dice_word(r, dice_mode, w);
+  ply_full_dice(s, st, (int)(dw & 15u), (int)((dw >> 4) & 15u), w, autoreset ? dw >> 8 : 0u, max_steps, autoreset,
+                o, term, trunc);
 }
 
 __device__ __forceinline__ void ply_policy_full(Side& s, int4& st, const Rng& g, uint32_t i, int max_steps,
@@ -715,7 +733,11 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
 //   consumer: draws plies 0 .. kPpR - 1 ahead; for each ply p: wait until
 //     produced > p, store ply p's outputs, then emitted = p + 1 (the result
 //     slot is free), draw ply p + kPpR into the draw slot ply p used (read
-//     before ply p was produced), then drawn = p + kPpR + 1.
+//     before ply p was produced), then drawn = p + kPpR + 1.  A draw is the
+//     Philox words and what the turn takes from them (ply_dice_word: the
+//     dice, the pick words, the auto-reset side), so that work is off the
+//     producer's stream (20 plies 0.371 -> 0.364, 1,000 plies 0.259 -> 0.254
+//     ms per 100 plies).
 // (Measured and not kept: the consumer running each ply's block test
 // (turn_block_set_sl on the masks the previous ply left) while the
 // producer computes C_0 -- the producer then waits for it: 20-ply launches
@@ -727,7 +749,8 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
 constexpr int kPpR = 8;  // ring depth in plies
 
 struct PpLds {
-  uint2 draw[kPcGroups][kPpR][64];
+  uint4 draw_w[kPcGroups][kPpR][64];   // the ply's pick words (turn_words)
+  uint32_t draw_d[kPcGroups][kPpR][64];  // ply_dice_word: dh | dl << 4 | reset side << 8
   uint4 nib0[kPcGroups][kPpR][64];
   uint2 nib1[kPcGroups][kPpR][64];
   uint2 legal[kPcGroups][kPpR][64];
@@ -858,16 +881,16 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pp_full(Planes pl, int n
       if (up >= dk) dk = pp_wait<1>(&L.drawn[cw], [&](uint32_t v) { return v > up; });
       if (kOut && up >= ek + (uint32_t)kPpR)
         ek = pp_wait<1>(&L.emitted[cw], [&](uint32_t v) { return v + (uint32_t)kPpR > up; });
-      const uint2 rv = L.draw[cw][sl][lane];
-      uint32_t r[4];
-      ply_words(rv.x, rv.y, g.dice_mode, r);
+      const uint4 wv = L.draw_w[cw][sl][lane];
+      const uint32_t dw = L.draw_d[cw][sl][lane];
+      const uint32_t w[4] = {wv.x, wv.y, wv.z, wv.w};
       // ply p - 1's results, published here: its LDS writes are long done
-      // and the release's wait covers only this ply's draw read, which the
-      // words above waited for anyway
+      // and the release's wait covers only this ply's draw reads, which the
+      // turn needs at once anyway
       if (p > 0) pp_publish(&L.produced[cw], up);
       TurnOut o;
       int term, trunc;
-      ply_full_words(s, st, r, g.dice_mode, max_steps, true, o, term, trunc);
+      ply_full_dice(s, st, (int)(dw & 15u), (int)((dw >> 4) & 15u), w, dw >> 8, max_steps, true, o, term, trunc);
       if (kOut) {
         L.nib0[cw][sl][lane] = make_uint4(s.own.w[0], s.own.w[1], s.own.w[2], s.opp.w[0]);
         L.nib1[cw][sl][lane] = make_uint2(s.opp.w[1], s.opp.w[2]);
@@ -886,10 +909,15 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pp_full(Planes pl, int n
   } else {
     const uint32_t t0 = valid ? pl.p1[i].w : 0u;
     uint32_t R[4];  // the Philox block of the last ply drawn (one block per ply pair)
+    // the words of ply p, and what the turn takes from them (ply_dice_word)
     auto draw = [&](int p) {
       const uint32_t t = t0 + (uint32_t)p;
       if (p == 0 || (t & 1u) == 0u) ply_block(t, g.env0 + (uint32_t)i, g.k0, g.k1, R);
-      L.draw[cw][p % kPpR][lane] = (t & 1u) ? make_uint2(R[2], R[3]) : make_uint2(R[0], R[1]);
+      uint32_t r[4], w[4];
+      ply_words_of(R, t, g.dice_mode, r);
+      const uint32_t dw = ply_dice_word(r, g.dice_mode, w);
+      L.draw_w[cw][p % kPpR][lane] = make_uint4(w[0], w[1], w[2], w[3]);
+      L.draw_d[cw][p % kPpR][lane] = dw;
     };
     const int ahead = min(kPpR, plies);
     for (int p = 0; p < ahead; ++p) {  // each ply's words published as drawn: ply 0 starts at once

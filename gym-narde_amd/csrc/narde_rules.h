@@ -1875,11 +1875,13 @@ NARDE_FN void dice_from(uint32_t r, int dice_mode, int& d0, int& d1) {
 
 // opening roll (narde_env.py:111-117): uniform over the 30 unequal ordered
 // pairs (same law as the reference's redraw loop); higher roll = white moves
-NARDE_FN Side side_reset(uint32_t r) {
+// first.  reset_black: the side to move of the new episode (1 = black)
+NARDE_FN uint32_t reset_black(uint32_t r) {
   int w, b;
   dice_from(r, 1, w, b);
-  return side_start(w > b ? 0u : 1u);
+  return w > b ? 0u : 1u;
 }
+NARDE_FN Side side_reset(uint32_t r) { return side_start(reset_black(r)); }
 
 // The ply stream.  One Philox4x32-10 block serves two
 // consecutive plies of an env: R = Philox(ctr = {t >> 1, env, 0, 0}); ply t
@@ -1931,9 +1933,10 @@ NARDE_FN void ply_close(Side& s, int4& st, int o_term, int o_reward, uint32_t mo
   s.t += 1u;
 }
 
-// ply_close with auto-reset as selects (the reset state is mostly constants)
-NARDE_FN void ply_close_sl(Side& s, int4& st, int o_term, int o_reward, uint32_t mover_black, uint32_t r3,
-                           int max_steps, int& term, int& trunc) {
+// ply_close with auto-reset as selects (the reset state is mostly constants);
+// rb = reset_black(r3) of the ply's words
+NARDE_FN void ply_close_sl_b(Side& s, int4& st, int o_term, int o_reward, uint32_t mover_black, uint32_t rb,
+                             int max_steps, int& term, int& trunc) {
   s.elapsed += 1u;
   term = o_term;
   trunc = max_steps > 0 && s.elapsed >= (uint32_t)max_steps;
@@ -1941,7 +1944,7 @@ NARDE_FN void ply_close_sl(Side& s, int4& st, int o_term, int o_reward, uint32_t
   st.x += end ? 1 : 0;
   st.y += (term && !mover_black) ? o_reward : 0;
   st.z += (term && mover_black) ? o_reward : 0;
-  const Side r = side_reset(r3);
+  const Side r = side_start(rb);
   s.own.w[0] = end ? r.own.w[0] : s.own.w[0];
   s.own.w[1] = end ? r.own.w[1] : s.own.w[1];
   s.own.w[2] = end ? r.own.w[2] : s.own.w[2];
@@ -1959,6 +1962,10 @@ NARDE_FN void ply_close_sl(Side& s, int4& st, int o_term, int o_reward, uint32_t
   s.black = end ? r.black : s.black;
   s.elapsed = end ? 0u : s.elapsed;
   s.t += 1u;
+}
+NARDE_FN void ply_close_sl(Side& s, int4& st, int o_term, int o_reward, uint32_t mover_black, uint32_t r3,
+                           int max_steps, int& term, int& trunc) {
+  ply_close_sl_b(s, st, o_term, o_reward, mover_black, reset_black(r3), max_steps, term, trunc);
 }
 
 // the four pick words of a FULL4 turn (see env_ply_full_with)
