@@ -153,6 +153,34 @@ def test_full4_rollout_equals_steps(max_steps):
         assert got["truncated"].sum() > n  # truncations inside the rollout launches
 
 
+def test_full4_rollout_ring_boundaries():
+    """k_rollout_pp_full launches at the edges of its hand-over: lengths
+    around the LDS ring depth (kPpR = 8 plies: 7, 8, 9, 16, 17; the consumer
+    draws min(8, plies) ahead) and on both sides of the store-policy switch
+    (32 plies non-temporal, 33 plain), n = 300 (a full workgroup and a
+    partial one) == per-ply k_step<full>, entry by entry."""
+    n, seed = 300, 4242
+    lens = (7, 8, 9, 16, 17, 32, 33)
+    a = vec(n, seed=seed)
+    b = vec(n, seed=seed)
+    bufs = a.rollout_buffers(max(lens))
+    got = {k: [] for k in bufs}
+    for plies in lens:
+        a.rollout(plies, bufs)
+        for k, v in bufs.items():
+            got[k].append(np_(v[:plies]).copy())
+    got = {k: np.concatenate(v) for k, v in got.items()}
+    for p in range(sum(lens)):
+        obs, rew, term, trunc, info = b.step()
+        assert np.array_equal(got["obs"][p], np_(obs)), p
+        assert np.array_equal(got["reward"][p], np_(rew)), p
+        assert np.array_equal(got["terminated"][p], np_(term)), p
+        assert np.array_equal(got["truncated"][p], np_(trunc)), p
+        assert np.array_equal(got["legal"][p], np_(info["legal"])), p
+        assert np.array_equal(got["actions"][p], np_(info["played"])), p
+    assert np.array_equal(np_(a.stats()), np_(b.stats()))
+
+
 @pytest.mark.parametrize("plies", [120, 20])
 def test_full4_full_batch_window_and_invariants(plies):
     """B = 65,536 (the bench shape; 120-ply launches, and the driver's 20-ply

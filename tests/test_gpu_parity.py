@@ -184,6 +184,28 @@ def test_rollout_vs_oracle_and_step(n):
     assert env.ply == 320
 
 
+def test_rollout_block_boundaries_vs_oracle():
+    """k_rollout_pc launches at the edges of its barrier blocks (blocks of 1,
+    2, then 4 plies: launches of 2, 3, 4, 5 and 7 plies end in each kind of
+    block) and on both sides of the store-policy switch (32 plies
+    non-temporal, 33 plain), n = 300 (a full workgroup and a partial one):
+    every output and list #1 of every ply == the oracle's."""
+    n, seed, env0 = 300, 0x5EED, 91
+    env = vec(n, seed=seed, env_id_offset=env0)
+    ref = O.SelfPlay(n, seed=seed, env0=env0)
+    ref.reset(0)
+    for plies in (2, 3, 4, 5, 7, 32, 33):
+        rec = ref.run(plies)
+        bufs = env.rollout(plies)
+        assert np.array_equal(np_(bufs["obs"]), rec["obs"].astype(np.int32)), plies
+        assert np.array_equal(np_(bufs["reward"]), rec["reward"].astype(np.int32)), plies
+        assert np.array_equal(np_(bufs["terminated"]), rec["terminated"]), plies
+        assert np.array_equal(np_(bufs["truncated"]), rec["truncated"]), plies
+        assert np.array_equal(np_(bufs["actions"]), rec["action"]), plies
+        assert np.array_equal(np_(bufs["legal"]).view(np.uint64), rec["legal"]), plies
+    assert np.array_equal(np_(env.stats()), ref.stats)
+
+
 @pytest.mark.parametrize("rules", ["ref2", "full4"])
 @pytest.mark.parametrize("n", [37, 130, 4097])
 def test_rollout_writes_only_its_buffers(rules, n):
