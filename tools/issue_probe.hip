@@ -75,6 +75,17 @@ KIND(k_add_f32, asm volatile("v_add_f32 %0, %0, %1" : "+v"(a) : "v"(b)))
 KIND(k_pk_add_u16, asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(a) : "v"(b)))
 KIND(k_mul_u32_u24, asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a) : "v"(b)))
 
+// scalar instructions beside the VALU stream of one wave (round 5): what an
+// SALU instruction, a lane-mask combine, a not-taken and a taken branch cost
+// a lone wave between its VALU instructions
+KIND(k_add_sadd, asm volatile("v_add_u32 %0, %0, %1\n\ts_add_u32 s8, s8, 1" : "+v"(a) : "v"(b) : "s8", "scc"))
+KIND(k_add_sand64, asm volatile("v_add_u32 %0, %0, %1\n\ts_and_b64 s[8:9], s[8:9], s[10:11]"
+                                : "+v"(a) : "v"(b) : "s8", "s9", "scc"))
+KIND(k_sadd_only, asm volatile("s_add_u32 s8, s8, 1" : : : "s8", "scc"))
+KIND(k_add_cbranch_nt, asm volatile("v_add_u32 %0, %0, %1\n\ts_cmp_eq_u32 s8, 0x12345\n\ts_cbranch_scc1 1f\n1:"
+                                    : "+v"(a) : "v"(b) : "scc"))
+KIND(k_add_branch_taken, asm volatile("v_add_u32 %0, %0, %1\n\ts_branch 1f\n1:" : "+v"(a) : "v"(b)))
+
 // 64-bit kinds: a 64-bit accumulator, so the register pair is exact (the
 // mad's carry-out goes to one SGPR pair, as the product's Philox and mulhi
 // code does).  The compiler puts an s_nop after each carry / compare write
@@ -240,6 +251,27 @@ void one(const char* name, uint32_t* d, Clock* dclk, int iters, bool& first) {
 }
 
 }  // namespace
+
+// the scalar kinds alone (tools/issue_probe.py --scalar)
+extern "C" int issue_probe_scalar(int iters) {
+  uint32_t* d;
+  Clock* dclk;
+  if (hipMalloc(&d, 256 * 1024 * sizeof(uint32_t)) != hipSuccess) return 1;
+  if (hipMalloc(&dclk, 256 * 16 * sizeof(Clock)) != hipSuccess) return 1;
+  bool first = true;
+  std::printf("[\n");
+  one<k_add_u32, false>("v_add_u32", d, dclk, iters, first);
+  one<k_add_sadd, false>("v_add_u32+s_add_u32", d, dclk, iters, first);
+  one<k_add_sand64, false>("v_add_u32+s_and_b64", d, dclk, iters, first);
+  one<k_sadd_only, false>("s_add_u32", d, dclk, iters, first);
+  one<k_add_cbranch_nt, false>("v_add_u32+s_cmp+s_cbranch (not taken)", d, dclk, iters, first);
+  one<k_add_branch_taken, false>("v_add_u32+s_branch (taken)", d, dclk, iters, first);
+  std::printf("\n]\n");
+  std::fflush(stdout);
+  hipFree(d);
+  hipFree(dclk);
+  return 0;
+}
 
 extern "C" int issue_probe_main(int iters) {
   uint32_t* d;

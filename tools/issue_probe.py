@@ -53,23 +53,24 @@ def build():
     return loops
 
 
-def run(iters):
+def run(iters, entry="issue_probe_main"):
     lib = ctypes.CDLL(LIB)
-    lib.issue_probe_main.argtypes = [ctypes.c_int]
+    fn = getattr(lib, entry)
+    fn.argtypes = [ctypes.c_int]
     # the library prints one JSON array on its stdout (fd 1): capture it
     r, w = os.pipe()
     saved = os.dup(1)
     sys.stdout.flush()
     os.dup2(w, 1)
     try:
-        rc = lib.issue_probe_main(iters)
+        rc = fn(iters)
     finally:
         os.dup2(saved, 1)
         os.close(w)
         os.close(saved)
     data = io.open(r, "r").read()
     if rc != 0:
-        raise SystemExit(f"issue_probe_main failed: {rc}")
+        raise SystemExit(f"{entry} failed: {rc}")
     return json.loads(data)
 
 
@@ -88,6 +89,9 @@ KIND_OF = {  # the probe's printed name -> its kernel's kind struct
     "v_mul_u32_u24": "k_mul_u32_u24", "v_cmp_e32+v_cndmask_e32 (vcc)": "k_cmp_cnd_vcc",
     "v_cmp_e64+v_cndmask_e64 (sgpr)": "k_cmp_cnd_sgpr",
     "v_cndmask_b32_e32 (vcc from a VALU compare)": "k_cndmask_vcc_valu",
+    "v_add_u32+s_add_u32": "k_add_sadd", "v_add_u32+s_and_b64": "k_add_sand64", "s_add_u32": "k_sadd_only",
+    "v_add_u32+s_cmp+s_cbranch (not taken)": "k_add_cbranch_nt",
+    "v_add_u32+s_branch (taken)": "k_add_branch_taken",
 }
 
 
@@ -148,6 +152,9 @@ def main():
     ap.add_argument("--sq-csv", help="summarise a counter pass's sq_counter_collection.csv")
     ap.add_argument("--iters", type=int, default=20000)
     ap.add_argument("--out")
+    ap.add_argument("--scalar", action="store_true",
+                    help="only the scalar kinds: an SALU instruction, a lane-mask combine, a not-taken and a "
+                         "taken branch beside each VALU instruction (cycles per loop trip of 32 pairs)")
     a = ap.parse_args()
     if a.build:
         loops = build()
@@ -160,7 +167,7 @@ def main():
         print(text)
         return
     loops = json.load(open(LOOPS)) if os.path.exists(LOOPS) else {}
-    rows = summarise(run(a.iters), loops)
+    rows = summarise(run(a.iters, "issue_probe_scalar" if a.scalar else "issue_probe_main"), loops)
     res = {"tool": "tools/issue_probe.hip", "iters": a.iters, "rows": rows}
     one = {r["kind"]: {w: x["simd_cycles_per_trip"] / 32.0 for w in (1, 2, 4)
                        for x in rows if x["kind"] == r["kind"] and x["waves_per_simd"] == w}
