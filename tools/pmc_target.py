@@ -26,11 +26,16 @@ def main():
     ap.add_argument("--plies", type=int, default=1000)
     ap.add_argument("--launches", type=int, default=3)
     ap.add_argument("--rules", choices=("ref2", "full4"), default="ref2")
+    ap.add_argument("--stats-only", action="store_true",
+                    help="the statistics-only launches (selfplay: k_rollout_*<false, false>, no per-ply output)")
     a = ap.parse_args()
     env = VecNardeEnv(a.envs, device="cuda:0", seed=0, rules=a.rules)
-    bufs = env.rollout_buffers(a.plies)
+    bufs = None if a.stats_only else env.rollout_buffers(a.plies)
     for _ in range(a.launches + 1):
-        env.rollout(a.plies, bufs)
+        if a.stats_only:
+            env.selfplay(a.plies)
+        else:
+            env.rollout(a.plies, bufs)
     torch.cuda.synchronize()
     env.close()
 
