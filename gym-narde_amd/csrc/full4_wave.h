@@ -1,6 +1,6 @@
 // full4_wave.h -- the wave-cooperative FULL4 turn:
-// coop_turn_full (explicit plays, given dice), coop_depth_w and
-// ply_bound_turn (the rollout's waves with a block-bound doubles lane).
+// coop_turn_full (explicit plays, given dice), coop_depth_w, coop_pair_w
+// and ply_bound_turn (the rollout's waves with a block-bound doubles lane).
 // Device functions only, every lane of a wave converged at each call; the
 // cross-lane operations are __ballot and __builtin_amdgcn_readlane and
 // nothing else (no LDS, no thread indices), so tests/hostcheck compiles this
@@ -272,7 +272,9 @@ __device__ void coop_turn_full(Side& s, int d0, int d1, bool play, uint64_t pw, 
 // the straight-line way (turn_c0_free, turn_c0_pair_bound_w), and only the
 // block-bound doubles lanes that f4_safe_bound does not settle search --
 // cooperatively, over lists filtered by the turn's failing windows
-// (block_reject_w, f4_depth_w: no block_info / die_filter loop at the nodes).
+// (block_reject_w, f4_depth_w: no block_info / die_filter loop at the nodes):
+// the root and sub-move 1 in one pass over (source, next source) pairs
+// (coop_pair_w, round 5), sub-move 2 in a pass of its own (coop_depth_w).
 // Same result as coop_turn_full (the host check: env_turn_full against
 // f4_depth_w, hc_dbl_bound_w_random).
 
@@ -318,6 +320,89 @@ __device__ void coop_depth_w(const Side& s, uint32_t fw, int d, int hl, uint32_t
   }
 }
 
+// The root search and the check of sub-move 1 in one pass (round 5): for
+// each owner lane (m0 != 0: its filtered root list) in turn, lane j takes
+// the pair (s0, s1) = (source r = j / 8 of m0, entry j % 8 of L1(s0), the
+// list after s0 -- the failing windows' filter, the head rule) and finds
+// whether one / two more sub-moves follow them (f4_probe_w<2>, the search
+// where the probe stops at one).  From the pairs: r0[j] (owner lane) = the
+// sources after which j + 1 more follow (coop_depth_w's out at need 3:
+// after s0, 1 more iff L1(s0) is not empty, 2 / 3 more iff some pair leaves
+// 1 / 2), and c1 = the check of sub-move 1 after the source p0 the turn will
+// pick (w0 over C_0 as turn code does it): the entries s1 of L1(p0) after
+// which M - 2 more follow -- so that sub-move needs no pass of its own.  ok
+// (owner lane): done here; an owner with more than 8 root sources or an
+// L1 of more than 8 entries is left to coop_depth_w.  (Host-checked with
+// the rest of ply_bound_turn, tests/hostcheck hc_ply_bound_turn_random.)
+__device__ void coop_pair_w(const Side& s, uint32_t fw, int d, int hl, uint32_t m0, uint32_t w0, int lane,
+                            uint32_t r0[3], uint32_t& c1, bool& ok) {
+  r0[0] = r0[1] = r0[2] = 0u;
+  c1 = 0u;
+  ok = false;
+  uint64_t owners = __ballot(m0 != 0u);
+  while (owners) {
+    const int ow = (int)__builtin_ctzll(owners);
+    owners &= owners - 1ull;
+    Side c;
+    c.own.w[0] = rl(s.own.w[0], ow); c.own.w[1] = rl(s.own.w[1], ow); c.own.w[2] = rl(s.own.w[2], ow);
+    c.O = rl(s.O, ow); c.S1o = rl(s.S1o, ow); c.P = rl(s.P, ow);
+    c.off_own = rl(s.off_own, ow);
+    c.opp.w[0] = c.opp.w[1] = c.opp.w[2] = 0u;
+    c.S1p = 0u; c.off_opp = 0u; c.ft_own = 0u; c.ft_opp = 0u; c.black = 0u; c.elapsed = 0u; c.t = 0u;
+    const uint32_t ofw = rl(fw, ow), om = rl(m0, ow), ow0 = rl(w0, ow);
+    const int od = (int)rl((uint32_t)d, ow), ohl = (int)rl((uint32_t)hl, ow);
+    const int nsrc = __builtin_popcount(om);
+    // lane j: source rank r, entry k
+    const int r = lane >> 3, k = lane & 7;
+    const bool hs = r < nsrc;
+    const int s0 = select_bit(om, hs ? r : 0);
+    Side ca = c;
+    apply_die_if(ca, s0, od, hs);
+    const int hla = ohl - ((hs && s0 == 23) ? 1 : 0);
+    uint32_t L1 = die_candidates_sl(ca.O, ca.P, od);
+    L1 &= ~block_reject_w(ca.O, ca.S1o, ofw, L1, od);
+    L1 &= hla <= 0 ? ~HEAD : ~0u;
+    L1 = hs ? L1 : 0u;
+    const int cnt = __builtin_popcount(L1);
+    if (nsrc > 8 || __ballot(k == 0 && cnt > 8) != 0ull) continue;  // wave-uniform: coop_depth_w's
+    const bool hp = k < cnt;
+    const int s1 = select_bit(L1, hp ? k : 0);
+    Side cp = ca;
+    apply_die_if(cp, s1, od, hp);
+    const int hlp = hla - ((hp && s1 == 23) ? 1 : 0);
+    int dep = f4_probe_w<2>(cp, ofw, od, hlp);
+    const bool miss = hp && dep == 1;  // one more follows the pair; does a second?
+    if (__ballot(miss) != 0ull) {     // wave-uniform
+      if (miss) dep = f4_depth_w<2>(cp, ofw, od, hlp);
+    }
+    const uint64_t B0 = __ballot(k == 0 && cnt > 0), B1 = __ballot(hp && dep >= 1), B2 = __ballot(hp && dep >= 2);
+    // the root sets as coop_depth_w's out: lane t < 24 (a source point) looks
+    // at its source's group of 8 pair lanes
+    const bool src = lane < 24 && ((om >> lane) & 1u);
+    const int rt = __builtin_popcount(om & ((1u << (lane & 31)) - 1u));  // its rank
+    const int sh = src ? 8 * rt : 0;
+    const uint32_t a0 = (uint32_t)__ballot(src && ((B0 >> sh) & 1ull) != 0ull);
+    const uint32_t a1 = (uint32_t)__ballot(src && ((B1 >> sh) & 0xFFull) != 0ull);
+    const uint32_t a2 = (uint32_t)__ballot(src && ((B2 >> sh) & 0xFFull) != 0ull);
+    // M, C_0 and the turn's first source as ply_bound_turn_c0 takes them
+    const int M = a2 ? 4 : (a1 ? 3 : (a0 ? 2 : 1));
+    const uint32_t Cs = a2 ? a2 : (a1 ? a1 : (a0 ? a0 : om));
+    const int p0 = select_bit(Cs, (int)mulhi_u32(ow0, (uint32_t)__builtin_popcount(Cs)));
+    const int r0p = __builtin_popcount(om & ((1u << p0) - 1u));
+    const uint32_t Lp = rl(L1, 8 * r0p);  // L1(p0)
+    const uint32_t G = (uint32_t)(((M >= 4 ? B2 : B1) >> (8 * r0p)) & 0xFFull);
+    // entry e of L1(p0) (in order) is kept iff bit e of G: lane t < 24 is point t
+    const bool inl = lane < 24 && ((Lp >> lane) & 1u);
+    const int e = __builtin_popcount(Lp & ((1u << (lane & 31)) - 1u));
+    const uint32_t cv = (uint32_t)__ballot(inl && ((G >> e) & 1u));
+    r0[0] = lane == ow ? a0 : r0[0];
+    r0[1] = lane == ow ? a1 : r0[1];
+    r0[2] = lane == ow ? a2 : r0[2];
+    c1 = lane == ow ? cv : c1;
+    ok = lane == ow ? true : ok;
+  }
+}
+
 // The turn of every lane of a wave holding a block-bound doubles lane (bs,
 // fw: turn_block_set_sl): C_0 / M from the masks (turn_c0_free);
 // block-bound two-dice lanes from the failing windows
@@ -341,7 +426,8 @@ __device__ __forceinline__ void ply_bound_turn_c0(Side& s, int dh, int dl, uint3
   if (__ballot(b2) != 0ull) {
     if (b2) turn_c0_pair_bound_w(s, dh, dl, bs, fw, Lh, Ll, Ch, Cl, M);
   }
-  bool srch = false;
+  bool srch = false, pairs = false;
+  uint32_t c1p = 0u;  // sub-move 1's checked list, when the pair pass made it (pairs)
   if (__ballot(bd) != 0ull) {
     // block-bound doubles: the filtered root list; M = 4 with every C_k =
     // L_k when the never-rejected moves give >= 4; else the search
@@ -349,7 +435,12 @@ __device__ __forceinline__ void ply_bound_turn_c0(Side& s, int dh, int dl, uint3
     const bool fast = bd && f4_safe_bound(s, dh, hl0, bs) >= 4;
     srch = bd && !fast && Lb != 0u;
     uint32_t r0[3];
-    coop_depth_w(s, fw, dh, hl0, srch ? Lb : 0u, 3, lane, r0);
+    coop_pair_w(s, fw, dh, hl0, srch ? Lb : 0u, w[0], lane, r0, c1p, pairs);
+    if (__ballot(srch && !pairs) != 0ull) {  // wave-uniform: owners too wide for the pairs
+      uint32_t rd[3];
+      coop_depth_w(s, fw, dh, hl0, (srch && !pairs) ? Lb : 0u, 3, lane, rd);
+      if (srch && !pairs) { r0[0] = rd[0]; r0[1] = rd[1]; r0[2] = rd[2]; }
+    }
     const int Ms = r0[2] ? 4 : (r0[1] ? 3 : (r0[0] ? 2 : 1));
     const uint32_t Cs = r0[2] ? r0[2] : (r0[1] ? r0[1] : (r0[0] ? r0[0] : Lb));
     Ch = bd ? (fast ? Lb : (Lb ? Cs : 0u)) : Ch;
@@ -379,7 +470,9 @@ __device__ __forceinline__ void ply_bound_turn_c0(Side& s, int dh, int dl, uint3
     }
     Lk &= hl <= 0 ? ~HEAD : ~0u;
     const int need = M - k - 1;
-    const bool chk = srch && act && need > 0;
+    const bool byp = k == 1 && pairs && need > 0;  // from the pair pass
+    Lk = (srch && act && byp) ? c1p : Lk;
+    const bool chk = srch && act && need > 0 && !byp;
     if (__ballot(chk) != 0ull) {  // wave-uniform
       uint32_t rk[3];
       coop_depth_w(s, fw, dk, hl, chk ? Lk : 0u, need, lane, rk);
