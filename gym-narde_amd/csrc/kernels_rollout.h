@@ -349,6 +349,24 @@ __device__ __forceinline__ int4 stats_after(int4* __restrict__ stats, int i, con
   return cur;
 }
 
+// k_rollout_pp_full's form of stats_after: env i's statistics read at the
+// start of the launch (pre) -- there the load at the end, after the
+// workgroup's closing barrier, sat on a short launch's critical path (one
+// 20-ply FULL4 launch at the driver's shape: medians of 8, 74.4 -> 73.6 us;
+// k_rollout_pc's producers finish while their consumers still store the
+// last block, and it gained nothing there) -- and stored back only when the
+// launch finished an episode of the env
+__device__ __forceinline__ int4 stats_read(const int4* __restrict__ stats, int i, bool valid) {
+  return valid ? stats[i] : make_int4(0, 0, 0, 0);
+}
+__device__ __forceinline__ int4 stats_after_pre(int4* __restrict__ stats, int i, int4 pre, const int4& st) {
+  pre.x += st.x;
+  pre.y += st.y;
+  pre.z += st.z;
+  if (st.x) stats[i] = pre;
+  return pre;
+}
+
 // The rollout's episode totals without a second launch: every thread of
 // the workgroup passes its env's statistics after the launch (zeros for
 // threads with no env), and the workgroup writes their sum
@@ -869,9 +887,10 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pp_full(Planes pl, int n
     L.emitted[threadIdx.x] = 0u;
   }
   __syncthreads();
-  int4 st = make_int4(0, 0, 0, 0);
+  int4 st = make_int4(0, 0, 0, 0), pre = make_int4(0, 0, 0, 0);
   if (producer) {
     Side s = valid ? side_from_record(pl.p0[i], pl.p1[i]) : side_start(0u);
+    pre = stats_read(pl.stats, i, valid);
     // the counters as last seen: a poll (an LDS round trip) only when ply p
     // is past them -- the consumer runs up to kPpR plies ahead
     uint32_t dk = 0u, ek = 0u;
@@ -939,7 +958,7 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pp_full(Planes pl, int n
   }
   __syncthreads();
   int4 cum = make_int4(0, 0, 0, 0);
-  if (producer && valid) cum = stats_after(pl.stats, i, st, out.totals != nullptr);
+  if (producer && valid) cum = stats_after_pre(pl.stats, i, pre, st);
   if (out.totals) wg_totals(cum, out.totals);
 }
 
