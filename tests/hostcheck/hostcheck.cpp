@@ -1177,3 +1177,128 @@ extern "C" int64_t hc_ply_bound_turn_random(int64_t waves, uint32_t seed, int64_
   }
   return bad;
 }
+
+// ply_bound_turn on emulated waves whose block-bound doubles lanes come from
+// random-legal self-play (round 5, the pair pass coop_pair_w): `envs` envs
+// play `plies` plies with env_turn_full; every searching block-bound
+// doubles turn met (f4_safe_bound < 4, a non-empty filtered root list) is
+// kept, and the kept turns are replayed 64 to a wave through ply_bound_turn
+// against env_turn_full.  Returns the lanes that differ; counts[0] = turns
+// kept, counts[1] = of them, turns whose sub-move 1 checks differ between
+// one and two more sub-moves for the source the turn picks (the case that
+// tells the pair pass's two result sets apart), counts[2] = waves run.
+extern "C" int64_t hc_pair_pass_selfplay(int64_t envs, int64_t plies, int64_t* counts) {
+  struct Kept {
+    Side s;
+    int d;
+    uint32_t w[4];
+  };
+  std::vector<Kept> kept;
+  std::vector<Side> S((size_t)envs);
+  for (int64_t i = 0; i < envs; ++i) {
+    uint32_t r[4];
+    philox4x32_10(0, (uint32_t)i, 0u, 1u, 0u, 0u, r);
+    S[i] = side_reset(r[0]);
+    S[i].t = 0;
+  }
+  counts[0] = counts[1] = counts[2] = 0;
+  for (int64_t p = 0; p < plies; ++p) {
+    for (int64_t i = 0; i < envs; ++i) {
+      Side& s = S[i];
+      uint32_t R[4], r[4];
+      ply_block(s.t, (uint32_t)i, 0u, 0u, R);
+      ply_words_of(R, s.t, 0, r);
+      int d0, d1;
+      dice_from(r[0], 0, d0, d1);
+      const int dh = d0 > d1 ? d0 : d1, dl = d0 > d1 ? d1 : d0;
+      uint32_t w[4];
+      turn_words(r, w);
+      uint32_t fw;
+      const uint32_t bs = turn_block_set_sl(s.O, s.S1o, s.P, block_lowmask(s.P), dh, dl, fw);
+      if (bs && dh == dl) {
+        const int hl = (s.ft_own && (dh == 3 || dh == 4 || dh == 6)) ? 2 : 1;
+        const uint32_t Lh = die_candidates(s.O, s.P, dh);
+        const uint32_t Lb = Lh & ~block_reject_w(s.O, s.S1o, fw, Lh, dh);
+        if (f4_safe_bound(s, dh, hl, bs) < 4 && Lb) {
+          Kept k;
+          k.s = s;
+          k.d = dh;
+          for (int j = 0; j < 4; ++j) k.w[j] = w[j];
+          kept.push_back(k);
+          // the source env_turn_full's first pick takes, and its sub-move 1 sets
+          Side e = s;
+          TurnOut oe;
+          env_turn_full(e, dh, dh, false, 0ull, w, oe);
+          if (oe.max_dice == 4) {
+            const int p0 = (int)(oe.played & 0xFFu);
+            Side a = s;
+            apply_die(a, p0, dh);
+            const int h1 = hl - (p0 == 23 ? 1 : 0);
+            uint32_t L1 = die_candidates_sl(a.O, a.P, dh);
+            L1 &= ~block_reject_w(a.O, a.S1o, fw, L1, dh);
+            if (h1 <= 0) L1 &= ~HEAD;
+            uint32_t c1 = 0u, c2 = 0u;
+            for (uint32_t m = L1; m; m &= m - 1u) {
+              const int q = __builtin_ctz(m);
+              Side b = a;
+              apply_die(b, q, dh);
+              const int dd = f4_depth_w<2>(b, fw, dh, h1 - (q == 23 ? 1 : 0));
+              c1 |= dd >= 1 ? 1u << q : 0u;
+              c2 |= dd >= 2 ? 1u << q : 0u;
+            }
+            counts[1] += c1 != c2;
+          }
+        }
+      }
+      const uint32_t mb = s.black;
+      TurnOut o;
+      env_turn_full(s, d0, d1, false, 0ull, w, o);
+      int4 st = make_int4(0, 0, 0, 0);
+      int tm, tr;
+      ply_close(s, st, o.term, o.reward, mb, r[3], 1000, true, tm, tr);
+    }
+  }
+  counts[0] = (int64_t)kept.size();
+  int64_t bad = 0;
+  for (size_t w0 = 0; w0 < kept.size(); w0 += 64) {
+    Side s[64], got[64];
+    int dh[64];
+    uint32_t w[64][4];
+    TurnOut o[64];
+    for (int l = 0; l < 64; ++l) {
+      const Kept& k = kept[(w0 + (size_t)l) % kept.size()];
+      s[l] = k.s;
+      dh[l] = k.d;
+      for (int j = 0; j < 4; ++j) w[l][j] = k.w[j];
+    }
+    wave_emu::Wave wave;
+    wave_emu::g_wave = &wave;
+    std::vector<std::thread> th;
+    for (int l = 0; l < 64; ++l) {
+      th.emplace_back([&, l] {
+        wave_emu::t_lane = l;
+        Side x = s[l];
+        uint32_t fw;
+        const uint32_t bs = turn_block_set_sl(x.O, x.S1o, x.P, block_lowmask(x.P), dh[l], dh[l], fw);
+        ply_bound_turn(x, dh[l], dh[l], bs, fw, w[l], false, o[l], l);
+        got[l] = x;
+      });
+    }
+    for (auto& t : th) t.join();
+    wave_emu::g_wave = nullptr;
+    ++counts[2];
+    for (int l = 0; l < 64; ++l) {
+      Side e = s[l];
+      TurnOut oe;
+      env_turn_full(e, dh[l], dh[l], false, 0ull, w[l], oe);
+      uint4 a1, b1, a2, b2;
+      side_to_record(got[l], a1, b1);
+      side_to_record(e, a2, b2);
+      const bool same = o[l].legal == oe.legal && o[l].played == oe.played && o[l].term == oe.term &&
+                        o[l].max_dice == oe.max_dice && a1.x == a2.x && a1.y == a2.y && a1.z == a2.z &&
+                        a1.w == a2.w && b1.x == b2.x && b1.y == b2.y && b1.z == b2.z;
+      bad += same ? 0 : 1;
+    }
+  }
+  return bad;
+}

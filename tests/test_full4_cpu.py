@@ -396,3 +396,22 @@ def test_hostcheck_ply_bound_turn_emulated_wave(hostcheck):
     bd, searched, b2, lanes = list(c)
     assert lanes == 64 * waves
     assert bd > 10 * waves and searched > 5 * waves and b2 > 10 * waves
+
+
+def test_hostcheck_pair_pass_selfplay_turns(hostcheck):
+    """coop_pair_w (full4_wave.h: the block-bound doubles search's root and
+    sub-move-1 check in one cooperative pass over source pairs) on the
+    searching turns random-legal self-play meets: ply_bound_turn on 64
+    emulated lanes == env_turn_full, lane by lane, including the turns whose
+    sub-move-1 check differs between one and two more sub-moves (the case
+    that tells the pass's two result sets apart; a mutant taking the wrong
+    set fails on them)."""
+    f = hostcheck.hc_pair_pass_selfplay
+    f.restype = ctypes.c_int64
+    c = (ctypes.c_int64 * 3)()
+    envs = max(1024, 8192 // SAN_DIV)
+    assert f(ctypes.c_int64(envs), ctypes.c_int64(200), c) == 0
+    kept, split, waves = list(c)
+    assert kept > envs // 8 and waves >= kept // 64
+    if envs == 8192:
+        assert split > 0
