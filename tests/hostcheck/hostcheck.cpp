@@ -1260,6 +1260,7 @@ extern "C" int64_t hc_pair_pass_selfplay(int64_t envs, int64_t plies, int64_t* c
   }
   counts[0] = (int64_t)kept.size();
   int64_t bad = 0;
+  if (kept.empty()) return 0;  // (the caller asserts that turns were kept)
   for (size_t w0 = 0; w0 < kept.size(); w0 += 64) {
     Side s[64], got[64];
     int dh[64];
