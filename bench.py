@@ -132,6 +132,44 @@ def cpu_baseline(seconds, cores, how):
     }
 
 
+# the parity_check leg's cost model: the C oracle's self-play rate per host
+# core (env steps/s; conservative -- measured 0.6-1.7e6 REF2 and 0.04-0.11e6
+# FULL4 on the build container and the GPU box's EPYC 9575F)
+ORACLE_RATE = {"ref2": 1.0e6, "full4": 8.0e4}
+PARITY_MIN_ENVS = 16384
+
+
+def parity_envs(per, plies, rules, core_s):
+    """Envs the checker replays for `plies` plies within `core_s` core-seconds
+    of oracle work: the whole shard when it fits, else a prefix of at least
+    PARITY_MIN_ENVS envs (a multiple of 256, one workgroup's envs)."""
+    fit = int(core_s * ORACLE_RATE[rules] / max(1, plies))
+    if fit >= per:
+        return per
+    return min(per, max(PARITY_MIN_ENVS, fit // 256 * 256))
+
+
+def host_bufs(bufs, plies, envs):
+    """Host copies of the first `plies` rows and `envs` envs of rollout
+    buffers (the checker's input; untimed)."""
+    return {k: (v[:plies, :envs].cpu().numpy() if v is not None else None) for k, v in bufs.items()}
+
+
+def run_parity(item, threads):
+    """The checker leg (oracle/replay.py): the oracle replays what the device
+    played from the snapshot taken before it and compares every output.
+    Same standing as cpu_baseline: test infrastructure, run after the GPU
+    work it checks, never inside a timed region."""
+    import replay as R
+
+    res = R.check(item["before"], item["bufs"], item["after"], item["plies"], item["seed"],
+                  env0=item["env0"], full=item["rules"] == "full4", envs=item["envs"], threads=threads,
+                  totals_rows=item.get("totals_rows"))
+    res["scope"] = item["scope"]
+    res["env_ids"] = f"{item['env0']}..{item['env0'] + item['envs'] - 1}"
+    return res
+
+
 def kernel_name(full4, plies):
     """The kernel narde_rollout[_full] launches for this shape (narde.hip):
     both store non-temporally up to 32 plies per launch (kPcNtMaxPlies);
@@ -149,7 +187,8 @@ def load_traffic(path, envs, plies, kernel):
         d = json.load(open(path))
     except (OSError, ValueError):
         return None
-    if d.get("envs") != envs or d.get("plies") != plies or d.get("kernel", "") not in kernel:
+    k = d.get("kernel")
+    if d.get("envs") != envs or d.get("plies") != plies or not k or k not in kernel:
         return None
     return d.get("hbm_bytes_per_launch")
 
@@ -177,7 +216,8 @@ def load_issue(full4, envs, plies, kernel_ms):
         return None
     if d.get("envs") != envs or d.get("plies") != plies or not d.get("valu_per_launch") or not kernel_ms:
         return None
-    if d.get("kernel", "") not in kernel_name(full4, plies):  # a summary of another kernel
+    k = d.get("kernel")
+    if not k or k not in kernel_name(full4, plies):  # no kernel named, or another kernel's summary
         return None
     achieved = d["valu_per_launch"] / (kernel_ms * 1e-3)
     return {
@@ -226,10 +266,12 @@ def spawn_ranks(n, argv, cpu=None):
     return subprocess.call(cmd, env=env)
 
 
-def _ancestors(depth=4):
-    """pids of this process's parent, grandparent, ... (Linux /proc)."""
+def _ancestors(depth=64):
+    """pids of this process's parent, grandparent, ... up to pid 1 (Linux
+    /proc; any number of wrapper processes between the launcher and the
+    rank)."""
     out, pid = [], os.getpid()
-    for _ in range(depth):
+    while pid > 1 and len(out) < depth:
         try:
             with open(f"/proc/{pid}/stat") as f:
                 pid = int(f.read().rsplit(")", 1)[1].split()[1])
@@ -251,8 +293,12 @@ def handed_cpu_baseline():
         ok = (str(d["master_port"]) == os.environ.get("MASTER_PORT")
               and int(d["launcher_pid"]) in _ancestors())
     except (ValueError, KeyError, TypeError):
+        ok = False
+    if not ok:
+        print(f"bench.py: {CPU_BASELINE_ENV} is set but is not this launch's; measuring the CPU "
+              "baseline here", file=sys.stderr)
         return None
-    return d["cpu"] if ok else None
+    return d["cpu"]
 
 
 def measure_cpu_baseline(args):
@@ -371,6 +417,11 @@ def main():
                     help="k_rollout launches of the other rules mode, timed beside the headline")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_summary.py); default profiles/pmc_k_rollout[_full].json")
+    ap.add_argument("--no-parity-check", action="store_true",
+                    help="skip the checker leg (the C oracle replaying the timed launches)")
+    ap.add_argument("--parity-core-s", type=float, default=160.0,
+                    help="oracle work the checker may spend per leg (host core-seconds): the whole "
+                         "shard when it fits, else a prefix of >= 16,384 envs")
     args = ap.parse_args()
 
     world_env = os.environ.get("WORLD_SIZE")
@@ -490,6 +541,24 @@ def main():
     ramp_n += 3 if len(calls) == 1 else 6
 
     run_plies(args.warmup)
+    # the checker leg (rank 0's shard, after the GPU work it checks): when
+    # the oracle can replay the whole timed region within --parity-core-s,
+    # the state before it is snapshotted here (untimed, before the barrier)
+    # and every timed ply is replayed; otherwise one launch of the timed
+    # kernel at the timed shape right after the region is checked instead
+    check_parity = rank == 0 and eng.name is None and not args.no_parity_check
+    parity_items, snap0 = [], None
+    if check_parity:
+        import replay as R
+
+        cores_p, _ = available_cores()
+        if parity_envs(per, K, args.rules, args.parity_core_s) == per:
+            # two small stream-ordered kernels into device tensors, no
+            # synchronize: the device goes from the warm-up into the region
+            # as without the checker (a host copy here left the GPU idle for
+            # ~ms before the region and the timed 20-ply launch ran 46 us
+            # instead of 37, profiles/r06/parity/)
+            snap0 = R.snapshot_async(env)
     # the rows' all-gather at N > 1: RCCL's own ncclAllGather on the
     # launching stream (D.RcclGather, one library call) -- ProcessGroupNCCL's
     # all_gather_into_tensor costs ~80 us of host time after a marked launch
@@ -567,6 +636,29 @@ def main():
     value = total_steps / elapsed
     summary = D.summarize(totals)
 
+    if check_parity:
+        # the checker's inputs, copied to the host before any other leg runs
+        # on this env (untimed)
+        last_p = sizes[-1]
+        if snap0 is not None:
+            parity_items.append(dict(
+                rules=args.rules, before=R.to_host(snap0), bufs=host_bufs(bufs, last_p, per), after=R.snapshot(env),
+                plies=K, envs=per, seed=args.seed, env0=first, totals_rows=rows_buf.cpu().numpy(),
+                scope=(f"the timed region itself: all {K} timed plies replayed from the state snapshotted "
+                       f"before it; the last launch's {last_p} plies of per-ply outputs, the final state "
+                       f"and its per-256-env totals rows compared")))
+        else:
+            n_chk = parity_envs(per, P, args.rules, args.parity_core_s)
+            before = R.snapshot(env)
+            full_launch()
+            eng.sync()
+            parity_items.append(dict(
+                rules=args.rules, before=before, bufs=host_bufs(bufs, P, n_chk), after=R.snapshot(env),
+                plies=P, envs=n_chk, seed=args.seed, env0=first,
+                scope=(f"the {K} timed plies are more than --parity-core-s lets the oracle replay: one "
+                       f"untimed launch of the timed kernel at the timed shape ({P} plies) right after "
+                       f"the region, its per-ply outputs and final state compared")))
+
     # secondary 1: per-ply API kernel k_step (eager, then hipGraph replay)
     api = None
     S = args.api_steps
@@ -642,12 +734,26 @@ def main():
         torch.cuda.synchronize()
         ev_o = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                 for _ in range(args.other_launches)]
+        n_o = parity_envs(per, P, other_rules, args.parity_core_s) if check_parity else 0
+        snap_o = None
         o0 = time.perf_counter()
-        for s_, e_ in ev_o:
+        for j, (s_, e_) in enumerate(ev_o):
+            if n_o and j == len(ev_o) - 1:
+                # the checker's snapshot of the state before the last timed
+                # launch: two small stream-ordered kernels into device
+                # tensors and the host ply counter, outside the launch's
+                # events (in the wall rate: ~0.2 % of 20 launches)
+                snap_o = R.snapshot_async(env_o)
             s_.record()
             env_o.rollout(P, bufs_o)
             e_.record()
         torch.cuda.synchronize()
+        if snap_o is not None:
+            parity_items.append(dict(
+                rules=other_rules, before=R.to_host(snap_o), bufs=host_bufs(bufs_o, P, n_o), after=R.snapshot(env_o),
+                plies=P, envs=n_o, seed=args.seed, env0=first, leg="other_rules",
+                scope=f"the last of the {len(ev_o)} timed launches of this leg ({P} plies): its per-ply "
+                      f"outputs and final state compared"))
         other_rate = per * P * args.other_launches / (time.perf_counter() - o0)
         other_ms = sum(s_.elapsed_time(e_) for s_, e_ in ev_o) / len(ev_o)
         other_M = None
@@ -726,6 +832,12 @@ def main():
             "final_loss": float(drv.last_loss) if drv.last_loss is not None else None,
         }
         env_q.close()
+
+    # the checker leg, after every GPU leg (rank 0's shard)
+    parity = {}
+    for item in parity_items:
+        parity[item.get("leg", "headline")] = run_parity(item, cores_p)
+    del parity_items
 
     if rank == 0:
         nbytes = launch_bytes(per, P, is_full4)
@@ -826,6 +938,11 @@ def main():
             # waiting for them (and the gather), the closing barrier + sync
             "timed_region_host_us": host_us,
             "cpu_baseline": cpu,
+            # the metric's "legal-move bit-exact vs CPU", checked on this
+            # run's own launches: the C oracle (oracle/replay.py) replays
+            # them from the snapshotted state; mismatches counts (ply, env)
+            # entries of every output plus envs whose final state differs
+            "parity_check": parity.get("headline"),
             "api_step": api,
             "other_rules": other,
             "config4_dqn": dqn,
@@ -834,6 +951,7 @@ def main():
         if other is not None:
             other["workload"] = f"{config_txt[other_rules]}; rules = {rules_txt[other_rules]}"
             other["parity"] = parity_txt[other_rules]
+            other["parity_check"] = parity.get("other_rules")
         if eng.name is not None:
             line["engine"] = eng.name
         # (a fresh line: a library banner on stdout may lack its newline)

@@ -776,6 +776,14 @@ struct PpLds {
   uint32_t rtt[kPcGroups][kPpR][64];
   uint32_t drawn[kPcGroups], produced[kPcGroups], emitted[kPcGroups];
 };
+// gfx950 has 160 KiB of LDS per CU: a k_rollout_pp_full workgroup holds
+// PpLds and wg_totals' reduction buffer (long long[16][3]); a deeper ring or
+// another per-slot array must still fit in it
+static_assert(sizeof(PpLds) + sizeof(long long) * 16 * 3 <= 160 * 1024, "PpLds exceeds the CU's LDS");
+// the producer publishes ply p - 1's `produced` only after ply p's drawn /
+// emitted waits, so the consumer must be able to draw ply p while ply p - 1
+// is unemitted: one slot would deadlock the pair
+static_assert(kPpR >= 2, "k_rollout_pp_full's hand-over needs at least two ring slots");
 
 __device__ __forceinline__ uint32_t pp_load(const uint32_t* c) {
   return __builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));

@@ -193,6 +193,19 @@ class SelfPlay:
                              _p(self.elapsed))
         self.stats[:] = 0
 
+    def load(self, board, off, ft, player, elapsed, stats, t):
+        """Take over a device handle's state at lockstep ply t (get_state(),
+        stats() and ply of VecNardeEnv): run() then replays the plies the
+        handle plays from there (oracle/replay.py)."""
+        n = self.n
+        self.board = np.array(board, dtype=np.int8).reshape(n, 24)
+        self.off = np.array(off, dtype=np.uint8).reshape(n, 2)
+        self.ft = np.array(ft, dtype=np.uint8).reshape(n, 2)
+        self.player = np.array(player, dtype=np.int8).reshape(n)
+        self.elapsed = np.array(elapsed).astype(np.uint16).reshape(n)
+        self.stats = np.array(stats, dtype=np.int32).reshape(n, 3)
+        self.t = int(t)
+
     def run(self, plies, record=True):
         n = self.n
         if record:

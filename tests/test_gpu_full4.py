@@ -13,10 +13,14 @@ import pytest
 from conftest import golden
 
 import oracle as O
+import replay as R
+from bench import available_cores
 
 pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
+
+THREADS = available_cores()[0]  # the oracle replay's thread pool (oracle/replay.py)
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -181,27 +185,24 @@ def test_full4_rollout_ring_boundaries():
     assert np.array_equal(np_(a.stats()), np_(b.stats()))
 
 
-@pytest.mark.parametrize("plies", [120, 20])
-def test_full4_full_batch_window_and_invariants(plies):
+@pytest.mark.parametrize("plies,seed", [(120, 7), (20, 0)])
+def test_full4_full_batch_vs_oracle_and_invariants(plies, seed):
     """B = 65,536 (the bench shape; 120-ply launches, and the driver's 20-ply
-    launch; k_rollout_pp_full): a 2,048-env window equals the
-    oracle run on those global ids; checker conservation and played == max
-    dice everywhere."""
-    n, seed = 65536, 7
+    launch at the bench's seed 0 and env ids 0..65,535; k_rollout_pp_full):
+    EVERY env's every output and final state equal the C oracle replaying
+    the launch (oracle/replay.py, the bench's parity_check leg); checker
+    conservation and played == max dice everywhere."""
+    n = 65536
     env = vec(n, seed=seed)
     bufs = env.rollout_buffers(plies)
+    before = R.snapshot(env)
     env.rollout(plies, bufs)
-    lo = 40000
-    ref = O.SelfPlay(2048, seed=seed, env0=lo)
-    ref.reset(0)
-    rec = ref.run_full(plies)
-    sl = slice(lo, lo + 2048)
-    assert np.array_equal(np_(bufs["obs"][:, sl]), rec["obs"].astype(np.int32))
-    assert np.array_equal(np_(bufs["legal"][:, sl]).view(np.uint64), rec["legal"])
-    assert np.array_equal(np_(bufs["actions"][:, sl]).view(np.uint64), rec["played"])
-    st = env.get_state()
-    b = np_(st["board"]).astype(np.int64)
-    off = np_(st["off"]).astype(np.int64)
+    after = R.snapshot(env)
+    res = R.check(before, {k: np_(v) for k, v in bufs.items()}, after, plies, seed, full=True,
+                  threads=THREADS)
+    assert res["mismatches"] == 0 and res["envs"] == n, res
+    b = after["board"].astype(np.int64)
+    off = after["off"].astype(np.int64)
     assert ((np.where(b > 0, b, 0).sum(1) + off[:, 0]) == 15).all()
     assert ((np.where(b < 0, -b, 0).sum(1) + off[:, 1]) == 15).all()
     legal = np_(bufs["legal"]).view(np.uint64)
@@ -213,28 +214,22 @@ def test_full4_full_batch_window_and_invariants(plies):
     assert (M == 4).mean() > 0.08
 
 
-def test_full4_steady_state_window_after_selfplay():
+def test_full4_steady_state_full_batch_after_selfplay():
     """The driver's 20-ply launch at B = 65,536 in the steady state (300
     plies of stats-only self-play first: the envs spread over every game
     phase, so block-bound two-dice and doubles turns, the failing-window
     loops per kind and the doubles search all occur in every launch,
-    tools/diag/wave_kinds.cpp): a 2,048-env window of the launch's outputs
-    and final boards equals the oracle."""
-    n, seed, pre, plies, lo = 65536, 11, 300, 20, 20000
+    tools/diag/wave_kinds.cpp): every env's outputs and final state equal
+    the oracle replaying the launch from the state before it."""
+    n, seed, pre, plies = 65536, 11, 300, 20
     env = vec(n, seed=seed)
     env.selfplay(pre)
     bufs = env.rollout_buffers(plies)
+    before = R.snapshot(env)
     env.rollout(plies, bufs)
-    ref = O.SelfPlay(2048, seed=seed, env0=lo)
-    ref.reset(0)
-    ref.run_full(pre, record=False)
-    rec = ref.run_full(plies)
-    sl = slice(lo, lo + 2048)
-    assert np.array_equal(np_(bufs["obs"][:, sl]), rec["obs"].astype(np.int32))
-    assert np.array_equal(np_(bufs["legal"][:, sl]).view(np.uint64), rec["legal"])
-    assert np.array_equal(np_(bufs["actions"][:, sl]).view(np.uint64), rec["played"])
-    assert np.array_equal(np_(bufs["reward"][:, sl]), rec["reward"].astype(np.int32))
-    assert np.array_equal(np_(env.get_state()["board"])[sl], ref.board)
+    res = R.check(before, {k: np_(v) for k, v in bufs.items()}, R.snapshot(env), plies, seed, full=True,
+                  threads=THREADS)
+    assert res["mismatches"] == 0 and res["envs"] == n, res
 
 
 @pytest.mark.parametrize("n", [1, 63, 65])

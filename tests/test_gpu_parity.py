@@ -5,10 +5,14 @@ import pytest
 from conftest import golden
 
 import oracle as O
+import replay as R
+from bench import available_cores
 
 pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
+
+THREADS = available_cores()[0]  # the oracle replay's thread pool (oracle/replay.py)
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -269,54 +273,46 @@ def test_step_graph_replay_vs_oracle():
     assert np.array_equal(np_(obs), rec["obs"][0].astype(np.int32))
 
 
-def test_full_batch_subset_and_invariants():
-    """B = 65536 (BASELINE configs[2]): a contiguous window of envs equals the
-    oracle run on just those global ids, and the whole batch conserves
-    checkers."""
+def test_full_batch_selfplay_vs_oracle():
+    """B = 65536 (BASELINE configs[2]): 400 plies of stats-only self-play
+    (k_selfplay) leave every env's state and statistics equal to the
+    oracle's, whole batch, and the whole batch conserves checkers."""
     B, plies, seed = 65536, 400, 2024
     env = vec(B, seed=seed)
+    before = R.snapshot(env)
     env.selfplay(plies)
-    st = env.get_state()
-    board = np_(st["board"]).astype(np.int64)
-    off = np_(st["off"]).astype(np.int64)
+    after = R.snapshot(env)
+    board = after["board"].astype(np.int64)
+    off = after["off"].astype(np.int64)
     w = np.where(board > 0, board, 0).sum(1) + off[:, 0]
     k = np.where(board < 0, -board, 0).sum(1) + off[:, 1]
     assert (w == 15).all() and (k == 15).all()
-    lo, m = 40000, 2048
-    ref = O.SelfPlay(m, seed=seed, env0=lo)
-    ref.reset(0)
-    ref.run(plies, record=False)
-    assert np.array_equal(board[lo:lo + m].astype(np.int8), ref.board)
-    stats = np_(env.stats())
-    assert np.array_equal(stats[lo:lo + m], ref.stats)
-    assert stats[:, 0].sum() > B  # several episodes per env on average
+    state, _ = R.replay(before, plies, 0, seed, threads=THREADS)
+    for key in ("board", "off", "first_turn", "player", "stats"):
+        assert np.array_equal(after[key], state[key]), key
+    assert np.array_equal(after["elapsed"].astype(np.int64), state["elapsed"].astype(np.int64))
+    assert after["stats"][:, 0].sum() > B  # several episodes per env on average
 
 
-def test_bench_launch_window_and_invariants():
+def test_bench_launches_full_batch_vs_oracle():
     """The launches bench.py times (k_rollout_pc<true, *>: B = 65,536, 1,000
     plies, every output), then a 100-ply one and the driver's 20-ply one
-    (non-temporal stores): a 2,048-env window of every output -- the legal
-    sets included -- equals the oracle on those global ids; over the whole batch the
-    outputs obey the rules' invariants (at most 15 checkers a side, reward
-    only on a finished game (1 or 2), no truncation: no random game lasts
-    1,000 plies)."""
-    B, seed, lo, m = 65536, 99, 50000, 2048
+    (non-temporal stores), at the bench's own seed 0 and env ids 0..65,535:
+    EVERY env's every output -- the legal sets included, the metric's
+    "legal-move bit-exact vs CPU" -- and final state equal the C oracle
+    replaying the launch from the state before it (oracle/replay.py, the
+    bench's parity_check leg); the outputs obey the rules' invariants (at
+    most 15 checkers a side, reward only on a finished game (1 or 2),
+    truncation only of an unfinished game)."""
+    B, seed = 65536, 0
     env = vec(B, seed=seed)
-    ref = O.SelfPlay(m, seed=seed, env0=lo)
-    ref.reset(0)
-    sl = slice(lo, lo + m)
     for P in (1000, 100, 20):
         bufs = env.rollout_buffers(P)
+        before = R.snapshot(env)
         env.rollout(P, bufs)
-        rec = ref.run(P)
-        assert np.array_equal(np_(bufs["obs"][:, sl]), rec["obs"].astype(np.int32))
-        assert np.array_equal(np_(bufs["reward"][:, sl]), rec["reward"].astype(np.int32))
-        assert np.array_equal(np_(bufs["terminated"][:, sl]), rec["terminated"])
-        assert np.array_equal(np_(bufs["truncated"][:, sl]), rec["truncated"])
-        assert np.array_equal(np_(bufs["actions"][:, sl]), rec["action"])
-        # the metric's "legal-move bit-exact vs CPU": list #1 of every ply of the
-        # window, word for word against the oracle's (or_compact2 of its list)
-        assert np.array_equal(np_(bufs["legal"][:, sl]).view(np.uint64), rec["legal"])
+        host = {k: np_(v) for k, v in bufs.items()}
+        res = R.check(before, host, R.snapshot(env), P, seed, threads=THREADS)
+        assert res["mismatches"] == 0 and res["envs"] == B, res
         obs = bufs["obs"]
         assert int(obs.abs().max()) <= 15
         assert bool((obs.clamp(min=0).sum(-1) <= 15).all()) and bool(((-obs).clamp(min=0).sum(-1) <= 15).all())
@@ -324,10 +320,32 @@ def test_bench_launch_window_and_invariants():
         # narde_env.py:134-141: 1 for a win, 2 for a mars (loser bore off nothing)
         assert bool(((rew == 0) | (((rew == 1) | (rew == 2)) & term)).all())
         assert bool((rew[term] > 0).all())
-        assert not bool(trunc.any())
-        del bufs, obs, rew, term, trunc
-    assert np.array_equal(np_(env.stats())[sl], ref.stats)
+        # TimeLimit 1000: a truncation ends an unfinished game (rare: at seed
+        # 0 a few games of the 65,536 reach 1,000 plies in the 1,000-ply launch)
+        assert not bool((trunc & term).any()) and float(trunc.float().mean()) < 1e-3
+        del bufs, obs, rew, term, trunc, host
     assert env.ply == 1120
+
+
+def test_bench_timed_launch_totals_rows_vs_oracle():
+    """The bench's timed launch shape with its totals rows
+    (narde_rollout_timed: the launch writes its envs' statistics summed per
+    256 envs): rows and every output against the oracle, whole batch."""
+    from gym_narde.vector import TimingEvent
+
+    B, seed, P = 65536, 0, 20
+    env = vec(B, seed=seed)
+    env.selfplay(137)  # mid-game, odd ply: the Philox block of a ply pair re-derived
+    bufs = env.rollout_buffers(P)
+    rows = torch.empty(((B + 255) // 256, 3), dtype=torch.int64, device="cuda:0")
+    ev0, ev1 = TimingEvent("cuda:0"), TimingEvent("cuda:0")
+    launch = env.rollout_launcher(P, bufs, events=(ev0, ev1), totals=rows)
+    before = R.snapshot(env)
+    launch()
+    host = {k: np_(v) for k, v in bufs.items()}
+    res = R.check(before, host, R.snapshot(env), P, seed, threads=THREADS, totals_rows=np_(rows))
+    assert res["mismatches"] == 0 and res["by_field"]["totals_rows"] == 0, res
+    assert ev0.elapsed_ms(ev1) > 0
 
 
 def test_sharded_handles_equal_single():

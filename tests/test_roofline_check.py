@@ -51,6 +51,23 @@ def test_summaries_apply_only_to_their_kernel():
     assert not rc.matches({"envs": 65536, "plies": 20, "kernel": "k_rollout_wave<true>"}, 65536, 20, k)
     assert not rc.matches({"envs": 65536, "plies": 20, "kernel": "k_rollout_full<true>"}, 65536, 20, k)
     assert not rc.matches({"envs": 65536, "plies": 20, "kernel": "k_rollout_pc"}, 65536, 20, k)
+    # a summary naming no kernel applies to none ("" is a
+    # substring of every name)
+    assert not rc.matches({"envs": 65536, "plies": 20}, 65536, 20, k)
+    assert not rc.matches({"envs": 65536, "plies": 20, "kernel": ""}, 65536, 20, k)
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "pmc.json")
+        for kern in (None, ""):
+            summ = {"envs": 65536, "plies": 20, "hbm_bytes_per_launch": 1}
+            if kern is not None:
+                summ["kernel"] = kern
+            json.dump(summ, open(p, "w"))
+            assert bench.load_traffic(p, 65536, 20, k) is None
+        json.dump({"envs": 65536, "plies": 20, "hbm_bytes_per_launch": 1, "kernel": "k_rollout_pp_full"},
+                  open(p, "w"))
+        assert bench.load_traffic(p, 65536, 20, k) == 1
 
 
 def test_cpu_baseline_handover_needs_this_launchs_marker(monkeypatch):

@@ -42,9 +42,11 @@ def launched_kernel(full, plies):
 
 def matches(summary, envs, plies, kernel):
     """A PMC/SQ summary applies only if it was measured at this shape on this
-    kernel (its `kernel` filter is a prefix of the launched kernel's name)."""
+    kernel (its `kernel` filter is a prefix of the launched kernel's name; a
+    summary that names no kernel applies to none)."""
+    k = summary.get("kernel") if summary is not None else None
     return (summary is not None and summary.get("envs") == envs and summary.get("plies") == plies
-            and summary.get("kernel", "") in kernel)
+            and bool(k) and k in kernel)
 
 
 def check(label, full, envs, plies, kernel_ms, line_frac, line_issue):
