@@ -130,6 +130,50 @@ __device__ __noinline__ int64_t nearest_positive(const float* __restrict__ p, in
   return k;
 }
 
+// sample j's row k and its unnormalised weight x (every lane of the wave
+// gets both; the wave must be converged)
+__device__ __forceinline__ void per_sample_row(const float* __restrict__ p, const float* __restrict__ cdf, int64_t n,
+                                               int j, uint32_t k0, uint32_t k1, uint32_t ctr, double beta, int lane,
+                                               int64_t& k_out, float& x_out, float& u_out) {
+  const float total = cdf[n - 1];
+  uint32_t r[4];
+  narde::philox4x32_10(ctr, (uint32_t)j, 0u, 7u, k0, k1, r);
+  const float u = (float)(r[0] >> 8) * (1.0f / 16777216.0f);
+  const float v = u * total;
+  // the first k in [lo, lo + len) with cdf[k] > v, or lo + len if none
+  int64_t lo = 0, len = n;
+  bool split = false;  // a split range ends in a row > v
+  while (len > 1) {
+    const int64_t step = (len + 63) / 64;
+    const int64_t off = (int64_t)(lane + 1) * step - 1;
+    const int64_t piv = lo + (off < len ? off : len - 1);
+    const uint64_t hit = __ballot(cdf[piv] > v);
+    if (hit == 0ull) {  // only possible in the first round: no row > v
+      lo += len;
+      len = 0;
+      break;
+    }
+    const int64_t f = (int64_t)__builtin_ctzll(hit);
+    const int64_t nlo = lo + f * step;
+    const int64_t end = lo + len;
+    len = (nlo + step < end ? nlo + step : end) - nlo;
+    lo = nlo;
+    split = true;
+  }
+  if (len == 1 && !split && !(cdf[lo] > v)) lo += 1;  // n == 1: the range was never split
+  int64_t k = lo < n - 1 ? lo : n - 1;
+  // never a zero-priority (pending) row: the clamp above (u * total
+  // rounded up to total) or a prefix sum whose flat run steps by an ulp
+  // (a scan's association differs across tiles) can land on one, and its
+  // weight (n * 0)^-beta = inf would turn the batch's weights into NaN.
+  // Take the last row before k with p > 0 (64 rows per round; the first
+  // one after k if there is none), as DeviceReplay.sample() does.
+  if (!(p[k] > 0.0f)) k = nearest_positive(p, n, k, lane);
+  k_out = k;
+  x_out = powf((float)n * (p[k] / total), -(float)beta);
+  u_out = u;
+}
+
 __global__ void __launch_bounds__(64 * kSampleWaves) k_per_sample(const float* __restrict__ p,
                                                                   const float* __restrict__ cdf, int64_t n,
                                                                   int batch, uint32_t k0, uint32_t k1,
@@ -141,46 +185,53 @@ __global__ void __launch_bounds__(64 * kSampleWaves) k_per_sample(const float* _
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int j = blockIdx.x * kSampleWaves + wave;
   if (j < batch) {  // wave-uniform
-    const float total = cdf[n - 1];
-    uint32_t r[4];
-    narde::philox4x32_10((uint32_t)*counter, (uint32_t)j, 0u, 7u, k0, k1, r);
-    const float u = (float)(r[0] >> 8) * (1.0f / 16777216.0f);
-    const float v = u * total;
-    // the first k in [lo, lo + len) with cdf[k] > v, or lo + len if none
-    int64_t lo = 0, len = n;
-    bool split = false;  // a split range ends in a row > v
-    while (len > 1) {
-      const int64_t step = (len + 63) / 64;
-      const int64_t off = (int64_t)(lane + 1) * step - 1;
-      const int64_t piv = lo + (off < len ? off : len - 1);
-      const uint64_t hit = __ballot(cdf[piv] > v);
-      if (hit == 0ull) {  // only possible in the first round: no row > v
-        lo += len;
-        len = 0;
-        break;
-      }
-      const int64_t f = (int64_t)__builtin_ctzll(hit);
-      const int64_t nlo = lo + f * step;
-      const int64_t end = lo + len;
-      len = (nlo + step < end ? nlo + step : end) - nlo;
-      lo = nlo;
-      split = true;
-    }
-    if (len == 1 && !split && !(cdf[lo] > v)) lo += 1;  // n == 1: the range was never split
-    int64_t k = lo < n - 1 ? lo : n - 1;
-    // never a zero-priority (pending) row: the clamp above (u * total
-    // rounded up to total) or a prefix sum whose flat run steps by an ulp
-    // (a scan's association differs across tiles) can land on one, and its
-    // weight (n * 0)^-beta = inf would turn the batch's weights into NaN.
-    // Take the last row before k with p > 0 (64 rows per round; the first
-    // one after k if there is none), as DeviceReplay.sample() does.
-    if (!(p[k] > 0.0f)) k = nearest_positive(p, n, k, lane);
-    const float x = powf((float)n * (p[k] / total), -(float)*beta);
+    int64_t k;
+    float x, u;
+    per_sample_row(p, cdf, n, j, k0, k1, (uint32_t)*counter, *beta, lane, k, x, u);
     if (lane == 0) {
       idx_out[j] = k;
       w_out[j] = x;
       if (u_out) u_out[j] = u;
     }
+  }
+}
+
+// k_per_sample and k_gather_batch in one launch (round 6): the wave that
+// found sample j's row copies its minibatch row -- s = obs[k], ns =
+// obs[(k + stride) % cap] (lane l: columns l, l + 64, ...), a / r / d -- and
+// writes the UNNORMALISED weight: k_dqn_loss_prio divides by the batch max
+// and steps beta and the counter (k_per_finish's work, in its one block).
+// Same rows, same weights, one launch and one kernel boundary fewer twice.
+__global__ void __launch_bounds__(64 * kSampleWaves) k_per_sample_gather(
+    const float* __restrict__ p, const float* __restrict__ cdf, int64_t n, int batch, uint32_t k0, uint32_t k1,
+    const int64_t* __restrict__ counter, const double* __restrict__ beta, int64_t* __restrict__ idx_out,
+    float* __restrict__ w_out, int ss, const float* __restrict__ obs, int64_t stride, int64_t cap,
+    const int64_t* __restrict__ action, const float* __restrict__ reward, const float* __restrict__ done,
+    float* __restrict__ s, float* __restrict__ ns, int64_t* __restrict__ a, float* __restrict__ r,
+    float* __restrict__ d) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = blockIdx.x * kSampleWaves + wave;
+  if (j >= batch) return;  // wave-uniform
+  int64_t k;
+  float x, u;
+  per_sample_row(p, cdf, n, j, k0, k1, (uint32_t)*counter, *beta, lane, k, x, u);
+  int64_t kn = k + stride;
+  if (kn >= cap) kn -= cap;
+  const float* so = obs + k * ss;
+  const float* no = obs + kn * ss;
+  float* sd = s + (size_t)j * ss;
+  float* nd = ns + (size_t)j * ss;
+  for (int c = lane; c < ss; c += 64) {
+    sd[c] = so[c];
+    nd[c] = no[c];
+  }
+  if (lane == 0) {
+    idx_out[j] = k;
+    w_out[j] = x;
+    a[2 * j] = action[2 * k];
+    a[2 * j + 1] = action[2 * k + 1];
+    r[j] = reward[k];
+    d[j] = done[k];
   }
 }
 
@@ -253,6 +304,53 @@ __global__ void __launch_bounds__(256) k_rowmax_addend(const float* __restrict__
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
   if (lane == 0) out[i] = m;
+}
+
+// The target heads' maxima in one launch (round 6): per row i (one wave),
+// m1 = max_c nq1[i][c] and am1 = its argmax with torch.max(dim)'s rules (a
+// NaN wins, ties go to the lowest code), then m2 = max_c base[i][c] +
+// tab[am1][c] (k_rowmax_addend's sum) -- torch's max reduction and
+// k_rowmax_addend were two launches.
+__device__ __forceinline__ bool gt_or_nan(float a, int ia, float b, int ib) {
+  if (a != a) return b != b ? ia < ib : true;
+  if (b != b) return false;
+  return a == b ? ia < ib : a > b;
+}
+
+__global__ void __launch_bounds__(256) k_target_max2(const float* __restrict__ nq1, int64_t ld1,
+                                                     const float* __restrict__ base, int64_t ld,
+                                                     const float* __restrict__ tab, int64_t ld_tab, int n,
+                                                     float* __restrict__ m1, int64_t* __restrict__ am1,
+                                                     float* __restrict__ m2) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (int)(threadIdx.x >> 6);
+  if (i >= n) return;
+  const float* qr = nq1 + (size_t)i * (size_t)ld1;
+  float bv = qr[lane];
+  int bi = lane;
+#pragma unroll
+  for (int j = 1; j < 9; ++j) {
+    const float v = qr[64 * j + lane];
+    if (gt_or_nan(v, 64 * j + lane, bv, bi)) { bv = v; bi = 64 * j + lane; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (gt_or_nan(ov, oi, bv, bi)) { bv = ov; bi = oi; }
+  }
+  const float* br = base + (size_t)i * (size_t)ld;
+  const float* tr = tab + (size_t)bi * (size_t)ld_tab;
+  float m = -__builtin_inff();
+#pragma unroll
+  for (int j = 0; j < 9; ++j) m = fmaxf(m, br[64 * j + lane] + tr[64 * j + lane]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if (lane == 0) {
+    m1[i] = bv;
+    if (am1) am1[i] = bi;
+    m2[i] = m;
+  }
 }
 
 // ------------------------------------------- the online heads, gathered
@@ -588,6 +686,69 @@ __global__ void __launch_bounds__(kLearnThreads) k_prio_update(const int64_t* __
   }
 }
 
+// k_per_finish, k_dqn_loss and k_prio_update in one block (round 6; the
+// three were one-block kernels back to back): the batch max of the raw
+// importance weights (k_per_sample_gather's) and w_j / max written back to
+// w; the loss, td and dloss/dq exactly as k_dqn_loss; then the priorities,
+// the running max priority, epsilon, the write cursor and the step tag as
+// k_prio_update, and beta / the sampling counter as k_per_finish.  The
+// priorities move before the backward and Adam: nothing between reads them
+// (the next step's sample does).
+__global__ void __launch_bounds__(kLearnThreads) k_dqn_loss_prio(
+    const float* __restrict__ q1, const float* __restrict__ q2, const float* __restrict__ m1,
+    const float* __restrict__ m2, const float* __restrict__ r, const float* __restrict__ d, float* __restrict__ w,
+    int batch, float gamma, float* __restrict__ td, float* __restrict__ loss, float* __restrict__ loss_copy,
+    float* __restrict__ g1, float* __restrict__ g2, const int64_t* __restrict__ idx, float eps,
+    float* __restrict__ prio, float* __restrict__ max_prio, float* __restrict__ epsilon, float eps_min,
+    float eps_decay, int64_t* __restrict__ cursor, int64_t cursor_add, int64_t cursor_mod, int64_t* __restrict__ tag,
+    int64_t* __restrict__ counter, double* __restrict__ beta, double beta_inc) {
+#pragma clang fp contract(off)
+  __shared__ float red[kLearnThreads / 64];
+  // k_per_finish: the batch max (from 0, as there), then every w normalised
+  float wm = 0.0f;
+  for (int i = threadIdx.x; i < batch; i += kLearnThreads) wm = fmaxf(wm, w[i]);
+  const float wmax = block_max(wm, red);
+  const float inv_b = 1.0f / (float)batch;
+  float s1 = 0.0f, s2 = 0.0f, pm = -__builtin_inff();
+  for (int j = threadIdx.x; j < batch; j += kLearnThreads) {
+    const float wj = w[j] / wmax;
+    w[j] = wj;
+    const float nd = (1.0f - d[j]) * gamma;
+    const float t1 = r[j] + nd * m1[j];
+    const float t2 = r[j] + nd * m2[j];
+    const float e1 = q1[j] - t1, e2 = q2[j] - t2;
+    const float a = fabsf(t1 - q1[j]) + fabsf(t2 - q2[j]);
+    const float tdj = fminf(fmaxf(a, 0.0f), 100.0f);
+    td[j] = tdj;
+    s1 += wj * (e1 * e1);
+    s2 += wj * (e2 * e2);
+    const float gw = inv_b * wj;
+    g1[j] = gw * (2.0f * e1);
+    g2[j] = gw * (2.0f * e2);
+    const float pr = tdj + eps;
+    prio[idx[j]] = pr;
+    pm = fmaxf(pm, pr);
+  }
+  s1 = block_sum(s1, red);
+  s2 = block_sum(s2, red);
+  pm = block_max(pm, red);
+  if (threadIdx.x == 0) {
+    const float l = s1 / (float)batch + s2 / (float)batch;
+    *loss = l;
+    if (loss_copy) *loss_copy = l;
+    *max_prio = fmaxf(*max_prio, pm);
+    if (epsilon) {
+      const float e = *epsilon;
+      *epsilon = e > eps_min ? e * eps_decay : e;
+    }
+    if (cursor) *cursor = (*cursor + cursor_add) % cursor_mod;
+    if (tag) *tag += 1;
+    const double b = *beta + beta_inc;
+    *beta = b < 1.0 ? b : 1.0;
+    *counter += 1;
+  }
+}
+
 // ------------------------------------------------ grad clip + Adam, fused
 // clip_grad_norm_(max_norm) followed by Adam (torch.optim.Adam's update:
 // m <- lerp(m, g, 1 - b1), v <- b2 v + (1 - b2) g^2, p -= lr / bc1 * m /
@@ -674,6 +835,79 @@ __global__ void __launch_bounds__(256) k_adam(ParamTable t, const float* __restr
   t.p[k][i] -= sc[0] * m / (sqrtf(v) / sc[1] + eps);
 }
 
+// The same two passes over float4s (round 6), when every tensor's size is a
+// multiple of 4 and every pointer 16-byte aligned: one 16-byte load per
+// thread and operand instead of a loop of dependent 4-byte loads (k_grad_sqnorm
+// ran ~16 per thread, each an L2 round trip: 11.4 us; k_adam 11.5 us, 2,900
+// blocks each adding the partials first).  A float4 never spans two tensors.
+__global__ void __launch_bounds__(256) k_grad_sqnorm4(ParamTable t, float* __restrict__ partial,
+                                                      int64_t* __restrict__ step) {
+  __shared__ float red[4];
+  const int64_t total4 = t.off[t.count] >> 2;
+  float acc = 0.0f;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total4; e += (int64_t)gridDim.x * 256) {
+    const int k = tensor_of(t, 4 * e);
+    const float4 g = reinterpret_cast<const float4*>(t.g[k] + (4 * e - t.off[k]))[0];
+    acc += ((g.x * g.x + g.y * g.y) + g.z * g.z) + g.w * g.w;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+    if (blockIdx.x == 0) *step += 1;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_adam4(ParamTable t, const float* __restrict__ partial, int nb,
+                                               float max_norm, const int64_t* __restrict__ step, float lr, float b1,
+                                               float b2, float eps) {
+  __shared__ float sc[3];
+  __shared__ float red[4];
+  float s = 0.0f;
+  for (int b = threadIdx.x; b < nb; b += 256) s += partial[b];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf((red[0] + red[1]) + (red[2] + red[3]));
+    const float c = max_norm / (norm + 1e-6f);
+    const float st = (float)*step;
+    const float bc1 = 1.0f - powf(b1, st), bc2 = 1.0f - powf(b2, st);
+    sc[0] = lr / bc1;
+    sc[1] = sqrtf(bc2);
+    sc[2] = c < 1.0f ? c : 1.0f;
+  }
+  __syncthreads();
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (4 * e >= t.off[t.count]) return;
+  const int k = tensor_of(t, 4 * e);
+  const int64_t i = 4 * e - t.off[k];
+  const float4 g4 = reinterpret_cast<const float4*>(t.g[k] + i)[0];
+  float4 m4 = reinterpret_cast<const float4*>(t.m[k] + i)[0];
+  float4 v4 = reinterpret_cast<const float4*>(t.v[k] + i)[0];
+  float4 p4 = reinterpret_cast<const float4*>(t.p[k] + i)[0];
+  float* gp = &m4.x;
+  float* vp = &v4.x;
+  float* pp = &p4.x;
+  const float* gg = &g4.x;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float g = gg[q] * sc[2];
+    float m = gp[q], v = vp[q];
+    m = m + (1.0f - b1) * (g - m);
+    v = b2 * v + (1.0f - b2) * (g * g);
+    gp[q] = m;
+    vp[q] = v;
+    pp[q] -= sc[0] * m / (sqrtf(v) / sc[1] + eps);
+  }
+  reinterpret_cast<float4*>(t.m[k] + i)[0] = m4;
+  reinterpret_cast<float4*>(t.v[k] + i)[0] = v4;
+  reinterpret_cast<float4*>(t.p[k] + i)[0] = p4;
+}
+
 }  // namespace
 
 extern "C" {
@@ -752,6 +986,10 @@ int narde_dqn_heads_backward(int device, const float* g1, const float* g2, const
   return check_launch("k_heads_grad_w");
 }
 
+// narde_adam_clip's form: float4 passes (default) or round 5's scalar ones
+// (narde_learner_variant, for A/B timing)
+static bool adam_vec4 = true;
+
 int narde_relu_bias_grad(int device, const float* gh, const float* h, int64_t n, int64_t cols, float* g,
                          float* db, float* scratch, void* stream) {
   if (!gh || !h || !g || !db || !scratch) return bad("NULL argument");
@@ -815,6 +1053,20 @@ int narde_adam_clip(int device, int n_tensors, float* const* params, const float
   // scratch: kNormBlocks partial sums (the words after them are unused)
   float* partial = scratch;
   DeviceGuard dg(device);
+  bool vec = adam_vec4;
+  for (int k = 0; k < n_tensors && vec; ++k)
+    vec = sizes[k] % 4 == 0 && aligned16(params[k]) && aligned16(grads[k]) && aligned16(m[k]) && aligned16(v[k]);
+  if (vec) {  // one float4 per thread (round 6)
+    const int64_t total4 = total / 4;
+    int nb4 = (int)((total4 + 255) / 256);
+    nb4 = nb4 < kNormBlocks ? nb4 : kNormBlocks;
+    k_grad_sqnorm4<<<nb4, 256, 0, (hipStream_t)stream>>>(t, partial, step);
+    const int rc = check_launch("k_grad_sqnorm4");
+    if (rc != NARDE_OK) return rc;
+    k_adam4<<<(unsigned)((total4 + 255) / 256), 256, 0, (hipStream_t)stream>>>(t, partial, nb4, max_norm, step, lr,
+                                                                              beta1, beta2, eps);
+    return check_launch("k_adam4");
+  }
   int nb = (int)((total + 256 * 16 - 1) / (256 * 16));  // ~16 elements per thread
   nb = nb < kNormBlocks ? nb : kNormBlocks;
   k_grad_sqnorm<<<nb, 256, 0, (hipStream_t)stream>>>(t, partial, step);
@@ -823,6 +1075,63 @@ int narde_adam_clip(int device, int n_tensors, float* const* params, const float
   k_adam<<<(unsigned)((total + 255) / 256), 256, 0, (hipStream_t)stream>>>(t, partial, nb, max_norm, step, lr, beta1,
                                                                            beta2, eps);
   return check_launch("k_adam");
+}
+
+int narde_per_sample_gather(int device, const float* p, const float* cdf, int64_t n, int64_t batch, uint64_t seed,
+                            const int64_t* counter, const double* beta, int64_t* idx, float* w, int state_size,
+                            const float* obs, int64_t next_stride, int64_t capacity, const int64_t* action,
+                            const float* reward, const float* done, float* s, float* ns, int64_t* a, float* r,
+                            float* d, void* stream) {
+  if (!p || !cdf || !counter || !beta || !idx || !w || !obs || !action || !reward || !done || !s || !ns || !a || !r ||
+      !d)
+    return bad("NULL argument");
+  if (n <= 0 || batch <= 0 || batch > (int64_t(1) << 24)) return bad("need n > 0 and 0 < batch <= 2^24");
+  if (state_size <= 0 || batch * state_size >= (int64_t(1) << 31)) return bad("bad sizes");
+  if (capacity <= 0 || n > capacity || next_stride < 0 || next_stride >= capacity) return bad("bad ring geometry");
+  DeviceGuard dg(device);
+  const unsigned blocks = (unsigned)((batch + kSampleWaves - 1) / kSampleWaves);
+  k_per_sample_gather<<<blocks, 64 * kSampleWaves, 0, (hipStream_t)stream>>>(
+      p, cdf, n, (int)batch, (uint32_t)seed, (uint32_t)(seed >> 32), counter, beta, idx, w, state_size, obs,
+      next_stride, capacity, action, reward, done, s, ns, a, r, d);
+  return check_launch("k_per_sample_gather");
+}
+
+int narde_target_max2(int device, const float* nq1, int64_t ld1, const float* base, int64_t ld, const float* tab,
+                      int64_t ld_tab, int64_t n, float* m1, int64_t* am1, float* m2, void* stream) {
+  if (!nq1 || !base || !tab || !m1 || !m2) return bad("NULL argument");
+  if (n < 0 || n > (int64_t(1) << 31) - 4 || ld1 < 576 || ld < 576 || ld_tab < 576) return bad("bad sizes");
+  if (n == 0) return NARDE_OK;
+  DeviceGuard dg(device);
+  k_target_max2<<<(unsigned)((n + 3) / 4), 256, 0, (hipStream_t)stream>>>(nq1, ld1, base, ld, tab, ld_tab, (int)n,
+                                                                          m1, am1, m2);
+  return check_launch("k_target_max2");
+}
+
+int narde_dqn_loss_prio(int device, const float* q1, const float* q2, const float* m1, const float* m2,
+                        const float* r, const float* d, float* w, int64_t batch, float gamma, float* td, float* loss,
+                        float* loss_copy, float* g1, float* g2, const int64_t* idx, float eps, float* prio,
+                        float* max_prio, float* epsilon, float eps_min, float eps_decay, int64_t* cursor,
+                        int64_t cursor_add, int64_t cursor_mod, int64_t* tag, int64_t* counter, double* beta,
+                        double beta_inc, void* stream) {
+  if (!q1 || !q2 || !m1 || !m2 || !r || !d || !w || !td || !loss || !g1 || !g2 || !idx || !prio || !max_prio ||
+      !counter || !beta)
+    return bad("NULL argument");
+  if (batch <= 0 || batch > (int64_t(1) << 24)) return bad("bad batch");
+  if (cursor && (cursor_mod <= 0 || cursor_add < 0)) return bad("bad cursor step");
+  DeviceGuard dg(device);
+  k_dqn_loss_prio<<<1, kLearnThreads, 0, (hipStream_t)stream>>>(q1, q2, m1, m2, r, d, w, (int)batch, gamma, td, loss,
+                                                                loss_copy, g1, g2, idx, eps, prio, max_prio, epsilon,
+                                                                eps_min, eps_decay, cursor, cursor_add, cursor_mod,
+                                                                tag, counter, beta, beta_inc);
+  return check_launch("k_dqn_loss_prio");
+}
+
+// A/B switch of the round-6 learner forms (tools, tests): bit 1 = the
+// float4 clip + Adam.  Returns the previous value.
+int narde_learner_variant(int flags) {
+  const int prev = adam_vec4 ? 2 : 0;
+  adam_vec4 = (flags & 2) != 0;
+  return prev;
 }
 
 }  // extern "C"

@@ -84,6 +84,13 @@ SIGNATURES = {
                               _vp, _vp, _vp]),
     "narde_prio_update": (_i32, [_i32, _vp, _vp, _i64, ctypes.c_float, _vp, _vp, _vp, ctypes.c_float,
                                  ctypes.c_float, _vp, _i64, _i64, _vp, _vp]),
+    "narde_per_sample_gather": (_i32, [_i32, _vp, _vp, _i64, _i64, _u64, _vp, _vp, _vp, _vp, _i32, _vp, _i64, _i64,
+                                       _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "narde_target_max2": (_i32, [_i32, _vp, _i64, _vp, _i64, _vp, _i64, _i64, _vp, _vp, _vp, _vp]),
+    "narde_dqn_loss_prio": (_i32, [_i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, ctypes.c_float, _vp, _vp, _vp,
+                                   _vp, _vp, _vp, ctypes.c_float, _vp, _vp, _vp, ctypes.c_float, ctypes.c_float, _vp,
+                                   _i64, _i64, _vp, _vp, _vp, ctypes.c_double, _vp]),
+    "narde_learner_variant": (_i32, [_i32]),
     "narde_adam_clip": (_i32, [_i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, ctypes.c_float, ctypes.c_float,
                                ctypes.c_float, ctypes.c_float, ctypes.c_float, _vp, _vp]),
     "narde_violates_block_rule": (_i32, [_i32, _vp, _i64, _vp, _vp]),

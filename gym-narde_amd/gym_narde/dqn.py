@@ -249,6 +249,30 @@ def rowmax_addend(base, tab, rows, out=None):
     return out
 
 
+def target_max2(nq1, base, tab, m1=None, am1=None, m2=None):
+    """(m1, am1, m2): nq1.max(1) (values, indices: torch's rules -- NaN wins,
+    ties to the lowest code) and rowmax_addend(base, tab, am1) in one launch
+    (k_target_max2)."""
+    n = nq1.shape[0]
+    for t in (nq1, base, tab):
+        if t.dtype != torch.float32 or t.stride(1) != 1 or t.shape[1] != MOVES:
+            raise ValueError("nq1 / base / tab must be (., 576) float32 with unit column stride")
+    z = dict(device=nq1.device)
+    m1 = torch.empty(n, dtype=torch.float32, **z) if m1 is None else m1
+    m2 = torch.empty(n, dtype=torch.float32, **z) if m2 is None else m2
+    am1 = torch.empty(n, dtype=torch.int64, **z) if am1 is None else am1
+    _lib.check(_lib.load().narde_target_max2(
+        nq1.device.index, _lib.ptr(nq1), nq1.stride(0), _lib.ptr(base), base.stride(0), _lib.ptr(tab), tab.stride(0),
+        n, _f32(m1), _lib.ptr(am1), _f32(m2), _stream(nq1.device)), "narde_target_max2")
+    return m1, am1, m2
+
+
+def learner_variant(flags):
+    """narde_learner_variant: bit 1 = the float4 clip + Adam (default), else
+    round 5's scalar passes; returns the previous flags."""
+    return int(_lib.load().narde_learner_variant(int(flags)))
+
+
 class GatheredHeads(torch.autograd.Function):
     """(q1, q2) = the online heads at the stored codes a (B,2):
     model.move1_head(f).gather(1, a[:, :1]) and
@@ -541,6 +565,44 @@ class DeviceReplay:
             _stream(p.device)), "narde_per_sample")
         return idx, w
 
+    def sample_gather_fused(self, batch, seed):
+        """sample_fused + gather in one launch (k_per_sample_gather): (idx, w,
+        s, ns, a, r, d) with w UNNORMALISED -- loss_prio_fused normalises it
+        in place and steps beta and the sampling counter."""
+        n, ss = self.rows, self.obs.shape[1]
+        p = self.prio[:n] ** self.alpha
+        cdf = torch.cumsum(p, 0)
+        z = dict(device=p.device)
+        idx = torch.empty(batch, dtype=torch.int64, **z)
+        w = torch.empty(batch, dtype=torch.float32, **z)
+        s = torch.empty((batch, ss), dtype=torch.float32, **z)
+        ns = torch.empty((batch, ss), dtype=torch.float32, **z)
+        a = torch.empty((batch, 2), dtype=torch.int64, **z)
+        r = torch.empty(batch, dtype=torch.float32, **z)
+        d = torch.empty(batch, dtype=torch.float32, **z)
+        _lib.check(_lib.load().narde_per_sample_gather(
+            p.device.index, _lib.ptr(p), _lib.ptr(cdf), n, batch, int(seed) & (2 ** 64 - 1), _lib.ptr(self.sample_ctr),
+            _lib.ptr(self.beta_t), _lib.ptr(idx), _lib.ptr(w), ss, _lib.ptr(self.obs), self.stride, self.capacity,
+            _lib.ptr(self.action), _lib.ptr(self.reward), _lib.ptr(self.done), _lib.ptr(s), _lib.ptr(ns), _lib.ptr(a),
+            _lib.ptr(r), _lib.ptr(d), _stream(p.device)), "narde_per_sample_gather")
+        return idx, w, s, ns, a, r, d
+
+    def loss_prio_fused(self, q1, q2, m1, m2, r, d, w, gamma, td, loss, idx, epsilon=None, eps_min=0.0,
+                        eps_decay=1.0, cursor_add=0, tag=None):
+        """DQNLoss.compute + update_fused + sample_fused's normalisation and
+        beta / counter steps in one block (k_dqn_loss_prio); w (raw, from
+        sample_gather_fused) is normalised in place.  Returns (g1, g2)."""
+        B = q1.shape[0]
+        g1, g2 = torch.empty_like(q1), torch.empty_like(q2)
+        _lib.check(_lib.load().narde_dqn_loss_prio(
+            q1.device.index, _f32(q1), _f32(q2), _f32(m1), _f32(m2), _f32(r), _f32(d), _f32(w), B, float(gamma),
+            _f32(td), _lib.ptr(loss), None, _lib.ptr(g1), _lib.ptr(g2), _lib.ptr(idx), float(self.epsilon),
+            _lib.ptr(self.prio), _lib.ptr(self.max_prio), None if epsilon is None else _lib.ptr(epsilon),
+            float(eps_min), float(eps_decay), _lib.ptr(self.pos_t) if cursor_add else None, int(cursor_add),
+            self.capacity, _lib.ptr(tag), _lib.ptr(self.sample_ctr), _lib.ptr(self.beta_t), float(self.beta_increment),
+            _stream(q1.device)), "narde_dqn_loss_prio")
+        return g1, g2
+
     def gather(self, idx):
         """(s, ns, a, r, d) rows of idx (k_gather_batch; ns from row
         next_index(idx))."""
@@ -586,7 +648,7 @@ class BatchedDQNDriver:
                  learning_rate=1e-4, gamma=0.99, epsilon=1.0, epsilon_min=0.01,
                  epsilon_decay=0.995, target_update=10, updates_per_step=1, shaping=True,
                  seed=0, fused=True, fused_heads=True, gathered_heads=True, fused_features=True,
-                 explore="plays", greedy="accepted"):
+                 explore="plays", greedy="accepted", one_launch_chains=True):
         if env.full:
             raise ValueError("the DQN driver plays the reference's (move1, move2) actions: rules='ref2'")
         if explore not in ("plays", "codes"):
@@ -635,6 +697,8 @@ class BatchedDQNDriver:
         # ... and its feature layers' ReLU mask + bias gradients in one kernel
         # each (LinearReLU)
         self.fused_features = bool(fused_features)
+        # round 6: the learner's one-block / one-launch chains (_update_fused6)
+        self.one_launch_chains = bool(one_launch_chains)
         self._rb_scratch = relu_bias_grad_scratch(self.train_batch, 256, self.dev)
         self.seed = seed
         self.tag_t = torch.zeros((), dtype=torch.int64, **z)
@@ -874,7 +938,12 @@ class BatchedDQNDriver:
     def _update_fused(self):
         """_update_torch with the non-GEMM chains as HIP kernels
         (csrc/dqn_learner.hip): sample, gather, target move-2 max, loss +
-        grads, priorities + epsilon.  ~40 fewer launches per update."""
+        grads, priorities + epsilon.  ~40 fewer launches per update.
+        one_launch_chains (round 6, default): sample + gather in one launch,
+        the target heads' max / argmax / move-2 max in one, and the weight
+        normalisation + loss + priorities + bookkeeping in one block."""
+        if self.one_launch_chains:
+            return self._update_fused6()
         rp = self.replay
         idx, w = rp.sample_fused(self.train_batch, self.seed)
         s, ns, a, r, d = rp.gather(idx)
@@ -898,6 +967,34 @@ class BatchedDQNDriver:
         cursor_add, tag = self._fold if self._fold is not None else (0, None)
         self._fold = None
         rp.update_fused(idx, td, self.eps_t, self.epsilon_min, self.epsilon_decay, cursor_add=cursor_add, tag=tag)
+        if self._capturing:
+            return self.loss_t
+        self._after_update()
+        return self.loss_t
+
+    def _update_fused6(self):
+        rp = self.replay
+        idx, w, s, ns, a, r, d = rp.sample_gather_fused(self.train_batch, self.seed)
+        f = features_fused(self.model, s, self._rb_scratch) if self.fused_features else self.model.features(s)
+        if self.gathered_heads:
+            q1, q2 = gathered_heads(self.model, f, a)
+        else:
+            q1 = self.model.move1_head(f).gather(1, a[:, :1]).squeeze(1)
+            q2 = self.model.move2_from_features(f, a[:, 0]).gather(1, a[:, 1:]).squeeze(1)
+        with torch.no_grad():
+            tf = self.target.features_nograd(ns)
+            nq1 = self.target.move1_head(tf)
+            wt = self.target.move2_head.weight
+            base2 = torch.nn.functional.linear(tf, wt[:, :256], self.target.move2_head.bias)
+            m1, _, m2 = target_max2(nq1, base2, self._target_onehot_rows())
+        td = torch.empty_like(r)
+        cursor_add, tag = self._fold if self._fold is not None else (0, None)
+        self._fold = None
+        g1, g2 = rp.loss_prio_fused(q1.detach(), q2.detach(), m1, m2, r, d, w, self.gamma, td, self.loss_t, idx,
+                                    self.eps_t, self.epsilon_min, self.epsilon_decay, cursor_add=cursor_add, tag=tag)
+        self.fopt.zero_grad(set_to_none=True)
+        torch.autograd.backward((q1, q2), (g1, g2))  # = loss.backward(): dloss/dq from k_dqn_loss_prio
+        self.fopt.step()  # clip_grad_norm_(10) + Adam
         if self._capturing:
             return self.loss_t
         self._after_update()

@@ -444,6 +444,41 @@ int narde_adam_clip(int device, int n_tensors, float *const *params, const float
                     float beta1, float beta2, float eps, float max_norm, float *scratch,
                     void *stream);
 
+/* Round 6's one-launch forms of the learner's chains (the calls above stay
+ * for the torch-restatement tests):
+ * narde_per_sample_gather = narde_per_sample's search + narde_gather_batch's
+ * rows in one launch, w UNNORMALISED ((n p / total)^-beta); beta and the
+ * counter are NOT stepped (narde_dqn_loss_prio does both). */
+int narde_per_sample_gather(int device, const float *p, const float *cdf, int64_t n, int64_t batch,
+                            uint64_t seed, const int64_t *counter, const double *beta, int64_t *idx,
+                            float *w, int state_size, const float *obs, int64_t next_stride,
+                            int64_t capacity, const int64_t *action, const float *reward,
+                            const float *done, float *s, float *ns, int64_t *a, float *r, float *d,
+                            void *stream);
+
+/* The target heads' maxima: m1[i] = max_c nq1[i][c], am1[i] = its argmax
+ * (torch.max(dim): NaN wins, ties to the lowest code; am1 may be NULL),
+ * m2[i] = max_c base[i][c] + tab[am1[i]][c] (narde_rowmax_addend's sum). */
+int narde_target_max2(int device, const float *nq1, int64_t ld1, const float *base, int64_t ld,
+                      const float *tab, int64_t ld_tab, int64_t n, float *m1, int64_t *am1,
+                      float *m2, void *stream);
+
+/* One block: w[j] /= max_j w[j] (narde_per_sample's normalisation, in place),
+ * then narde_dqn_loss, then narde_prio_update on the same td, then beta =
+ * min(1, beta + beta_inc) and *counter += 1 (narde_per_sample's steps). */
+int narde_dqn_loss_prio(int device, const float *q1, const float *q2, const float *m1,
+                        const float *m2, const float *r, const float *d, float *w, int64_t batch,
+                        float gamma, float *td, float *loss, float *loss_copy, float *g1, float *g2,
+                        const int64_t *idx, float eps, float *prio, float *max_prio, float *epsilon,
+                        float eps_min, float eps_decay, int64_t *cursor, int64_t cursor_add,
+                        int64_t cursor_mod, int64_t *tag, int64_t *counter, double *beta,
+                        double beta_inc, void *stream);
+
+/* A/B switch of narde_adam_clip's form: bit 1 = float4 passes where sizes
+ * and pointers allow (default), else round 5's scalar passes.  Returns the
+ * previous flags. */
+int narde_learner_variant(int flags);
+
 /* Stateless: Narde._violates_block_rule on n perspective boards i8[n][24]. */
 int narde_violates_block_rule(int device, const int8_t *boards, int64_t n, uint8_t *out,
                               void *stream);

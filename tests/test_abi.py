@@ -80,6 +80,10 @@ def test_argument_errors_are_einval_before_any_device_call():
         ("narde_dqn_loss", (0, N, N, N, N, N, N, N, 64, 0.99, N, N, N, N, N, N)),
         ("narde_prio_update", (0, N, N, 64, 0.01, N, N, N, 0.01, 0.995, N, 0, 1, N, N)),
         ("narde_adam_clip", (0, 0, N, N, N, N, N, N, 1e-3, 0.9, 0.999, 1e-8, 10.0, N, N)),
+        ("narde_per_sample_gather", (0, N, N, 100, 64, 0, N, N, N, N, 198, N, 64, 128, N, N, N, N, N, N, N, N, N)),
+        ("narde_target_max2", (0, N, 576, N, 576, N, 576, 64, N, N, N, N)),
+        ("narde_dqn_loss_prio", (0, N, N, N, N, N, N, N, 64, 0.99, N, N, N, N, N, N, 0.01, N, N, N, 0.01, 0.995,
+                                 N, 0, 1, N, N, N, 0.001, N)),
     ]
     for name, args in cases:
         rc = getattr(lib, name)(*args)

@@ -775,3 +775,168 @@ def test_sampler_never_returns_zero_priority_rows(fused):
     # the rule itself: the last positive row before, else the first after
     k = torch.tensor([2500, 5999, 0, 5, 10, 1999], device="cuda:0")
     assert nearest_positive(p, k).tolist() == [1999, 5499, 10, 10, 10, 1999]
+
+
+# ------------------------------------- round 6: the one-launch learner chains
+def _filled_replay(n=5000, ss=198, stride=1234, seed=5):
+    from gym_narde.dqn import DeviceReplay
+
+    rp = DeviceReplay(n, ss, "cuda:0", stride=stride)
+    g = torch.Generator(device="cuda:0").manual_seed(seed)
+    for t in (rp.obs, rp.reward, rp.done):
+        t.copy_(torch.rand(t.shape, device="cuda:0", generator=g))
+    rp.action.copy_(torch.randint(0, 576, rp.action.shape, device="cuda:0", generator=g))
+    rp.prio.copy_(torch.rand(n, device="cuda:0", generator=g) * 3 + 0.01)
+    rp.prio[n - stride:] = 0.0  # pending rows: never sampled
+    rp.size = n - stride
+    return rp
+
+
+def test_per_sample_gather_equals_sample_then_gather():
+    """k_per_sample_gather == k_per_sample + k_per_finish + k_gather_batch:
+    the same rows and minibatch, its raw weights normalised by their max are
+    the sampler's weights bit for bit; beta and the counter left untouched
+    (the loss block steps them)."""
+    rp = _filled_replay()
+    ctr, beta = rp.sample_ctr.clone(), rp.beta_t.clone()
+    idx, w = rp.sample_fused(4096, seed=21)
+    want = rp.gather(idx)
+    rp.sample_ctr.copy_(ctr)
+    rp.beta_t.copy_(beta)
+    idx2, w_raw, *got = rp.sample_gather_fused(4096, seed=21)
+    assert torch.equal(idx2, idx)
+    for x, y in zip(got, want):
+        assert torch.equal(x, y)
+    assert torch.equal(w_raw / w_raw.max(), w)
+    assert int(rp.sample_ctr) == int(ctr) and float(rp.beta_t) == float(beta)
+    assert bool((rp.prio[idx2] > 0).all())
+
+
+def test_target_max2_vs_torch_max_and_rowmax():
+    """k_target_max2: (values, indices) of torch.max(dim=1) -- exact ties go to
+    the lowest code, a NaN row's first NaN wins -- and the move-2 maximum of
+    k_rowmax_addend at that argmax, bit for bit."""
+    from gym_narde.dqn import rowmax_addend, target_max2
+
+    g = torch.Generator(device="cuda:0").manual_seed(8)
+    n = 4099
+    nq1 = torch.randn((n, 576), device="cuda:0", generator=g)
+    nq1[::7] = torch.round(nq1[::7])          # many exact ties
+    nq1[5, 300] = float("nan")
+    nq1[6, 17] = float("nan")
+    nq1[6, 400] = float("nan")
+    base = torch.randn((n, 576), device="cuda:0", generator=g)
+    tab = torch.randn((576, 576), device="cuda:0", generator=g)
+    m1, am1, m2 = target_max2(nq1, base, tab)
+    v, i = nq1.max(1)
+    assert torch.equal(am1, i)
+    assert torch.equal(m1[~v.isnan()], v[~v.isnan()]) and bool(m1[v.isnan()].isnan().all())
+    assert int(am1[5]) == 300 and int(am1[6]) == 17
+    assert torch.equal(m2, rowmax_addend(base, tab, am1))
+    # ties: the lowest code holding the row maximum
+    rows = torch.arange(0, n, 7, device="cuda:0")
+    first = (nq1[rows] == v[rows, None]).int().argmax(1)
+    assert torch.equal(am1[rows], first)
+
+
+def test_loss_prio_block_equals_the_three_kernels():
+    """k_dqn_loss_prio == the weight normalisation, k_dqn_loss and
+    k_prio_update (+ beta / counter steps): td, dloss/dq, the loss, the
+    priorities, max priority, epsilon, cursor and tag, bit for bit."""
+    from gym_narde.dqn import DQNLoss
+
+    B, gamma = 4096, 0.99
+    rp = _filled_replay(n=20000, stride=64)
+    g = torch.Generator(device="cuda:0").manual_seed(12)
+    rnd = lambda: torch.randn(B, device="cuda:0", generator=g)  # noqa: E731
+    q1, q2, m1, m2 = rnd(), rnd(), rnd(), rnd()
+    r = (torch.rand(B, device="cuda:0", generator=g) < 0.1).float() * 2
+    d = (torch.rand(B, device="cuda:0", generator=g) < 0.2).float()
+    w_raw = torch.rand(B, device="cuda:0", generator=g) * 5 + 0.1
+    idx = torch.randperm(20000 - 64, device="cuda:0", generator=g)[:B]
+    # the unfused sequence on copies
+    prio0, maxp0, ctr0, beta0 = rp.prio.clone(), rp.max_prio.clone(), rp.sample_ctr.clone(), rp.beta_t.clone()
+    pos0 = rp.pos_t.clone()
+    eps_a = torch.full((), 0.5, device="cuda:0")
+    tag_a = torch.zeros((), dtype=torch.int64, device="cuda:0")
+    w_n = w_raw / w_raw.max()
+    td_a = torch.empty(B, device="cuda:0")
+    loss_a, g1a, g2a = DQNLoss.compute(q1, q2, m1, m2, r, d, w_n, gamma, td_a, None)
+    rp.update_fused(idx, td_a, eps_a, 0.01, 0.995, cursor_add=64, tag=tag_a)
+    prio_a, maxp_a, pos_a = rp.prio.clone(), rp.max_prio.clone(), rp.pos_t.clone()
+    # the fused block from the same state
+    rp.prio.copy_(prio0); rp.max_prio.copy_(maxp0); rp.pos_t.copy_(pos0)
+    eps_b = torch.full((), 0.5, device="cuda:0")
+    tag_b = torch.zeros((), dtype=torch.int64, device="cuda:0")
+    td_b = torch.empty(B, device="cuda:0")
+    loss_b = torch.empty((), device="cuda:0")
+    w_b = w_raw.clone()
+    g1b, g2b = rp.loss_prio_fused(q1, q2, m1, m2, r, d, w_b, gamma, td_b, loss_b, idx, eps_b, 0.01, 0.995,
+                                  cursor_add=64, tag=tag_b)
+    assert torch.equal(w_b, w_n)
+    assert torch.equal(td_b, td_a) and torch.equal(g1b, g1a) and torch.equal(g2b, g2a)
+    assert float(loss_b) == float(loss_a)
+    assert torch.equal(rp.prio, prio_a) and float(rp.max_prio) == float(maxp_a) and int(rp.pos_t) == int(pos_a)
+    assert float(eps_b) == float(eps_a) and int(tag_b) == int(tag_a) == 1
+    assert int(rp.sample_ctr) == int(ctr0) + 1
+    assert float(rp.beta_t) == min(1.0, float(beta0) + rp.beta_increment)
+
+
+def test_adam_float4_vs_scalar_kernels():
+    """narde_adam_clip's float4 passes (round 6) against round 5's scalar
+    ones: the same clipped Adam steps to fp32 rounding, both deterministic."""
+    import copy
+
+    from gym_narde.dqn import DecomposedDQN, FusedAdamClip, learner_variant
+
+    torch.manual_seed(4)
+    a = DecomposedDQN(198).cuda()
+    b = copy.deepcopy(a)
+    fa = FusedAdamClip(a.parameters(), lr=1e-3, max_norm=10.0)
+    fb = FusedAdamClip(b.parameters(), lr=1e-3, max_norm=10.0)
+    g = torch.Generator(device="cuda:0").manual_seed(6)
+    prev = learner_variant(2)
+    try:
+        for _ in range(3):
+            grads = [torch.randn(p.shape, device="cuda:0", generator=g) * 5 for p in a.parameters()]
+            for p, q, gr in zip(a.parameters(), b.parameters(), grads):
+                p.grad = gr.clone()
+                q.grad = gr.clone()
+            learner_variant(2)
+            fa.step()
+            learner_variant(0)
+            fb.step()
+    finally:
+        learner_variant(prev)
+    for p, q in zip(a.parameters(), b.parameters()):
+        assert torch.allclose(p, q, rtol=1e-5, atol=1e-6)
+    assert int(fa.step_t) == int(fb.step_t) == 3
+
+
+def test_one_launch_learner_equals_round5_learner():
+    """Two drivers from the same seed, one with round 6's one-launch chains
+    and one with round 5's: the same losses, priorities and parameters over
+    three updates (the fused chains compute the same fp32 values; only the
+    clip's norm sums in another order)."""
+    from gym_narde.dqn import BatchedDQNDriver
+    from gym_narde.vector import VecNardeEnv
+
+    drv = []
+    for one in (True, False):
+        env = VecNardeEnv(4096, device="cuda:0", seed=41)
+        drv.append(BatchedDQNDriver(env, capacity=1 << 14, train_batch=1024, seed=3, one_launch_chains=one))
+    losses = [[], []]
+    for _ in range(6):
+        for k, d in enumerate(drv):
+            l = d.step()
+            if l is not None:
+                losses[k].append(float(l))
+    torch.cuda.synchronize()
+    assert len(losses[0]) >= 2 and len(losses[0]) == len(losses[1])
+    for x, y in zip(*losses):
+        assert x == pytest.approx(y, rel=1e-4, abs=1e-6)
+    for (k, p), (_, q) in zip(drv[0].model.state_dict().items(), drv[1].model.state_dict().items()):
+        assert torch.allclose(p, q, rtol=1e-4, atol=1e-5), k
+    assert int(drv[0].replay.sample_ctr) == int(drv[1].replay.sample_ctr)
+    assert float(drv[0].replay.beta_t) == float(drv[1].replay.beta_t)
+    assert float(drv[0].eps_t) == float(drv[1].eps_t) and int(drv[0].tag_t) == int(drv[1].tag_t)

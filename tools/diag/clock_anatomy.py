@@ -32,8 +32,10 @@ def main():
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     e1.record()
-    L = env.rollout_launcher(P, b, events=(e0, e1))
+    rows = torch.empty(((65536 + 255) // 256, 3), dtype=torch.int64, device="cuda:0")
+    L = env.rollout_launcher(P, b, events=(e0, e1), totals=rows)  # the bench's timed launch
     res = []
+    trials = []
     for trial in range(5):
         for _ in range(120 if trial == 0 else 3):
             ramp()
@@ -49,20 +51,28 @@ def main():
         assert lib.narde_diag_ts(ts.ctypes.data_as(ctypes.c_void_p)) == 0
         ts = ts[:2048]
         t0 = ts[:, 0].min()
-        rel = (ts - t0) * 0.01  # us
+        rel = np.where(ts > 0, (ts - t0) * 0.01, np.nan)  # us
         prod = np.array([w % 8 < 4 for w in range(2048)])
         nb = 2 + (P - 3 + 3) // 4 if P > 3 else (1 if P <= 1 else 2)
         out = {"plies": P, "stats_only": stats, "event_span_us": round(e0.elapsed_time(e1) * 1e3, 2),
-               "in_kernel_span_us": round(float(rel[:, 63].max()), 2)}
-        cols = {"entry": 0, "start_barrier": 1}
-        for k in range(min(nb, 60)):
-            cols[f"block{k}"] = 2 + k
-        cols["end"] = 63
+               "in_kernel_span_us": round(float(np.nanmax(rel[:, 63])), 2)}
+        cols = {"entry": 0, "loaded_or_drawn": 1, "start_barrier": 2}
+        for k in range(min(nb, 56)):
+            cols[f"block{k}"] = 3 + k
+        cols.update({"last_emit": 59, "record_stored": 60, "stats_loaded": 61, "totals": 62, "end": 63})
         for name, c in cols.items():
-            v = rel[prod, c]
-            out[name] = [round(float(np.percentile(v, q)), 2) for q in (0, 50, 100)]
+            for who, m in (("prod", prod), ("cons", ~prod)):
+                v = rel[m, c]
+                v = v[~np.isnan(v)]
+                if len(v):
+                    out[f"{name}.{who}"] = [round(float(np.percentile(v, q)), 2) for q in (0, 50, 100)]
+        ts0 = ts[:, 0]
+        ts0 = ts0[ts0 > 0]
+        trials.append(rel)
         res.append(out)
-    print(json.dumps(res[-1]))
+    print(json.dumps(res[-1], indent=0))
+    if len(sys.argv) > 3:
+        np.save(sys.argv[3], np.stack(trials))
     print(json.dumps({"event_span_us": [r["event_span_us"] for r in res],
                       "in_kernel_span_us": [r["in_kernel_span_us"] for r in res]}))
 

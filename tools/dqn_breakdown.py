@@ -7,7 +7,7 @@
 
 Splits every graph-replayed step of the trace (BatchedDQNDriver._step_body,
 gym_narde/dqn.py) at its env step: `act` = the kernels from the previous
-step's last learner kernel (k_prio_update) up to k_step (the 65,536-row
+step's last learner kernel (k_prio_update, or round 6's k_adam4) up to k_step (the 65,536-row
 feature GEMMs, the two head-policy kernels, the masks, the exploration
 draw), `env` = k_step + k_dqn_transition, `update` = the rest (the 4,096-row
 learner: sampling, gathers, GEMMs, loss, gradients, clip + Adam, priority
@@ -42,14 +42,16 @@ def main():
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     ks = [(r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in rows]
     step_ix = [j for j, k in enumerate(ks) if "k_step<false>" in k[0]]
-    prio_ix = [j for j, k in enumerate(ks) if "k_prio_update" in k[0]]
+    # a learner ends at k_prio_update (round 5) or at its clip + Adam
+    # (round 6: the priorities ride in k_dqn_loss_prio, before the backward)
+    prio_ix = [j for j, k in enumerate(ks) if "k_prio_update" in k[0] or "k_adam" in k[0]]
     steps = []
     for s0, s1 in zip(step_ix, step_ix[1:]):
         before = [p for p in prio_ix if p < s0]
         if not before:
             continue
         a0 = before[-1] + 1
-        end = max(p for p in prio_ix if p < s1)  # this step's learner ends at its k_prio_update
+        end = max(p for p in prio_ix if p < s1)  # this step's learner ends at its last marker
         act = ks[a0:s0]
         env = [k for k in ks[s0:end + 1] if "k_step<false>" in k[0] or "k_dqn_transition" in k[0]]
         upd = [k for k in ks[s0:end + 1] if k not in env]

@@ -1,7 +1,8 @@
 """Profiling target for the config-4 DQN driver (rocprofv3 --kernel-trace):
 B envs, graph-captured step, N replays.  argv: [B] [steps] [eager];
 $NARDE_GATHERED=0 takes the dense online heads in the learner,
-$NARDE_FUSED_FEATURES=0 autograd's feature-layer backward."""
+$NARDE_FUSED_FEATURES=0 autograd's feature-layer backward, $NARDE_ONE_LAUNCH=0
+round 5's learner (no one-launch chains, scalar clip + Adam)."""
 import os
 import sys
 import time
@@ -20,7 +21,12 @@ if os.environ.get("NARDE_TUNED_GEMMS", "1") == "1":
 env = VecNardeEnv(B, device="cuda:0", seed=1)
 drv = BatchedDQNDriver(env, train_batch=4096, capacity=max(1 << 20, 4 * B),
                        gathered_heads=os.environ.get("NARDE_GATHERED", "1") == "1",
-                       fused_features=os.environ.get("NARDE_FUSED_FEATURES", "1") == "1")
+                       fused_features=os.environ.get("NARDE_FUSED_FEATURES", "1") == "1",
+                       one_launch_chains=os.environ.get("NARDE_ONE_LAUNCH", "1") == "1")
+if os.environ.get("NARDE_ONE_LAUNCH", "1") != "1":  # round 5's learner forms throughout
+    from gym_narde.dqn import learner_variant
+
+    learner_variant(0)
 if not eager:
     drv.capture_graph(warmup=2)
 for _ in range(3):

@@ -6,6 +6,7 @@ set -o pipefail
 TAG=${1:-r06}
 PHASE=${2:-parity}
 OUT=gpurun_out/$TAG
+ROOT=$(pwd)
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 T="python -u -m pytest -x -v --timeout 200 --timeout-method thread"
@@ -21,5 +22,20 @@ drv)  # the driver's command, with and without the checker leg, alternating
       && timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-parity-check --no-cpu-baseline \
            > "$OUT/drv_nochk_$k.json" 2> "$OUT/drv_nochk_$k.err" || exit 1
   done ;;
+clock)  # per-wave stamps of the driver's timed REF2 launch (tools/diag/build_clock.py, built beforehand)
+  for P in 20 1000; do
+    timeout -k 10 120 python tools/diag/clock_anatomy.py $P x "$OUT/clock_p$P.npy" > "$OUT/clock_p$P.json" 2> "$OUT/clock_p$P.err" || exit 1
+  done ;;
+pp)  # FULL4 rollout per-ply clocks by kind of turn (tools/diag/build_ppclock.py, built beforehand)
+  timeout -k 10 180 python tools/diag/pp_phase.py > "$OUT/pp_phase.json" 2> "$OUT/pp_phase.err" ;;
+dqn)  # the DQN learner's tests, then a graph-replayed trace of the driver (both learner forms)
+  timeout -k 10 400 $T tests/test_gpu_dqn.py -m gpu > "$OUT/pytest_dqn.log" 2>&1 \
+    && (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/dqn_trace" -o dqn \
+          -- python3 "$ROOT/tools/dqn_target.py" 65536 20 > "$ROOT/$OUT/dqn_trace.log" 2>&1) \
+    && (cd /tmp && NARDE_ONE_LAUNCH=0 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/dqn_trace_r5" -o dqn \
+          -- python3 "$ROOT/tools/dqn_target.py" 65536 20 > "$ROOT/$OUT/dqn_trace_r5.log" 2>&1) \
+    && timeout -k 10 120 python3 tools/dqn_target.py 65536 30 > "$OUT/dqn_time.log" 2>&1 \
+    && NARDE_ONE_LAUNCH=0 timeout -k 10 120 python3 tools/dqn_target.py 65536 30 >> "$OUT/dqn_time.log" 2>&1
+  rc=$?; tail -3 "$OUT/pytest_dqn.log"; cat "$OUT/dqn_time.log"; exit $rc ;;
 *) echo "unknown phase $PHASE"; exit 2 ;;
 esac
