@@ -1183,10 +1183,15 @@ extern "C" int64_t hc_ply_bound_turn_random(int64_t waves, uint32_t seed, int64_
 // play `plies` plies with env_turn_full; every searching block-bound
 // doubles turn met (f4_safe_bound < 4, a non-empty filtered root list) is
 // kept, and the kept turns are replayed 64 to a wave through ply_bound_turn
-// against env_turn_full.  Returns the lanes that differ; counts[0] = turns
-// kept, counts[1] = of them, turns whose sub-move 1 checks differ between
-// one and two more sub-moves for the source the turn picks (the case that
-// tells the pair pass's two result sets apart), counts[2] = waves run.
+// against env_turn_full, every field hc_ply_bound_turn_random compares.
+// Returns the lanes that differ; counts[0] = turns kept, counts[1] = of
+// them, turns whose sub-move 1 checks differ between one and two more
+// sub-moves for the source the turn picks (the case that tells the pair
+// pass's two result sets apart), counts[2] = waves run, counts[3] = kept
+// turns coop_pair_w leaves to coop_depth_w (more than 8 root sources, or a
+// list after some source longer than 8), counts[4] = kept turns whose
+// sub-move 1 takes the pair pass's checked list (done there, M >= 3) -- so
+// the caller can assert that both branches of the pass ran.
 extern "C" int64_t hc_pair_pass_selfplay(int64_t envs, int64_t plies, int64_t* counts) {
   struct Kept {
     Side s;
@@ -1201,7 +1206,7 @@ extern "C" int64_t hc_pair_pass_selfplay(int64_t envs, int64_t plies, int64_t* c
     S[i] = side_reset(r[0]);
     S[i].t = 0;
   }
-  counts[0] = counts[1] = counts[2] = 0;
+  counts[0] = counts[1] = counts[2] = counts[3] = counts[4] = 0;
   for (int64_t p = 0; p < plies; ++p) {
     for (int64_t i = 0; i < envs; ++i) {
       Side& s = S[i];
@@ -1225,10 +1230,24 @@ extern "C" int64_t hc_pair_pass_selfplay(int64_t envs, int64_t plies, int64_t* c
           k.d = dh;
           for (int j = 0; j < 4; ++j) k.w[j] = w[j];
           kept.push_back(k);
+          // coop_pair_w's branch for this owner: the pairs (<= 8 root sources,
+          // <= 8 entries after each) or coop_depth_w's fallback
+          bool wide = __builtin_popcount(Lb) > 8;
+          for (uint32_t m = Lb; m && !wide; m &= m - 1u) {
+            const int q = __builtin_ctz(m);
+            Side a = s;
+            apply_die(a, q, dh);
+            uint32_t L1 = die_candidates_sl(a.O, a.P, dh);
+            L1 &= ~block_reject_w(a.O, a.S1o, fw, L1, dh);
+            if (hl - (q == 23 ? 1 : 0) <= 0) L1 &= ~HEAD;
+            wide = __builtin_popcount(L1) > 8;
+          }
           // the source env_turn_full's first pick takes, and its sub-move 1 sets
           Side e = s;
           TurnOut oe;
           env_turn_full(e, dh, dh, false, 0ull, w, oe);
+          counts[3] += wide;
+          counts[4] += !wide && oe.max_dice >= 3;
           if (oe.max_dice == 4) {
             const int p0 = (int)(oe.played & 0xFFu);
             Side a = s;
@@ -1296,8 +1315,10 @@ extern "C" int64_t hc_pair_pass_selfplay(int64_t envs, int64_t plies, int64_t* c
       side_to_record(got[l], a1, b1);
       side_to_record(e, a2, b2);
       const bool same = o[l].legal == oe.legal && o[l].played == oe.played && o[l].term == oe.term &&
-                        o[l].max_dice == oe.max_dice && a1.x == a2.x && a1.y == a2.y && a1.z == a2.z &&
-                        a1.w == a2.w && b1.x == b2.x && b1.y == b2.y && b1.z == b2.z;
+                        o[l].reward == oe.reward && o[l].max_dice == oe.max_dice && a1.x == a2.x &&
+                        a1.y == a2.y && a1.z == a2.z && a1.w == a2.w && b1.x == b2.x && b1.y == b2.y &&
+                        b1.z == b2.z && got[l].O == e.O && got[l].P == e.P && got[l].S1o == e.S1o &&
+                        got[l].S1p == e.S1p;
       bad += same ? 0 : 1;
     }
   }

@@ -405,13 +405,17 @@ def test_hostcheck_pair_pass_selfplay_turns(hostcheck):
     emulated lanes == env_turn_full, lane by lane, including the turns whose
     sub-move-1 check differs between one and two more sub-moves (the case
     that tells the pass's two result sets apart; a mutant taking the wrong
-    set fails on them)."""
+    set fails on them); every field of the turn compared (reward, the
+    record, the O / P / S1 masks), and both branches of the pass met."""
     f = hostcheck.hc_pair_pass_selfplay
     f.restype = ctypes.c_int64
-    c = (ctypes.c_int64 * 3)()
+    c = (ctypes.c_int64 * 5)()
     envs = max(1024, 8192 // SAN_DIV)
     assert f(ctypes.c_int64(envs), ctypes.c_int64(200), c) == 0
-    kept, split, waves = list(c)
+    kept, split, waves, fallback, bypass = list(c)
     assert kept > envs // 8 and waves >= kept // 64
+    # both branches of the pass ran: owners left to coop_depth_w, and
+    # sub-move 1 taken from the pairs' checked list (ADVICE r05)
+    assert fallback > 0 and bypass > 0
     if envs == 8192:
         assert split > 0

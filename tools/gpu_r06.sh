@@ -37,5 +37,8 @@ dqn)  # the DQN learner's tests, then a graph-replayed trace of the driver (both
     && timeout -k 10 120 python3 tools/dqn_target.py 65536 30 > "$OUT/dqn_time.log" 2>&1 \
     && NARDE_ONE_LAUNCH=0 timeout -k 10 120 python3 tools/dqn_target.py 65536 30 >> "$OUT/dqn_time.log" 2>&1
   rc=$?; tail -3 "$OUT/pytest_dqn.log"; cat "$OUT/dqn_time.log"; exit $rc ;;
+ab)  # sustained FULL4 20 / 1,000-ply rollouts of tools/diag/build/libnarde_<tag>.so ($TAGS), 2 rounds
+  timeout -k 10 600 bash tools/diag/gpu_sus20.sh $TAGS > "$OUT/sus20.log" 2>&1
+  rc=$?; cat "$OUT/sus20.log"; exit $rc ;;
 *) echo "unknown phase $PHASE"; exit 2 ;;
 esac
