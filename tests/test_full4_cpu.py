@@ -414,8 +414,9 @@ def test_hostcheck_pair_pass_selfplay_turns(hostcheck):
     assert f(ctypes.c_int64(envs), ctypes.c_int64(200), c) == 0
     kept, split, waves, fallback, bypass = list(c)
     assert kept > envs // 8 and waves >= kept // 64
-    # both branches of the pass ran: owners left to coop_depth_w, and
-    # sub-move 1 taken from the pairs' checked list
-    assert fallback > 0 and bypass > 0
+    # both branches of the pass ran: sub-move 1 taken from the pairs'
+    # checked list, and (rare: 1 of 1,925 kept turns at 8,192 envs) an owner
+    # left to coop_depth_w
+    assert bypass > kept // 2
     if envs == 8192:
-        assert split > 0
+        assert split > 0 and fallback > 0
