@@ -4,7 +4,9 @@ tree's library with per-ply clocks in k_rollout_pp_full's producer waves
 (lane 0, wall_clock64 at 100 MHz, vector stores) and an export
 narde_diag_pp(int64 *host) that copies them out: [1024 producer waves][plies
 <= 160][12] = {ply start (after the draw wait), ply end (results in LDS),
-kind bits, searching lanes, 8 segment cycle counts (s_memtime): 0 block
+kind bits, searching lanes (NOT trusted: it reads 0.1-0.4 % of wave-plies
+where round 5's k_step clocks found 6.7 %), 8 segment
+cycle counts (s_memtime): 0 block
 test, 1 turn_c0_free, 2 the turn, 3 / 4 / 5 the bound turn's pair-bound C_0,
 doubles-bound C_0 and sub-moves, 6 the close}.  kind bit 0: the wave holds a block-bound
 doubles lane (ply_bound_turn_c0), bit 1: a block-bound two-dice lane, bit 2:
