@@ -405,6 +405,81 @@ int narde_rollout_timed(narde_env* e, int full, int plies, int32_t* obs, int32_t
   return NARDE_OK;
 }
 
+// narde_rollout_timed pre-bound (round 6): everything but the launch is done
+// once at create -- argument checks, the device check, the kernel chosen,
+// its arguments packed -- so the timed call is one ctypes argument and
+// three runtime calls (event, hipLaunchKernel, event), no device switch.
+struct narde_rollout_plan {
+  narde_env* e;
+  const void* kernel;
+  dim3 grid, block;
+  Planes pl;
+  int n;
+  Rng g;
+  int plies;
+  int max_steps;
+  Outs out;
+  void* args[6];
+  hipEvent_t ev0, ev1;
+  hipStream_t stream;
+};
+
+int narde_rollout_plan_create(narde_env* e, int full, int plies, int32_t* obs, int32_t* reward, uint8_t* terminated,
+                              uint8_t* truncated, uint64_t* legal, void* last, void* ev_start, void* ev_stop,
+                              int64_t* totals, void* stream, void** plan) {
+  if (!e || !plan || plies <= 0) return fail(NARDE_EINVAL, "bad argument (a plan needs plies > 0)");
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev != e->device)
+    return fail(NARDE_EINVAL, "the calling thread's current device must be the env's");
+  narde_rollout_plan* p = new (std::nothrow) narde_rollout_plan();
+  if (!p) return fail(NARDE_ENOMEM, "out of host memory");
+  const bool any = obs || reward || terminated || truncated || legal || last;
+  const bool nt = any && plies <= kPcNtMaxPlies;
+  if (full) {
+    p->out = Outs{obs, reward, terminated, truncated, legal, nullptr, (uint64_t*)last, totals};
+    p->kernel = any ? (nt ? (const void*)k_rollout_pp_full<true, true> : (const void*)k_rollout_pp_full<true, false>)
+                    : (const void*)k_rollout_pp_full<false, false>;
+  } else {
+    p->out = Outs{obs, reward, terminated, truncated, legal, (int16_t*)last, nullptr, totals};
+    p->kernel = any ? (nt ? (const void*)k_rollout_pc<true, true> : (const void*)k_rollout_pc<true, false>)
+                    : (const void*)k_rollout_pc<false, false>;
+  }
+  p->e = e;
+  p->grid = dim3((unsigned)((e->n + kPcEnvs - 1) / kPcEnvs));
+  p->block = dim3(kPcThreads);
+  p->pl = e->pl;
+  p->n = (int)e->n;
+  p->g = rng_of(e);  // seed, env ids, dice law (the ply counter is each env's record word)
+  p->plies = plies;
+  p->max_steps = e->max_steps;
+  p->args[0] = &p->pl;
+  p->args[1] = &p->n;
+  p->args[2] = &p->g;
+  p->args[3] = &p->plies;
+  p->args[4] = &p->max_steps;
+  p->args[5] = &p->out;
+  p->ev0 = (hipEvent_t)ev_start;
+  p->ev1 = (hipEvent_t)ev_stop;
+  p->stream = (hipStream_t)stream;
+  *plan = p;
+  return NARDE_OK;
+}
+
+int narde_rollout_plan_launch(void* plan) {
+  narde_rollout_plan* p = (narde_rollout_plan*)plan;
+  if (!p) return fail(NARDE_EINVAL, "NULL plan");
+  if (p->ev0 && hipEventRecord(p->ev0, p->stream) != hipSuccess) return fail(NARDE_EHIP, "hipEventRecord(ev_start) failed");
+  if (hipLaunchKernel(p->kernel, p->grid, p->block, p->args, 0, p->stream) != hipSuccess)
+    return fail(NARDE_EHIP, "hipLaunchKernel(k_rollout) failed");
+  if (p->ev1 && hipEventRecord(p->ev1, p->stream) != hipSuccess) return fail(NARDE_EHIP, "hipEventRecord(ev_stop) failed");
+  return NARDE_OK;
+}
+
+int narde_rollout_plan_destroy(void* plan) {
+  delete (narde_rollout_plan*)plan;
+  return NARDE_OK;
+}
+
 int narde_timing_event_create(int device, unsigned flags, void** event) {
   if (!event) return fail(NARDE_EINVAL, "NULL argument");
   DeviceGuard dg(device);

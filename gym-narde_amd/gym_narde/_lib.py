@@ -49,6 +49,9 @@ SIGNATURES = {
     "narde_rollout_full": (_i32, [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "narde_selfplay_full": (_i32, [_vp, _i32, _vp]),
     "narde_rollout_timed": (_i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "narde_rollout_plan_create": (_i32, [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "narde_rollout_plan_launch": (_i32, [_vp]),
+    "narde_rollout_plan_destroy": (_i32, [_vp]),
     "narde_timing_event_create": (_i32, [_i32, ctypes.c_uint, ctypes.POINTER(_vp)]),
     "narde_timing_event_destroy": (_i32, [_vp]),
     "narde_timing_event_elapsed_ms": (_i32, [_vp, _vp, ctypes.POINTER(ctypes.c_float)]),

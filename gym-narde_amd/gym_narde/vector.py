@@ -21,6 +21,8 @@ set with the max dice usable in bits 56-58, info["played"] the sub-moves
 played (bytes 2k/2k+1 = from/die, 0xFF unused).
 """
 import ctypes
+import os
+import weakref
 
 import numpy as np
 
@@ -397,6 +399,9 @@ class VecNardeEnv:
         exactly one ctypes call (one kernel launch on the stream current
         NOW), for hot loops where the per-call Python of rollout() would
         show (the buffers must stay alive and unmoved while it is used).
+        With events, the launch is pre-bound in the library
+        (narde_rollout_plan_*: one pointer per call; $NARDE_ROLLOUT_PLAN=0
+        takes narde_rollout_timed's per-call arguments instead).
         events = (start, stop) torch.cuda.Event or TimingEvent (either None): recorded on
         that stream right before / after the launch, inside the same call
         (narde_rollout_timed); a torch event must have been recorded once
@@ -434,11 +439,21 @@ class VecNardeEnv:
             fn, name = self.handle.lib.narde_rollout_timed, "narde_rollout_timed"
             args = (self.handle.h, int(self.full), int(plies)) + bufargs + (evs[0], evs[1], _lib.ptr(totals),
                                                                             self._s())
+            if int(plies) > 0 and os.environ.get("NARDE_ROLLOUT_PLAN", "1") == "1":
+                # round 6: the same launch pre-bound in the library
+                # (narde_rollout_plan_*): the timed call is one pointer
+                plan = ctypes.c_void_p()
+                _lib.check(self.handle.lib.narde_rollout_plan_create(*args, ctypes.byref(plan)),
+                           "narde_rollout_plan_create")
+                fn, name, args = self.handle.lib.narde_rollout_plan_launch, "narde_rollout_plan_launch", (plan,)
 
         def launch():
             rc = fn(*args)
             if rc:
                 _lib.check(rc, name)
+
+        if fn is self.handle.lib.narde_rollout_plan_launch:
+            weakref.finalize(launch, self.handle.lib.narde_rollout_plan_destroy, args[0])
 
         launch.bufs = bufs  # keeps the buffers referenced as long as the launcher
         launch.events = events

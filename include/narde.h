@@ -190,6 +190,19 @@ int narde_selfplay_full(narde_env *env, int plies, void *stream);
 int narde_rollout_timed(narde_env *env, int full, int plies, int32_t *obs, int32_t *reward,
                         uint8_t *terminated, uint8_t *truncated, uint64_t *legal, void *last,
                         void *ev_start, void *ev_stop, int64_t *totals, void *stream);
+/* narde_rollout_timed pre-bound (round 6): _create checks the arguments,
+ * chooses the kernel and packs its arguments once (plies > 0; the calling
+ * thread's current device must be the env's); _launch then records ev_start,
+ * launches and records ev_stop on `stream` -- the same launch as
+ * narde_rollout_timed with the same arguments, one pointer per call (the
+ * caller keeps the thread's current device and every buffer as at create);
+ * _destroy frees the plan (host memory only). */
+int narde_rollout_plan_create(narde_env *env, int full, int plies, int32_t *obs, int32_t *reward,
+                              uint8_t *terminated, uint8_t *truncated, uint64_t *legal,
+                              void *last, void *ev_start, void *ev_stop, int64_t *totals,
+                              void *stream, void **plan);
+int narde_rollout_plan_launch(void *plan);
+int narde_rollout_plan_destroy(void *plan);
 /* Timing events for narde_rollout_timed on `device`: a HIP event (returned
  * as void*) created with hipEventCreateWithFlags(flags); flags 0 = HIP's
  * default, 0x20000000 = hipEventDisableSystemFence (the event's record does

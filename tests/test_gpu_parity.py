@@ -469,3 +469,32 @@ def test_mask576_move2_device_dice_vs_oracle():
     for i in range(n):
         exp = _codes_of(ref["list2"][i], ref["count2"][i]) if ref["count2"][i] >= 0 else set()
         assert _bits(m2[i]) == exp, i
+
+
+@pytest.mark.parametrize("rules,plies", [("ref2", 20), ("ref2", 40), ("full4", 20)])
+def test_rollout_plan_equals_timed_call(rules, plies, monkeypatch):
+    """narde_rollout_plan_launch (the pre-bound timed launch, round 6) ==
+    narde_rollout_timed's per-call form: the same outputs, totals rows and
+    final state from the same start, ragged n, both rules, both store
+    policies."""
+    from gym_narde.vector import TimingEvent
+
+    n, seed = 3000 + 17, 77
+    got = []
+    for plan in ("1", "0"):
+        monkeypatch.setenv("NARDE_ROLLOUT_PLAN", plan)
+        env = vec(n, seed=seed, rules=rules)
+        env.selfplay(33)
+        bufs = env.rollout_buffers(plies)
+        rows = torch.empty(((n + 255) // 256, 3), dtype=torch.int64, device="cuda:0")
+        ev0, ev1 = TimingEvent("cuda:0"), TimingEvent("cuda:0")
+        launch = env.rollout_launcher(plies, bufs, events=(ev0, ev1), totals=rows)
+        launch()
+        launch()
+        got.append(({k: np_(v) for k, v in bufs.items()}, np_(rows), np_(env.get_state()["board"]), env.ply))
+        assert ev0.elapsed_ms(ev1) > 0
+        env.close()
+    (a, ra, ba, pa), (b, rb, bb, pb) = got
+    for k in a:
+        assert np.array_equal(a[k], b[k]), k
+    assert np.array_equal(ra, rb) and np.array_equal(ba, bb) and pa == pb == 33 + 2 * plies

@@ -40,5 +40,12 @@ dqn)  # the DQN learner's tests, then a graph-replayed trace of the driver (both
 ab)  # sustained FULL4 20 / 1,000-ply rollouts of tools/diag/build/libnarde_<tag>.so ($TAGS), 2 rounds
   timeout -k 10 600 bash tools/diag/gpu_sus20.sh $TAGS > "$OUT/sus20.log" 2>&1
   rc=$?; cat "$OUT/sus20.log"; exit $rc ;;
+plan)  # the driver's command with the pre-bound timed launch and without it, alternating
+  timeout -k 10 300 $T tests/test_gpu_parity.py -m gpu -k "plan or totals_rows" > "$OUT/pytest_plan.log" 2>&1 || exit 1
+  for k in 1 2 3 4; do
+    timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/plan1_$k.json" 2> "$OUT/plan1_$k.err" \
+      && NARDE_ROLLOUT_PLAN=0 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline \
+           > "$OUT/plan0_$k.json" 2> "$OUT/plan0_$k.err" || exit 1
+  done ;;
 *) echo "unknown phase $PHASE"; exit 2 ;;
 esac
