@@ -514,8 +514,8 @@ __device__ __forceinline__ int4 pc_obs_quad(const Lds& L, int slot, int k, int l
 // scalar resource (base, extent) per output and ply, built by SALU, and a
 // 32-bit per-lane byte offset -- the 64-bit address arithmetic of global
 // stores (two VALU per store and ply) leaves the VALU that the SIMD's rule
-// and consumer waves share.  aux 2 = the non-temporal policy
-// (buffer_store ... nt).  Dword 3 = 0x00020000, the
+// and consumer waves share.  The policy: kPcStorePolicy below.  Dword 3 =
+// 0x00020000, the
 // gfx9 raw-buffer word (/opt/rocm/include/ck/ck.hpp).
 typedef int pc_v4i __attribute__((ext_vector_type(4)));
 typedef unsigned pc_v2u __attribute__((ext_vector_type(2)));
@@ -534,19 +534,29 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t pc_rsrc_u(const void* base, ui
   void* ub = reinterpret_cast<void*>((uint64_t)lo | ((uint64_t)hi << 32));
   return __builtin_amdgcn_make_buffer_rsrc(ub, (short)0, __builtin_amdgcn_readfirstlane((int)bytes), 0x00020000);
 }
+// The stores' cache policy (gfx950 CPol bits: sc0 = 1, nt = 2, sc1 = 16):
+// sc1 | nt -- non-temporal at device scope, so the lines are written
+// through the XCD's L2 instead of left dirty in it for the end-of-kernel
+// write-back of a short launch.  One 20-ply launch after an idle GPU
+// (tools/diag/single_launch.py, medians of 30, two rounds, one box,
+// profiles/r06/store_policy/): REF2 event span 34.8 -> 33.3 us, host round
+// trip 49.6 -> 48.1 us, FULL4 74.8 -> 73.5 us; nt alone (round 5's policy)
+// 34.8, nt | sc0 34.9, sc1 36.4, plain 38.6, sc0 38.8, sc0 | sc1 36.3,
+// sc0 | sc1 | nt 33.4.
+constexpr int kPcStorePolicy = 16 | 2;
 __device__ __forceinline__ void pc_st16(__amdgpu_buffer_rsrc_t r, uint32_t off, int4 v) {
   const pc_v4i x = {v.x, v.y, v.z, v.w};
-  __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)off, 0, 2);
+  __builtin_amdgcn_raw_buffer_store_b128(x, r, (int)off, 0, kPcStorePolicy);
 }
 __device__ __forceinline__ void pc_st8(__amdgpu_buffer_rsrc_t r, uint32_t off, uint64_t v) {
   const pc_v2u x = {(unsigned)v, (unsigned)(v >> 32)};
-  __builtin_amdgcn_raw_buffer_store_b64(x, r, (int)off, 0, 2);
+  __builtin_amdgcn_raw_buffer_store_b64(x, r, (int)off, 0, kPcStorePolicy);
 }
 __device__ __forceinline__ void pc_st4(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t v) {
-  __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, 2);
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, (int)off, 0, kPcStorePolicy);
 }
 __device__ __forceinline__ void pc_st1(__amdgpu_buffer_rsrc_t r, uint32_t off, uint8_t v) {
-  __builtin_amdgcn_raw_buffer_store_b8(v, r, (int)off, 0, 2);
+  __builtin_amdgcn_raw_buffer_store_b8(v, r, (int)off, 0, kPcStorePolicy);
 }
 
 // consumer: outputs of ply p (block slot `slot`, index k) for the 64 envs of

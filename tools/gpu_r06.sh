@@ -47,5 +47,23 @@ plan)  # the driver's command with the pre-bound timed launch and without it, al
       && NARDE_ROLLOUT_PLAN=0 timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline \
            > "$OUT/plan0_$k.json" 2> "$OUT/plan0_$k.err" || exit 1
   done ;;
+single)  # one 20-ply launch after an idle synchronize (the driver's shape), per library in $TAGS, 2 rounds
+  for rep in 1 2; do for tag in $TAGS; do
+    echo -n "$tag ref2 "
+    NARDE_LIB=$PWD/tools/diag/build/libnarde_$tag.so NARDE_EVENTS=nofence timeout -k 5 120 python tools/diag/single_launch.py 20 2>/dev/null | tail -1 || exit 1
+    echo -n "$tag full4 "
+    NARDE_LIB=$PWD/tools/diag/build/libnarde_$tag.so NARDE_EVENTS=nofence timeout -k 5 120 python tools/diag/single_launch.py full4 20 2>/dev/null | tail -1 || exit 1
+  done; done > "$OUT/single.log" 2>&1
+  rc=$?; cat "$OUT/single.log"; exit $rc ;;
+api)  # the API kernels (tools/api_target.py, graph-replayed and eager) per library in $TAGS, 2 rounds, then the tests on the last
+  for rep in 1 2; do for tag in $TAGS; do
+    echo -n "$tag "
+    NARDE_LIB=$PWD/tools/diag/build/libnarde_$tag.so timeout -k 5 120 python tools/api_target.py 2>/dev/null | tail -1 || exit 1
+  done; done > "$OUT/api_ab.log" 2>&1 || { cat "$OUT/api_ab.log"; exit 1; }
+  for tag in $TAGS; do
+    NARDE_LIB=$PWD/tools/diag/build/libnarde_$tag.so timeout -k 10 400 $T tests/test_gpu_parity.py tests/test_gpu_full4.py tests/test_gpu_facade.py -m gpu > "$OUT/pytest_$tag.log" 2>&1
+    echo "$tag tests rc=$? $(tail -1 $OUT/pytest_$tag.log)" >> "$OUT/api_ab.log"
+  done
+  cat "$OUT/api_ab.log" ;;
 *) echo "unknown phase $PHASE"; exit 2 ;;
 esac
