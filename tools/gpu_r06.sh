@@ -65,5 +65,11 @@ api)  # the API kernels (tools/api_target.py, graph-replayed and eager) per libr
     echo "$tag tests rc=$? $(tail -1 $OUT/pytest_$tag.log)" >> "$OUT/api_ab.log"
   done
   cat "$OUT/api_ab.log" ;;
+sus)  # sustained REF2 and FULL4 rollouts at $PLIES plies per launch per library in $TAGS, 2 rounds
+  for rep in 1 2; do for tag in $TAGS; do for rules in ref2 full4; do
+    echo -n "$tag $rules "
+    NARDE_LIB=$PWD/tools/diag/build/libnarde_$tag.so timeout -k 5 120 python tools/diag/sustained_rollout.py ${PLIES:-100,1000} $rules 2>/dev/null | python3 -c "import sys,json; print(' '.join(str(json.loads(l)['plies_per_launch'])+':'+str(json.loads(l)['ms_per_100_plies']) for l in sys.stdin))" || exit 1
+  done; done; done > "$OUT/sus.log" 2>&1
+  rc=$?; cat "$OUT/sus.log"; exit $rc ;;
 *) echo "unknown phase $PHASE"; exit 2 ;;
 esac
