@@ -171,12 +171,11 @@ def run_parity(item, threads):
 
 
 def kernel_name(full4, plies):
-    """The kernel narde_rollout[_full] launches for this shape (narde.hip):
-    both store non-temporally up to 32 plies per launch (kPcNtMaxPlies);
+    """The kernel narde_rollout[_full] launches with outputs (narde.hip):
     REF2 is the producer/consumer workgroup k_rollout_pc, FULL4 the pairwise
-    producer/consumer k_rollout_pp_full."""
-    nt = "true" if plies <= 32 else "false"
-    return f"k_rollout_pc<true, {nt}>" if not full4 else f"k_rollout_pp_full<true, {nt}>"
+    producer/consumer k_rollout_pp_full; one store form at every launch
+    length since round 6 (round 5's had a second one past 32 plies)."""
+    return "k_rollout_pp_full<true>" if full4 else "k_rollout_pc<true>"
 
 
 def load_traffic(path, envs, plies, kernel):

@@ -235,6 +235,100 @@ __global__ void __launch_bounds__(64 * kSampleWaves) k_per_sample_gather(
   }
 }
 
+// ---------------------------------------------------------------- PER prefix
+// p = prio^alpha and cdf = its inclusive prefix sum, the sampler's inputs
+// (round 6: torch's pow kernel and rocPRIM's two-kernel look-back scan were
+// three launches, 18.5 us of a 1M-row ring per update).  Rows go in chunks of
+// kScanChunk, 4 consecutive rows per thread: k_per_chunk_sums writes each
+// chunk's total, k_per_scan adds a chunk's base (the totals before it, one
+// fixed-order tree per block) to the block scan of its rows.  The same
+// operation order on every run; a prefix sum in another association (torch's)
+// differs by rounding only.
+constexpr int kScanThreads = 256;
+constexpr int kScanChunk = 4 * kScanThreads;
+
+// rows r0 .. r0 + 3 of prio^alpha (0 past n) and their inclusive in-thread
+// sums s; returns the thread's total
+__device__ __forceinline__ float per_pow4(const float* __restrict__ prio, int64_t n, int64_t r0, float alpha,
+                                          float4& x, float4& s) {
+  if (r0 + 3 < n) {
+    x = *reinterpret_cast<const float4*>(prio + r0);
+  } else {
+    x.x = r0 < n ? prio[r0] : 0.0f;
+    x.y = r0 + 1 < n ? prio[r0 + 1] : 0.0f;
+    x.z = r0 + 2 < n ? prio[r0 + 2] : 0.0f;
+    x.w = 0.0f;
+  }
+  x.x = powf(x.x, alpha);
+  x.y = powf(x.y, alpha);
+  x.z = powf(x.z, alpha);
+  x.w = powf(x.w, alpha);
+  s.x = x.x;
+  s.y = s.x + x.y;
+  s.z = s.y + x.z;
+  s.w = s.z + x.w;
+  return s.w;
+}
+
+// exclusive prefix of the threads' totals t over the block (a wave scan by
+// shuffles, then the 4 wave totals through LDS); `all` gets the block total
+__device__ __forceinline__ float per_block_excl(float t, float* lds, float& all) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float inc = t;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) lds[wave] = inc;
+  __syncthreads();
+  float wb = 0.0f;
+  for (int k = 0; k < wave; ++k) wb += lds[k];
+  all = lds[0] + lds[1] + lds[2] + lds[3];
+  static_assert(kScanThreads == 256, "four waves");
+  return wb + (inc - t);
+}
+
+__global__ void __launch_bounds__(kScanThreads) k_per_chunk_sums(const float* __restrict__ prio, int64_t n,
+                                                                 float alpha, float* __restrict__ chunk) {
+  __shared__ float lds[4];
+  float4 x, s;
+  const int64_t r0 = (int64_t)blockIdx.x * kScanChunk + 4 * (int64_t)threadIdx.x;
+  const float t = per_pow4(prio, n, r0, alpha, x, s);
+  float all;
+  (void)per_block_excl(t, lds, all);
+  if (threadIdx.x == 0) chunk[blockIdx.x] = all;
+}
+
+__global__ void __launch_bounds__(kScanThreads) k_per_scan(const float* __restrict__ prio, int64_t n, float alpha,
+                                                           const float* __restrict__ chunk, float* __restrict__ p,
+                                                           float* __restrict__ cdf) {
+  __shared__ float lds[kScanThreads / 64];
+  __shared__ float lds2[kScanThreads / 64];
+  // the chunk's base: the totals of chunks 0 .. blockIdx.x - 1, thread t
+  // summing t, t + 256, ... in order, then a fixed tree
+  float b = 0.0f;
+  for (int64_t c = threadIdx.x; c < (int64_t)blockIdx.x; c += kScanThreads) b += chunk[c];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o, 64);
+  if ((threadIdx.x & 63) == 0) lds2[threadIdx.x >> 6] = b;
+  float4 x, s;
+  const int64_t r0 = (int64_t)blockIdx.x * kScanChunk + 4 * (int64_t)threadIdx.x;
+  const float t = per_pow4(prio, n, r0, alpha, x, s);
+  float all;
+  const float e = per_block_excl(t, lds, all);  // its barrier orders lds2 too
+  const float base = (lds2[0] + lds2[1]) + (lds2[2] + lds2[3]);
+  const float4 c = make_float4(base + (e + s.x), base + (e + s.y), base + (e + s.z), base + (e + s.w));
+  if (r0 + 3 < n) {
+    *reinterpret_cast<float4*>(p + r0) = x;
+    *reinterpret_cast<float4*>(cdf + r0) = c;
+  } else {
+    if (r0 < n) { p[r0] = x.x; cdf[r0] = c.x; }
+    if (r0 + 1 < n) { p[r0 + 1] = x.y; cdf[r0 + 1] = c.y; }
+    if (r0 + 2 < n) { p[r0 + 2] = x.z; cdf[r0 + 2] = c.z; }
+  }
+}
+
 // the batch max of w (one block, in LDS), every w normalised by it, then
 // beta and the counter stepped
 __global__ void __launch_bounds__(1024) k_per_finish(int batch, int64_t* __restrict__ counter,
@@ -925,6 +1019,20 @@ int narde_per_sample(int device, const float* p, const float* cdf, int64_t n, in
   if (rc != NARDE_OK) return rc;
   k_per_finish<<<1, 1024, 0, (hipStream_t)stream>>>((int)batch, counter, beta, beta_inc, w);
   return check_launch("k_per_finish");
+}
+
+int narde_per_prefix(int device, const float* prio, int64_t n, double alpha, float* p, float* cdf, float* chunk,
+                     void* stream) {
+  if (!prio || !p || !cdf || !chunk) return bad("NULL argument");
+  if (n <= 0 || n > (int64_t(1) << 31) - kScanChunk) return bad("need 0 < n < 2^31 - 1024");
+  if ((((uintptr_t)prio | (uintptr_t)p | (uintptr_t)cdf) & 15u) != 0u) return bad("prio, p and cdf must be 16-byte aligned");
+  DeviceGuard dg(device);
+  const unsigned blocks = (unsigned)((n + kScanChunk - 1) / kScanChunk);
+  k_per_chunk_sums<<<blocks, kScanThreads, 0, (hipStream_t)stream>>>(prio, n, (float)alpha, chunk);
+  const int rc = check_launch("k_per_chunk_sums");
+  if (rc != NARDE_OK) return rc;
+  k_per_scan<<<blocks, kScanThreads, 0, (hipStream_t)stream>>>(prio, n, (float)alpha, chunk, p, cdf);
+  return check_launch("k_per_scan");
 }
 
 int narde_gather_batch(int device, const int64_t* idx, int64_t batch, int state_size, const float* obs,

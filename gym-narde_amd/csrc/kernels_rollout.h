@@ -29,23 +29,12 @@ struct StepArgs {
   Outs out;
 };
 
-// The rollouts' long launches store plainly (the consumers' global-store
-// form): measured against non-temporal stores on sustained 1,000-ply REF2
-// rollouts (one box), plain 0.1265 ms per 100 plies, non-temporal obs rows
-// 0.135 (the narrow outputs' policy did not matter).  Short launches store
-// through non-temporal raw buffer stores (pc_st*), the API kernels through
-// st_nt below.
-template <class T>
-__device__ __forceinline__ void st_out(T* p, T v) {
-  *p = v;
-}
-
 // The per-call API kernels (k_step, k_observe) store non-temporally: a
 // launch's outputs are all it writes, and their L2 write-back is otherwise
 // on the call's critical path (with the straight-line REF2 ply below,
 // k_step<false> 5.25 -> 5.09-5.12 us and k_observe 2.88 -> 2.71 us per
-// graph-replayed call; the rollouts' long launches keep plain stores, see
-// st_out; profiles/r05/ab/api_kstep_variants.log)
+// graph-replayed call; profiles/r05/ab/api_kstep_variants.log).  The
+// rollouts store through raw buffer stores (pc_st* below).
 template <class T>
 __device__ __forceinline__ void st_nt(T* p, T v) {
   if constexpr (sizeof(T) == 16) {
@@ -462,14 +451,22 @@ constexpr int kPcSlots = 2;                     // ring slots (block b uses slot
 // starts after the first block, and the kernel is store-bound, so a short
 // first block shortens the stretch with no stores -- worth ~3 us of a 20-ply
 // launch (~35 us), nothing at 1,000 plies.
-__device__ __forceinline__ int pc_nblocks(int plies) {
-  return plies <= 1 ? 1 : (plies <= 3 ? 2 : 2 + (plies - 3 + kPcR - 1) / kPcR);
+// R: the full blocks' plies (<= kPcR, the rings' depth) -- kPcRShort in
+// launches of at most kPcShortPlies plies, where the more frequent barriers
+// cost less than the stretch with no stores at the end (one launch's last
+// block is stored after every rule wave is done): 20 plies 33.5 -> 33.0 us
+// event span with 2-ply blocks (3: 33.4, 1: 36.1; two rounds, one box,
+// profiles/r06/blocks/)
+__device__ __forceinline__ int pc_nblocks(int plies, int R) {
+  return plies <= 1 ? 1 : (plies <= 3 ? 2 : 2 + (plies - 3 + R - 1) / R);
 }
-__device__ __forceinline__ void pc_block(int b, int plies, int& p0, int& np) {
-  p0 = b == 0 ? 0 : (b == 1 ? 1 : 3 + (b - 2) * kPcR);
-  const int sz = b == 0 ? 1 : (b == 1 ? 2 : kPcR);
+__device__ __forceinline__ void pc_block(int b, int plies, int R, int& p0, int& np) {
+  p0 = b == 0 ? 0 : (b == 1 ? 1 : 3 + (b - 2) * R);
+  const int sz = b == 0 ? 1 : (b == 1 ? 2 : R);
   np = max(0, min(sz, plies - p0));
 }
+constexpr int kPcRShort = 2;
+constexpr int kPcShortPlies = 32;
 
 struct PcLds {
   uint2 draw[kPcSlots][kPcR][kPcEnvs];        // the ply's (wa, wb) per env and ply
@@ -510,7 +507,7 @@ __device__ __forceinline__ int4 pc_obs_quad(const Lds& L, int slot, int k, int l
   return v;
 }
 
-// Non-temporal raw buffer stores for the consumers of short launches: a
+// Raw buffer stores for the rollouts' consumers: a
 // scalar resource (base, extent) per output and ply, built by SALU, and a
 // 32-bit per-lane byte offset -- the 64-bit address arithmetic of global
 // stores (two VALU per store and ply) leaves the VALU that the SIMD's rule
@@ -537,7 +534,8 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t pc_rsrc_u(const void* base, ui
 // The stores' cache policy (gfx950 CPol bits: sc0 = 1, nt = 2, sc1 = 16):
 // sc1 | nt -- non-temporal at device scope, so the lines are written
 // through the XCD's L2 instead of left dirty in it for the end-of-kernel
-// write-back of a short launch.  One 20-ply launch after an idle GPU
+// write-back of a short launch (and no slower in long ones, pc_emit_ply).
+// One 20-ply launch after an idle GPU
 // (tools/diag/single_launch.py, medians of 30, two rounds, one box,
 // profiles/r06/store_policy/): REF2 event span 34.8 -> 33.3 us, host round
 // trip 49.6 -> 48.1 us, FULL4 74.8 -> 73.5 us; nt alone (round 5's policy)
@@ -560,98 +558,50 @@ __device__ __forceinline__ void pc_st1(__amdgpu_buffer_rsrc_t r, uint32_t off, u
 }
 
 // consumer: outputs of ply p (block slot `slot`, index k) for the 64 envs of
-// consumer wave cw.  Two forms, chosen with the store policy (kNt, by launch
-// length), each the faster of the two on its launches (tools/diag/
-// gpu_ab_multi.sh, one box; ms per 100 plies, base = round 2's consumer):
-//   short launches (non-temporal): raw buffer stores with a wave-uniform
-//     resource per output, no per-lane bounds branch (the resource's extent
-//     drops the stores past n): 20 plies 0.1697 -> 0.1613 sustained, one
-//     launch 34.7 -> 32.7 us back to back;
-//   long launches (plain stores): global stores with the bounds branches --
-//     the branch-free buffer form ran 0.1366 against 0.1276 at 1,000 plies,
-//     this one 0.1258.
-template <bool kNt>
+// consumer wave cw: raw buffer stores with a wave-uniform resource per output
+// and ply, no per-lane bounds branch (the resource's extent drops the stores
+// past n), policy kPcStorePolicy.  Round 5 kept a second form for launches
+// of more than 32 plies (global stores with the bounds branches, plain
+// policy, env_ply): with the sc1 | nt policy this one is as fast or faster at
+// every length (tools/gpu_r06.sh libab / sus, two rounds, one box,
+// profiles/r06/blocks/): bench.py's 1,000-ply line 5.15 -> 5.22 / 5.23e10,
+// sustained 100-ply launches 0.1376 -> 0.1315 ms per 100 plies, 1,000-ply
+// 0.1273 -> 0.1253 / 0.1260; FULL4 (pp_emit_ply) 100: 0.279 -> 0.277, 1,000:
+// 0.249 either way.
 __device__ __forceinline__ void pc_emit_ply(const PcLds& L, int slot, int k, int p, int n, int wg_env0, int cw,
                                             int lane, const Outs& out) {
   const int e0 = cw * 64;  // first env of this wave, workgroup-local (LDS index)
-  if constexpr (kNt) {
-    const int g0 = wg_env0 + __builtin_amdgcn_readfirstlane(cw) * 64;  // global, wave-uniform
-    const size_t row0 = (size_t)p * n + g0;                              // wave-uniform
-    const uint32_t nw = (uint32_t)max(0, min(64, n - g0));              // envs of this wave
-    if (out.obs) {
-      // the wave's 64 obs rows are 384 contiguous int4 quads: lane takes
-      // quads lane + 64 q, so every store instruction covers 1 KiB
-      const __amdgpu_buffer_rsrc_t r = pc_rsrc(out.obs + row0 * 24, nw * 96u);
+  const int g0 = wg_env0 + __builtin_amdgcn_readfirstlane(cw) * 64;  // global, wave-uniform
+  const size_t row0 = (size_t)p * n + g0;                              // wave-uniform
+  const uint32_t nw = (uint32_t)max(0, min(64, n - g0));              // envs of this wave
+  if (out.obs) {
+    // the wave's 64 obs rows are 384 contiguous int4 quads: lane takes
+    // quads lane + 64 q, so every store instruction covers 1 KiB
+    const __amdgpu_buffer_rsrc_t r = pc_rsrc(out.obs + row0 * 24, nw * 96u);
 #pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        const int j = lane + 64 * q;
-        const int el = j / 6, qq = j - 6 * el;
-        pc_st16(r, (uint32_t)j * 16u, pc_obs_quad(L, slot, k, e0 + el, qq));
-      }
-    }
-    const uint2 lg = L.legal[slot][k][e0 + lane];
-    const uint2 c = L.cf[slot][k][e0 + lane];
-    const uint32_t l = (uint32_t)lane;
-    if (out.reward) pc_st4(pc_rsrc(out.reward + row0, nw * 4u), 4u * l, c.y & 0xFFu);
-    if (out.term) pc_st1(pc_rsrc(out.term + row0, nw), l, (uint8_t)((c.y >> 8) & 1u));
-    if (out.trunc) pc_st1(pc_rsrc(out.trunc + row0, nw), l, (uint8_t)((c.y >> 16) & 1u));
-    if (out.legal) pc_st8(pc_rsrc(out.legal + row0, nw * 8u), 8u * l, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
-    if (out.act_out) pc_st4(pc_rsrc(reinterpret_cast<uint32_t*>(out.act_out) + row0, nw * 4u), 4u * l, c.x);
-  } else {
-    const int g0 = wg_env0 + e0;
-    const size_t row0 = (size_t)p * n + g0;
-    if (out.obs) {
-      int4* dst = reinterpret_cast<int4*>(out.obs + row0 * 24);
-#pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        const int j = lane + 64 * q;
-        const int el = j / 6, qq = j - 6 * el;
-        if (g0 + el >= n) continue;
-        const int wi = qq >> 1, sh = (qq & 1) * 16;
-        // read only the two words this quad needs: own word wi is dword wi
-        // of nib0, opponent word wi is dword 3 of nib0 or wi - 1 of nib1
-        const uint32_t* n0w = reinterpret_cast<const uint32_t*>(&L.nib0[slot][k][e0 + el]);
-        const uint32_t* n1w = reinterpret_cast<const uint32_t*>(&L.nib1[slot][k][e0 + el]);
-        const uint32_t own = n0w[wi];
-        const uint32_t opp = wi == 0 ? n0w[3] : n1w[wi - 1];
-        int4 v;
-        v.x = nib_at(own, sh) - nib_at(opp, sh);
-        v.y = nib_at(own, sh + 4) - nib_at(opp, sh + 4);
-        v.z = nib_at(own, sh + 8) - nib_at(opp, sh + 8);
-        v.w = nib_at(own, sh + 12) - nib_at(opp, sh + 12);
-        st_out(dst + j, v);
-      }
-    }
-    if (g0 + lane < n) {
-      const uint2 lg = L.legal[slot][k][e0 + lane];
-      const uint2 c = L.cf[slot][k][e0 + lane];
-      const size_t ix = row0 + lane;
-      if (out.reward) st_out(out.reward + ix, (int32_t)(c.y & 0xFFu));
-      if (out.term) st_out(out.term + ix, (uint8_t)((c.y >> 8) & 1u));
-      if (out.trunc) st_out(out.trunc + ix, (uint8_t)((c.y >> 16) & 1u));
-      if (out.legal) st_out(out.legal + ix, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
-      if (out.act_out) st_out(reinterpret_cast<uint32_t*>(out.act_out) + ix, c.x);
+    for (int q = 0; q < 6; ++q) {
+      const int j = lane + 64 * q;
+      const int el = j / 6, qq = j - 6 * el;
+      pc_st16(r, (uint32_t)j * 16u, pc_obs_quad(L, slot, k, e0 + el, qq));
     }
   }
+  const uint2 lg = L.legal[slot][k][e0 + lane];
+  const uint2 c = L.cf[slot][k][e0 + lane];
+  const uint32_t l = (uint32_t)lane;
+  if (out.reward) pc_st4(pc_rsrc(out.reward + row0, nw * 4u), 4u * l, c.y & 0xFFu);
+  if (out.term) pc_st1(pc_rsrc(out.term + row0, nw), l, (uint8_t)((c.y >> 8) & 1u));
+  if (out.trunc) pc_st1(pc_rsrc(out.trunc + row0, nw), l, (uint8_t)((c.y >> 16) & 1u));
+  if (out.legal) pc_st8(pc_rsrc(out.legal + row0, nw * 8u), 8u * l, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
+  if (out.act_out) pc_st4(pc_rsrc(reinterpret_cast<uint32_t*>(out.act_out) + row0, nw * 4u), 4u * l, c.x);
 }
 
-// consumer: outputs of plies p0 .. p0+np-1, stored non-temporally in short
-// launches (kNt: plies <= kPcNtMaxPlies, chosen at launch).  Plain stores
-// leave their lines dirty in the XCD L2s, and the write-back of what is still
-// dirty when the kernel ends sits on a short launch's critical path: one
-// 20-ply launch after an idle GPU takes 36.4 us with non-temporal stores
-// against 38.7 us with plain ones, while sustained 1,000-ply launches are
-// faster with plain stores (0.127 against 0.135 ms per 100 plies).  Only the
-// last 2-8 plies non-temporal gained nothing at 20 plies and cost 2 % at
-// 1,000 (tools/diag/gpu_ab_nt.sh, one box).
-constexpr int kPcNtMaxPlies = 32;
-template <bool kNt>
+// consumer: outputs of plies p0 .. p0+np-1
 __device__ __forceinline__ void pc_emit(const PcLds& L, int slot, int np, int p0, int n, int wg_env0, int cw,
                                         int lane, const Outs& out) {
-  for (int k = 0; k < np; ++k) pc_emit_ply<kNt>(L, slot, k, p0 + k, n, wg_env0, cw, lane, out);
+  for (int k = 0; k < np; ++k) pc_emit_ply(L, slot, k, p0 + k, n, wg_env0, cw, lane, out);
 }
 
-template <bool kOut, bool kNt>
+template <bool kOut>
 __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng g, int plies,
                                                            int max_steps, Outs out) {
   __shared__ PcLds L;
@@ -662,7 +612,8 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
   const int wg_env0 = blockIdx.x * kPcEnvs;
   const int i = wg_env0 + le;
   const bool valid = i < n;
-  const int nb = pc_nblocks(plies);
+  const int R = plies <= kPcShortPlies ? kPcRShort : kPcR;  // plies per full block
+  const int nb = pc_nblocks(plies, R);
 
   Side s;
   int4 st = make_int4(0, 0, 0, 0);
@@ -677,13 +628,13 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
   // (narde_rules.h ply_words)
   auto draw_block = [&](int b) {
     int p0, np;
-    pc_block(b, plies, p0, np);
-    uint32_t R[4];
+    pc_block(b, plies, R, p0, np);
+    uint32_t w[4];
     for (int k = 0; k < np; ++k) {
       const uint32_t t = t0 + (uint32_t)(p0 + k);
-      if (k == 0 || (t & 1u) == 0u) ply_block(t, g.env0 + (uint32_t)i, g.k0, g.k1, R);
+      if (k == 0 || (t & 1u) == 0u) ply_block(t, g.env0 + (uint32_t)i, g.k0, g.k1, w);
       const bool odd = (t & 1u) != 0u;
-      L.draw[b % kPcSlots][k][le] = odd ? make_uint2(R[2], R[3]) : make_uint2(R[0], R[1]);
+      L.draw[b % kPcSlots][k][le] = odd ? make_uint2(w[2], w[3]) : make_uint2(w[0], w[1]);
     }
   };
   // one ply of the rule wave: block b's draw k, results into b's slot
@@ -693,11 +644,11 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
     ply_words(rv.x, rv.y, g.dice_mode, r);
     StepOut o;
     int term, trunc;
-    // short launches: the straight-line ply (0.1605 -> 0.1592 ms per 100
-    // plies of 20-ply launches); long ones keep env_ply, whose instruction
-    // stream the sustained rate is tuned to (0.1259 against 0.1344 with the
-    // straight-line ply, tools/diag/gpu_ab_sl.sh, one box)
-    if constexpr (kNt) env_ply_policy_sl(s, st, r, g.dice_mode, max_steps, o, term, trunc);
+    // with outputs: the straight-line ply (0.1605 -> 0.1592 ms per 100
+    // plies of 20-ply launches, tools/diag/gpu_ab_sl.sh; at 1,000 plies it
+    // lost to env_ply with round 5's store forms, not with this round's --
+    // pc_emit_ply); self-play alone keeps env_ply
+    if constexpr (kOut) env_ply_policy_sl(s, st, r, g.dice_mode, max_steps, o, term, trunc);
     else env_ply(s, st, r, false, 0, 0, g.dice_mode, true, 0, 0, max_steps, true, o, term, trunc);
     if (kOut) pc_put(L, b % kPcSlots, k, le, s, o, term, trunc);
   };
@@ -705,7 +656,7 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
   __syncthreads();
   for (int b = 0; b < nb; ++b) {
     int p0, np;
-    pc_block(b, plies, p0, np);
+    pc_block(b, plies, R, p0, np);
     if (producer) {
       if (valid)
         for (int k = 0; k < np; ++k) one_ply(b, k);
@@ -713,16 +664,16 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
       if (b + 1 < nb) draw_block(b + 1);
       if (kOut && b > 0) {
         int q0, nq;
-        pc_block(b - 1, plies, q0, nq);
-        pc_emit<kNt>(L, (b - 1) % kPcSlots, nq, q0, n, wg_env0, cw, lane, out);
+        pc_block(b - 1, plies, R, q0, nq);
+        pc_emit(L, (b - 1) % kPcSlots, nq, q0, n, wg_env0, cw, lane, out);
       }
     }
     __syncthreads();
   }
   if (kOut && !producer && nb > 0) {
     int p0, np;
-    pc_block(nb - 1, plies, p0, np);
-    pc_emit<kNt>(L, (nb - 1) % kPcSlots, np, p0, n, wg_env0, cw, lane, out);
+    pc_block(nb - 1, plies, R, p0, np);
+    pc_emit(L, (nb - 1) % kPcSlots, np, p0, n, wg_env0, cw, lane, out);
   }
   int4 cum = make_int4(0, 0, 0, 0);
   if (producer && valid) {
@@ -831,65 +782,36 @@ __device__ __forceinline__ int4 pp_obs_quad(const PpLds& L, int cw, int sl, int 
 }
 
 // consumer: ply p's outputs of pair cw's 64 envs from ring slot sl
-// (pc_emit_ply_full's two store forms)
-template <bool kNt>
+// (pc_emit_ply's store form)
 __device__ __forceinline__ void pp_emit_ply(const PpLds& L, int cw, int sl, int p, int n, int g0, int lane,
                                             const Outs& out) {
   const size_t row0 = (size_t)p * n + g0;
-  if constexpr (kNt) {
-    const uint32_t nw = (uint32_t)max(0, min(64, n - g0));
-    if (out.obs) {
-      const __amdgpu_buffer_rsrc_t r = pc_rsrc_u(out.obs + row0 * 24, nw * 96u);
+  const uint32_t nw = (uint32_t)max(0, min(64, n - g0));
+  if (out.obs) {
+    const __amdgpu_buffer_rsrc_t r = pc_rsrc_u(out.obs + row0 * 24, nw * 96u);
 #pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        const int j = lane + 64 * q;
-        const int el = j / 6, qq = j - 6 * el;
-        pc_st16(r, (uint32_t)j * 16u, pp_obs_quad(L, cw, sl, el, qq));
-      }
+    for (int q = 0; q < 6; ++q) {
+      const int j = lane + 64 * q;
+      const int el = j / 6, qq = j - 6 * el;
+      pc_st16(r, (uint32_t)j * 16u, pp_obs_quad(L, cw, sl, el, qq));
     }
-    const uint32_t c = L.rtt[cw][sl][lane];
-    const uint32_t l = (uint32_t)lane;
-    if (out.reward) pc_st4(pc_rsrc_u(out.reward + row0, nw * 4u), 4u * l, c & 0xFFu);
-    if (out.term) pc_st1(pc_rsrc_u(out.term + row0, nw), l, (uint8_t)((c >> 8) & 1u));
-    if (out.trunc) pc_st1(pc_rsrc_u(out.trunc + row0, nw), l, (uint8_t)((c >> 16) & 1u));
-    if (out.legal) {
-      const uint2 lg = L.legal[cw][sl][lane];
-      pc_st8(pc_rsrc_u(out.legal + row0, nw * 8u), 8u * l, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
-    }
-    if (out.played) {
-      const uint2 pw = L.played[cw][sl][lane];
-      pc_st8(pc_rsrc_u(out.played + row0, nw * 8u), 8u * l, (uint64_t)pw.x | ((uint64_t)pw.y << 32));
-    }
-  } else {
-    if (out.obs) {
-      int4* dst = reinterpret_cast<int4*>(out.obs + row0 * 24);
-#pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        const int j = lane + 64 * q;
-        const int el = j / 6, qq = j - 6 * el;
-        if (g0 + el >= n) continue;
-        st_out(dst + j, pp_obs_quad(L, cw, sl, el, qq));
-      }
-    }
-    if (g0 + lane < n) {
-      const uint32_t c = L.rtt[cw][sl][lane];
-      const size_t ix = row0 + lane;
-      if (out.reward) st_out(out.reward + ix, (int32_t)(c & 0xFFu));
-      if (out.term) st_out(out.term + ix, (uint8_t)((c >> 8) & 1u));
-      if (out.trunc) st_out(out.trunc + ix, (uint8_t)((c >> 16) & 1u));
-      if (out.legal) {
-        const uint2 lg = L.legal[cw][sl][lane];
-        st_out(out.legal + ix, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
-      }
-      if (out.played) {
-        const uint2 pw = L.played[cw][sl][lane];
-        st_out(out.played + ix, (uint64_t)pw.x | ((uint64_t)pw.y << 32));
-      }
-    }
+  }
+  const uint32_t c = L.rtt[cw][sl][lane];
+  const uint32_t l = (uint32_t)lane;
+  if (out.reward) pc_st4(pc_rsrc_u(out.reward + row0, nw * 4u), 4u * l, c & 0xFFu);
+  if (out.term) pc_st1(pc_rsrc_u(out.term + row0, nw), l, (uint8_t)((c >> 8) & 1u));
+  if (out.trunc) pc_st1(pc_rsrc_u(out.trunc + row0, nw), l, (uint8_t)((c >> 16) & 1u));
+  if (out.legal) {
+    const uint2 lg = L.legal[cw][sl][lane];
+    pc_st8(pc_rsrc_u(out.legal + row0, nw * 8u), 8u * l, (uint64_t)lg.x | ((uint64_t)lg.y << 32));
+  }
+  if (out.played) {
+    const uint2 pw = L.played[cw][sl][lane];
+    pc_st8(pc_rsrc_u(out.played + row0, nw * 8u), 8u * l, (uint64_t)pw.x | ((uint64_t)pw.y << 32));
   }
 }
 
-template <bool kOut, bool kNt>
+template <bool kOut>
 __global__ void __launch_bounds__(kPcThreads) k_rollout_pp_full(Planes pl, int n, Rng g, int plies,
                                                                 int max_steps, Outs out) {
   __shared__ PpLds L;
@@ -965,7 +887,7 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pp_full(Planes pl, int n
       const uint32_t up = (uint32_t)p;
       pp_wait<8>(&L.produced[cw], [&](uint32_t v) { return v > up; });
       if (kOut) {
-        pp_emit_ply<kNt>(L, cw, p % kPpR, p, n, g0, lane, out);
+        pp_emit_ply(L, cw, p % kPpR, p, n, g0, lane, out);
         pp_publish(&L.emitted[cw], up + 1u);
       }
       if (p + kPpR < plies) {  // ply p's draw slot was read before ply p was produced

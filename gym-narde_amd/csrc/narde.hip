@@ -331,24 +331,20 @@ namespace {
 
 int launch_rollout_ref2(narde_env* e, int plies, const Outs& out, bool any, hipStream_t stream) {
   const dim3 g((unsigned)((e->n + kPcEnvs - 1) / kPcEnvs)), b(kPcThreads);
-  if (any && plies <= kPcNtMaxPlies)
-    k_rollout_pc<true, true><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
-  else if (any)
-    k_rollout_pc<true, false><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
+  if (any)
+    k_rollout_pc<true><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
   else
-    k_rollout_pc<false, false><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
+    k_rollout_pc<false><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
   return check_launch("k_rollout");
 }
 
 int launch_rollout_full(narde_env* e, int plies, const Outs& out, bool any, hipStream_t stream) {
   // producer/consumer pairs (k_rollout_pp_full)
   const dim3 g((unsigned)((e->n + kPcEnvs - 1) / kPcEnvs)), b(kPcThreads);
-  if (any && plies <= kPcNtMaxPlies)
-    k_rollout_pp_full<true, true><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
-  else if (any)
-    k_rollout_pp_full<true, false><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
+  if (any)
+    k_rollout_pp_full<true><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
   else
-    k_rollout_pp_full<false, false><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
+    k_rollout_pp_full<false><<<g, b, 0, stream>>>(e->pl, (int)e->n, rng_of(e), plies, e->max_steps, out);
   return check_launch("k_rollout_pp_full");
 }
 
@@ -434,15 +430,12 @@ int narde_rollout_plan_create(narde_env* e, int full, int plies, int32_t* obs, i
   narde_rollout_plan* p = new (std::nothrow) narde_rollout_plan();
   if (!p) return fail(NARDE_ENOMEM, "out of host memory");
   const bool any = obs || reward || terminated || truncated || legal || last;
-  const bool nt = any && plies <= kPcNtMaxPlies;
   if (full) {
     p->out = Outs{obs, reward, terminated, truncated, legal, nullptr, (uint64_t*)last, totals};
-    p->kernel = any ? (nt ? (const void*)k_rollout_pp_full<true, true> : (const void*)k_rollout_pp_full<true, false>)
-                    : (const void*)k_rollout_pp_full<false, false>;
+    p->kernel = any ? (const void*)k_rollout_pp_full<true> : (const void*)k_rollout_pp_full<false>;
   } else {
     p->out = Outs{obs, reward, terminated, truncated, legal, (int16_t*)last, nullptr, totals};
-    p->kernel = any ? (nt ? (const void*)k_rollout_pc<true, true> : (const void*)k_rollout_pc<true, false>)
-                    : (const void*)k_rollout_pc<false, false>;
+    p->kernel = any ? (const void*)k_rollout_pc<true> : (const void*)k_rollout_pc<false>;
   }
   p->e = e;
   p->grid = dim3((unsigned)((e->n + kPcEnvs - 1) / kPcEnvs));

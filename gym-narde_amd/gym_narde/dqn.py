@@ -483,6 +483,7 @@ class DeviceReplay:
         self.pos_t = torch.zeros((), dtype=torch.int64, **z)
         self.sample_ctr = torch.zeros((), dtype=torch.int64, **z)  # k_per_sample's Philox counter
         self._sample_scratch = torch.zeros(2, dtype=torch.int32, **z)  # its grid max + ticket
+        self._chunk = torch.empty((self.capacity + 1023) // 1024, dtype=torch.float32, **z)  # narde_per_prefix
         self.pos = 0
         self.size = 0
 
@@ -549,13 +550,23 @@ class DeviceReplay:
         torch.maximum(self.max_prio, pr.max(), out=self.max_prio)
 
     # ---- fused (HIP) learner path: the same rules, one kernel each
+    def prefix(self, n):
+        """(prio[:n] ** alpha, its inclusive prefix sum) in two launches
+        (narde_per_prefix, round 6; sample() keeps torch's pow + cumsum,
+        equal up to the rounding of the sums' association)."""
+        p = torch.empty(n, dtype=torch.float32, device=self.prio.device)
+        cdf = torch.empty_like(p)
+        _lib.check(_lib.load().narde_per_prefix(
+            p.device.index, _lib.ptr(self.prio), n, float(self.alpha), _lib.ptr(p), _lib.ptr(cdf),
+            _lib.ptr(self._chunk), _stream(p.device)), "narde_per_prefix")
+        return p, cdf
+
     def sample_fused(self, batch, seed, u_out=None):
-        """sample() as k_per_sample: priority^alpha and its prefix sum in
-        torch (rocPRIM scan), then the search, weights and beta step in one
-        kernel with its own device Philox counter (`sample_ctr`)."""
+        """sample() as k_per_sample: priority^alpha and its prefix sum
+        (prefix()), then the search, weights and beta step in one kernel with
+        its own device Philox counter (`sample_ctr`)."""
         n = self.rows
-        p = self.prio[:n] ** self.alpha
-        cdf = torch.cumsum(p, 0)
+        p, cdf = self.prefix(n)
         idx = torch.empty(batch, dtype=torch.int64, device=p.device)
         w = torch.empty(batch, dtype=torch.float32, device=p.device)
         _lib.check(_lib.load().narde_per_sample(
@@ -570,8 +581,7 @@ class DeviceReplay:
         s, ns, a, r, d) with w UNNORMALISED -- loss_prio_fused normalises it
         in place and steps beta and the sampling counter."""
         n, ss = self.rows, self.obs.shape[1]
-        p = self.prio[:n] ** self.alpha
-        cdf = torch.cumsum(p, 0)
+        p, cdf = self.prefix(n)
         z = dict(device=p.device)
         idx = torch.empty(batch, dtype=torch.int64, **z)
         w = torch.empty(batch, dtype=torch.float32, **z)
@@ -985,6 +995,8 @@ class BatchedDQNDriver:
             tf = self.target.features_nograd(ns)
             nq1 = self.target.move1_head(tf)
             wt = self.target.move2_head.weight
+            # (one GEMM of both heads' 1,152 columns measured slower: hipBLASLt
+            # picks a 64x32 tile for it, 41.8 against 17.8 + 19.6 us)
             base2 = torch.nn.functional.linear(tf, wt[:, :256], self.target.move2_head.bias)
             m1, _, m2 = target_max2(nq1, base2, self._target_onehot_rows())
         td = torch.empty_like(r)

@@ -290,11 +290,13 @@ def test_per_sample_kernel_vs_torch():
     total = cdf[-1]
     v = u * total
     want = torch.searchsorted(cdf, v, right=True).clamp_(max=n - 1)
-    # torch's cumsum (a rocPRIM look-back scan) does not fix its summation
-    # order, so the kernel's prefix sums and this one may differ by rounding:
-    # a pick may differ only where v lies within rounding of a prefix sum
+    # the sampler's prefix sums (narde_per_prefix, chunked) and torch's
+    # cumsum (a rocPRIM look-back scan) sum in other associations, so they
+    # differ by rounding -- over 300,000 rows by more than the spacing of a
+    # few rows' sums here and there: a pick may differ only where v lies
+    # within rounding of a prefix sum
     off = idx != want
-    assert float(off.double().mean()) < 1e-3
+    assert float(off.double().mean()) < 0.05
     lo = torch.minimum(idx, want)[off]
     assert bool(((cdf[lo] - v[off]).abs() <= 1e-4 * total).all())
     x = (n * (p[idx] / total)) ** (-beta0)
@@ -310,6 +312,30 @@ def test_per_sample_kernel_vs_torch():
         counts += torch.bincount(i, minlength=n).float()
     head = float(counts[:1000].sum() / counts.sum())
     assert head == pytest.approx(float(p[:1000].sum() / total), rel=0.05)
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 1023, 1024, 1025, 4099, 300001])
+def test_per_prefix_vs_torch_pow_cumsum(n):
+    """narde_per_prefix (round 6): p == prio ** alpha to powf's rounding,
+    cdf == the fp64 prefix sum of p to fp32 rounding, for ragged sizes and
+    zero-priority runs; deterministic (a second call equal bit for bit)."""
+    from gym_narde.dqn import DeviceReplay
+
+    rp = DeviceReplay(max(n, 2), 4, "cuda:0", stride=1)
+    g = torch.Generator(device="cuda:0").manual_seed(n)
+    rp.prio.copy_(torch.rand(rp.capacity, device="cuda:0", generator=g) * 3 + 0.01)
+    if n > 8:
+        rp.prio[torch.rand(rp.capacity, device="cuda:0", generator=g) < 0.2] = 0.0
+        rp.prio[n // 3:n // 3 + n // 5] = 0.0
+    p, cdf = rp.prefix(n)
+    torch.cuda.synchronize()
+    want_p = rp.prio[:n] ** rp.alpha
+    assert torch.allclose(p, want_p, rtol=3e-7, atol=0)
+    assert bool((p[rp.prio[:n] == 0] == 0).all())
+    ref = torch.cumsum(p.double(), 0)
+    assert torch.allclose(cdf.double(), ref, rtol=2e-6, atol=1e-6)
+    p2, cdf2 = rp.prefix(n)
+    assert torch.equal(p2, p) and torch.equal(cdf2, cdf)
 
 
 def test_gather_batch_and_rowmax_addend_exact():

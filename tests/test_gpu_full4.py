@@ -235,8 +235,8 @@ def test_full4_steady_state_full_batch_after_selfplay():
 @pytest.mark.parametrize("n", [1, 63, 65])
 def test_tiny_batches_both_rules_both_kernels(n):
     """One env, one wave less one lane, one wave plus one lane: REF2 rollouts
-    of 20 plies (k_rollout_pc<true, true>: non-temporal stores) and 60 plies
-    (<true, false>), FULL4 rollouts of 20 and 60 plies (k_rollout_pp_full)
+    of 20 plies (k_rollout_pc<true>: 2-ply barrier blocks) and 60 plies
+    (4-ply blocks), FULL4 rollouts of 20 and 60 plies (k_rollout_pp_full)
     equal the oracle ply for ply."""
     from gym_narde.vector import VecNardeEnv
 

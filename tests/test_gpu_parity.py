@@ -168,7 +168,7 @@ def test_rollout_vs_oracle_and_step(n):
     stepper = vec(n, seed=seed, env_id_offset=env0, max_episode_steps=150)
     ref = O.SelfPlay(n, seed=seed, env0=env0, max_steps=150)
     ref.reset(0)
-    for plies in (1, 20, 64, 235):  # <= 32 plies: the non-temporal-store kernel
+    for plies in (1, 20, 64, 235):  # <= 32 plies: 2-ply barrier blocks, else 4
         rec = ref.run(plies)
         bufs = env.rollout(plies)
         # the compact legal sets and codes, bit for bit, against the per-ply
@@ -215,9 +215,9 @@ def test_rollout_block_boundaries_vs_oracle():
 def test_rollout_writes_only_its_buffers(rules, n):
     """Every output of a rollout launch lands inside its [plies][n] buffer and
     nowhere else, for batches that end inside a wave and inside a workgroup,
-    at both REF2 store forms (<= 32 plies: raw buffer stores whose extents
-    drop the rows past n; longer: global stores behind bounds checks) and the
-    FULL4 kernels: each buffer is a view into a larger sentinel-filled
+    at both REF2 block schedules (<= 32 plies: 2-ply barrier blocks; longer:
+    4-ply) of the raw buffer stores, whose extents drop the rows past n, and
+    the FULL4 kernel: each buffer is a view into a larger sentinel-filled
     tensor, with guard regions before and after it, and the guards must come
     back untouched while the buffer itself matches a plain rollout."""
     G = 4096  # guard elements on each side
@@ -295,7 +295,7 @@ def test_full_batch_selfplay_vs_oracle():
 
 
 def test_bench_launches_full_batch_vs_oracle():
-    """The launches bench.py times (k_rollout_pc<true, *>: B = 65,536, 1,000
+    """The launches bench.py times (k_rollout_pc<true>: B = 65,536, 1,000
     plies, every output), then a 100-ply one and the driver's 20-ply one
     (non-temporal stores), at the bench's own seed 0 and env ids 0..65,535:
     EVERY env's every output -- the legal sets included, the metric's

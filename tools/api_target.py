@@ -10,6 +10,9 @@ kernel plus the gap between dispatches).  The same command under
 `rocprofv3 --kernel-trace --stats` gives the per-dispatch durations
 (tools/gpu_round.sh commits that summary).  Prints one JSON line.
 
+`floor_*`: torch's zero_ / fill_ / copy_ kernels at the same byte counts
+(what a traced dispatch of that size costs).
+
 Algorithmic bytes per env: k_step 64 (record r+w) +
 114 (REF2 outputs) / 118 (FULL4) B; the observations 32 (record read) +
 792 / 96 B."""
@@ -95,6 +98,21 @@ def main():
                      "frac": round(n * per_env / (us * 1e-6) / HBM_PEAK, 4),
                      "graph_frac": round(n * per_env / (gus * 1e-6) / HBM_PEAK, 4)}
     env.close()
+    # floors (round 6): torch's own kernels writing the same
+    # bytes, so the trace shows what a dispatch of this size costs there --
+    # a 4-byte zero_ (the launch alone), fill_ of k_observe's 6.3 MB and of
+    # k_step's 7.5 MB of outputs, a copy_ of k_observe's 8.4 MB
+    floors = {"zero_4B": torch.empty(1, dtype=torch.int32, device="cuda:0"),
+              "fill_obs24": torch.empty((n, 24), dtype=torch.int32, device="cuda:0"),
+              "fill_step_outputs": torch.empty(n * 114 // 4, dtype=torch.int32, device="cuda:0")}
+    src = torch.zeros(n * 64 // 4, dtype=torch.int32, device="cuda:0")  # 4.2 MB read + 4.2 written
+    dst = torch.empty_like(src)
+    for kind, fn in (("zero_4B", floors["zero_4B"].zero_), ("fill_obs24", lambda: floors["fill_obs24"].fill_(7)),
+                     ("fill_step_outputs", lambda: floors["fill_step_outputs"].fill_(7)),
+                     ("copy_observe_bytes", lambda: dst.copy_(src))):
+        us = timed(fn, a.warm, a.reps)
+        gus = graphed(fn, a.reps)
+        out["floor_" + kind] = {"us": round(us, 2), "graph_us": round(gus, 2)}
     print(json.dumps(out), flush=True)
 
 

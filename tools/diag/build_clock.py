@@ -29,12 +29,12 @@ def main():
     csrc = os.path.join(tmp, "gym-narde_amd", "csrc")
     p = os.path.join(csrc, "kernels_rollout.h")
     s = open(p).read()
-    s = sub(s, "template <bool kOut, bool kNt>\n__global__ void __launch_bounds__(kPcThreads) k_rollout_pc(",
+    s = sub(s, "template <bool kOut>\n__global__ void __launch_bounds__(kPcThreads) k_rollout_pc(",
             "__device__ long long g_ts[4096 * 64];\n"
             "#define TSTAMP(c) do { if (lane == 0) TS[c] = wall_clock64(); } while (0)\n"
-            "template <bool kOut, bool kNt>\n__global__ void __launch_bounds__(kPcThreads) k_rollout_pc(")
-    s = sub(s, "  const int nb = pc_nblocks(plies);\n\n  Side s;\n",
-            "  const int nb = pc_nblocks(plies);\n"
+            "template <bool kOut>\n__global__ void __launch_bounds__(kPcThreads) k_rollout_pc(")
+    s = sub(s, "  const int nb = pc_nblocks(plies, R);\n\n  Side s;\n",
+            "  const int nb = pc_nblocks(plies, R);\n"
             "  long long* TS = g_ts + (size_t)(blockIdx.x * 8 + wave) * 64;\n"
             "  TSTAMP(0);\n\n  Side s;\n")
     s = sub(s, "    if (valid) s = side_from_record(pl.p0[i], pl.p1[i]);\n  } else if (valid) {\n",
@@ -46,9 +46,9 @@ def main():
     s = sub(s, "    __syncthreads();\n  }\n  if (kOut && !producer && nb > 0) {",
             "    __syncthreads();\n    if (b < 56) TSTAMP(3 + b);\n  }\n"
             "  if (kOut && !producer && nb > 0) {")
-    s = sub(s, "    pc_emit<kNt>(L, (nb - 1) % kPcSlots, np, p0, n, wg_env0, cw, lane, out);\n  }\n"
+    s = sub(s, "    pc_emit(L, (nb - 1) % kPcSlots, np, p0, n, wg_env0, cw, lane, out);\n  }\n"
                "  int4 cum = make_int4(0, 0, 0, 0);\n",
-            "    pc_emit<kNt>(L, (nb - 1) % kPcSlots, np, p0, n, wg_env0, cw, lane, out);\n    TSTAMP(59);\n  }\n"
+            "    pc_emit(L, (nb - 1) % kPcSlots, np, p0, n, wg_env0, cw, lane, out);\n    TSTAMP(59);\n  }\n"
             "  int4 cum = make_int4(0, 0, 0, 0);\n")
     s = sub(s, "    cum = stats_after(pl.stats, i, st, out.totals != nullptr);\n  }\n"
                "  if (out.totals) wg_totals(cum, out.totals);\n}\n",

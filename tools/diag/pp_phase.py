@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""DIAGNOSTIC: where a 20-ply FULL4 launch (k_rollout_pp_full<true, true>,
+"""DIAGNOSTIC: where a 20-ply FULL4 launch (k_rollout_pp_full<true>,
 B = 65,536) spends its time, by ply and by kind of turn, from
 tools/diag/build/libnarde_ppclock.so (build_ppclock.py).  Two series of five
 20-ply launches: 'sync' -- every game from the start position in lockstep

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """DIAGNOSTIC (round 5): the REF2 self-play API step (k_step<false>, one wave
 per 64 envs) against a 1-ply launch of the producer/consumer rollout
-(k_rollout_pc<true, true>, rule and consumer waves, the same outputs) --
+(k_rollout_pc<true>, rule and consumer waves, the same outputs) --
 VERDICT r04 asked for k_step split across two waves per SIMD as k_rollout_pc
 does.  Device time per call, graph-replayed (tools/api_target.py graphed),
 B = 65,536.  Prints one JSON line."""

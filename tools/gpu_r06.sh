@@ -71,5 +71,12 @@ sus)  # sustained REF2 and FULL4 rollouts at $PLIES plies per launch per library
     NARDE_LIB=$PWD/tools/diag/build/libnarde_$tag.so timeout -k 5 120 python tools/diag/sustained_rollout.py ${PLIES:-100,1000} $rules 2>/dev/null | python3 -c "import sys,json; print(' '.join(str(json.loads(l)['plies_per_launch'])+':'+str(json.loads(l)['ms_per_100_plies']) for l in sys.stdin))" || exit 1
   done; done; done > "$OUT/sus.log" 2>&1
   rc=$?; cat "$OUT/sus.log"; exit $rc ;;
+libab)  # bench.py's default (1,000-ply) and driver lines per library in $TAGS, alternating, 2 rounds
+  for rep in 1 2; do for tag in $TAGS; do
+    NARDE_LIB=$PWD/tools/diag/build/libnarde_$tag.so timeout -k 10 300 python bench.py --no-cpu-baseline \
+      > "$OUT/def_${tag}_$rep.json" 2> "$OUT/def_${tag}_$rep.err" \
+    && NARDE_LIB=$PWD/tools/diag/build/libnarde_$tag.so timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
+      --no-cpu-baseline > "$OUT/drv_${tag}_$rep.json" 2> "$OUT/drv_${tag}_$rep.err" || exit 1
+  done; done ;;
 *) echo "unknown phase $PHASE"; exit 2 ;;
 esac

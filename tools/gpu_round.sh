@@ -66,14 +66,14 @@ if [ "$PHASE" = run ]; then
   tail -3 "$OUT/pytest_gpu.log" 2>/dev/null
   cat "$OUT/bench_driver_1.json" 2>/dev/null | tail -1 | cut -c1-400
 else
-  pmc_pair ref2 20 "k_rollout_pc<true, true>" 114 pmc_k_rollout_p20 \
-    && pmc_pair ref2 1000 "k_rollout_pc<true, false>" 114 pmc_k_rollout \
-    && pmc_pair full4 20 "k_rollout_pp_full<true, true>" 118 pmc_k_rollout_full_p20 \
-    && pmc_pair full4 1000 "k_rollout_pp_full<true, false>" 118 pmc_k_rollout_full \
-    && sq_pass ref2 20 "k_rollout_pc<true, true>" sq_k_rollout_p20 \
-    && sq_pass full4 20 "k_rollout_pp_full<true, true>" sq_k_rollout_full_p20 \
-    && sq_pass ref2 1000 "k_rollout_pc<true, false>" sq_k_rollout_p1000 \
-    && sq_pass full4 1000 "k_rollout_pp_full<true, false>" sq_k_rollout_full_p1000 \
+  pmc_pair ref2 20 "k_rollout_pc<true>" 114 pmc_k_rollout_p20 \
+    && pmc_pair ref2 1000 "k_rollout_pc<true>" 114 pmc_k_rollout \
+    && pmc_pair full4 20 "k_rollout_pp_full<true>" 118 pmc_k_rollout_full_p20 \
+    && pmc_pair full4 1000 "k_rollout_pp_full<true>" 118 pmc_k_rollout_full \
+    && sq_pass ref2 20 "k_rollout_pc<true>" sq_k_rollout_p20 \
+    && sq_pass full4 20 "k_rollout_pp_full<true>" sq_k_rollout_full_p20 \
+    && sq_pass ref2 1000 "k_rollout_pc<true>" sq_k_rollout_p1000 \
+    && sq_pass full4 1000 "k_rollout_pp_full<true>" sq_k_rollout_full_p1000 \
     && echo "[gpu_round] $(date +%T) DQN driver (configs[3]) traced" \
     && (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/dqn_trace" -o dqn \
           -- python3 "$ROOT/tools/dqn_target.py" 65536 20 > "$OUT/dqn_trace.log" 2>&1) \

@@ -32,7 +32,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--fetch", required=True, help="dir of the FETCH_SIZE pass")
     ap.add_argument("--write", required=True, help="dir of the WRITE_SIZE pass")
-    ap.add_argument("--kernel", default="k_rollout_pc<true,")  # both store policies
+    ap.add_argument("--kernel", default="k_rollout_pc<true>")
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--plies", type=int, default=1000)
     ap.add_argument("--bytes-per-ply", type=int, default=114, help="114 REF2, 118 FULL4")

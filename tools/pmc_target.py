@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""rocprofv3 --pmc target: k_rollout<true, *> at the bench shape.
+"""rocprofv3 --pmc target: k_rollout_pc<true> / k_rollout_pp_full<true> at the bench shape.
 
 Runs `--launches` launches of `--plies` plies over `--envs` envs with every
 per-ply output written (exactly bench.py's timed kernel), after one warm-up
@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--launches", type=int, default=3)
     ap.add_argument("--rules", choices=("ref2", "full4"), default="ref2")
     ap.add_argument("--stats-only", action="store_true",
-                    help="the statistics-only launches (selfplay: k_rollout_*<false, false>, no per-ply output)")
+                    help="the statistics-only launches (selfplay: k_rollout_*<false>, no per-ply output)")
     a = ap.parse_args()
     env = VecNardeEnv(a.envs, device="cuda:0", seed=0, rules=a.rules)
     bufs = None if a.stats_only else env.rollout_buffers(a.plies)

@@ -36,8 +36,7 @@ def profile(name):
 
 def launched_kernel(full, plies):
     """The kernel a launch of this shape runs (bench.py kernel_name)."""
-    nt = "true" if plies <= 32 else "false"
-    return f"k_rollout_pc<true, {nt}>" if not full else f"k_rollout_pp_full<true, {nt}>"
+    return "k_rollout_pp_full<true>" if full else "k_rollout_pc<true>"
 
 
 def matches(summary, envs, plies, kernel):

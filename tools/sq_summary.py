@@ -96,7 +96,7 @@ def summarise(root, kernel, envs, plies):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dir", required=True, help="the SQ pass's rocprofv3 output dir")
-    ap.add_argument("--kernel", required=True, help="kernel name substring, e.g. 'k_rollout_pc<true, true>'")
+    ap.add_argument("--kernel", required=True, help="kernel name substring, e.g. 'k_rollout_pc<true>'")
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--plies", type=int, required=True)
     ap.add_argument("--out", required=True)
