@@ -239,35 +239,50 @@ __global__ void __launch_bounds__(64 * kSampleWaves) k_per_sample_gather(
 // p = prio^alpha and cdf = its inclusive prefix sum, the sampler's inputs
 // (round 6: torch's pow kernel and rocPRIM's two-kernel look-back scan were
 // three launches, 18.5 us of a 1M-row ring per update).  Rows go in chunks of
-// kScanChunk, 4 consecutive rows per thread: k_per_chunk_sums writes each
-// chunk's total, k_per_scan adds a chunk's base (the totals before it, one
-// fixed-order tree per block) to the block scan of its rows.  The same
-// operation order on every run; a prefix sum in another association (torch's)
-// differs by rounding only.
+// kScanChunk (1,024), 4 consecutive rows per thread: k_per_chunk_sums
+// writes each chunk's total, k_per_scan adds a chunk's base (the totals of
+// the chunks before it, one fixed-order tree per block) to the block scan of
+// its rows -- 7.0 + 8.7 us per 1M-row ring.  The same operation order on
+// every run; a prefix sum in another association (torch's) differs by
+// rounding only.  (Measured and dropped: 4,096-row chunks, 9.2 + 12.4 us;
+// one launch whose blocks take tickets and read the earlier chunks' totals
+// from tagged 64-bit status words as they appear, 22.0 us at 1,024-row
+// chunks and 16.2 at 4,096 -- the wait for the other blocks' totals
+// outlasts a kernel boundary.)
 constexpr int kScanThreads = 256;
-constexpr int kScanChunk = 4 * kScanThreads;
+constexpr int kScanQuads = 1;                            // float4s per thread
+constexpr int kScanRows = 4 * kScanQuads;                // consecutive rows per thread
+constexpr int kScanChunk = kScanRows * kScanThreads;     // rows per chunk (block)
 
-// rows r0 .. r0 + 3 of prio^alpha (0 past n) and their inclusive in-thread
-// sums s; returns the thread's total
-__device__ __forceinline__ float per_pow4(const float* __restrict__ prio, int64_t n, int64_t r0, float alpha,
-                                          float4& x, float4& s) {
-  if (r0 + 3 < n) {
-    x = *reinterpret_cast<const float4*>(prio + r0);
-  } else {
-    x.x = r0 < n ? prio[r0] : 0.0f;
-    x.y = r0 + 1 < n ? prio[r0 + 1] : 0.0f;
-    x.z = r0 + 2 < n ? prio[r0 + 2] : 0.0f;
-    x.w = 0.0f;
+// a thread's rows r0 .. r0 + kScanRows - 1 of prio^alpha (0 past n) and
+// their inclusive in-thread sums s, in order; returns the thread's total
+__device__ __forceinline__ float per_pow(const float* __restrict__ prio, int64_t n, int64_t r0, float alpha,
+                                         float4 (&x)[kScanQuads], float4 (&s)[kScanQuads]) {
+  float run = 0.0f;
+#pragma unroll
+  for (int q = 0; q < kScanQuads; ++q) {
+    const int64_t r = r0 + 4 * q;
+    float4 v;
+    if (r + 3 < n) {
+      v = *reinterpret_cast<const float4*>(prio + r);
+    } else {
+      v.x = r < n ? prio[r] : 0.0f;
+      v.y = r + 1 < n ? prio[r + 1] : 0.0f;
+      v.z = r + 2 < n ? prio[r + 2] : 0.0f;
+      v.w = 0.0f;
+    }
+    v.x = powf(v.x, alpha);
+    v.y = powf(v.y, alpha);
+    v.z = powf(v.z, alpha);
+    v.w = powf(v.w, alpha);
+    x[q] = v;
+    s[q].x = run + v.x;
+    s[q].y = s[q].x + v.y;
+    s[q].z = s[q].y + v.z;
+    s[q].w = s[q].z + v.w;
+    run = s[q].w;
   }
-  x.x = powf(x.x, alpha);
-  x.y = powf(x.y, alpha);
-  x.z = powf(x.z, alpha);
-  x.w = powf(x.w, alpha);
-  s.x = x.x;
-  s.y = s.x + x.y;
-  s.z = s.y + x.z;
-  s.w = s.z + x.w;
-  return s.w;
+  return run;
 }
 
 // exclusive prefix of the threads' totals t over the block (a wave scan by
@@ -292,12 +307,41 @@ __device__ __forceinline__ float per_block_excl(float t, float* lds, float& all)
 __global__ void __launch_bounds__(kScanThreads) k_per_chunk_sums(const float* __restrict__ prio, int64_t n,
                                                                  float alpha, float* __restrict__ chunk) {
   __shared__ float lds[4];
-  float4 x, s;
-  const int64_t r0 = (int64_t)blockIdx.x * kScanChunk + 4 * (int64_t)threadIdx.x;
-  const float t = per_pow4(prio, n, r0, alpha, x, s);
+  float4 x[kScanQuads], s[kScanQuads];
+  const int64_t r0 = (int64_t)blockIdx.x * kScanChunk + kScanRows * (int64_t)threadIdx.x;
+  const float t = per_pow(prio, n, r0, alpha, x, s);
   float all;
   (void)per_block_excl(t, lds, all);
   if (threadIdx.x == 0) chunk[blockIdx.x] = all;
+}
+
+// the chunk's base from thread-strided partial sums b (fixed-order tree),
+// after per_block_excl's barrier
+__device__ __forceinline__ float per_base(float b, float* lds2) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o, 64);
+  if ((threadIdx.x & 63) == 0) lds2[threadIdx.x >> 6] = b;
+  __syncthreads();
+  return (lds2[0] + lds2[1]) + (lds2[2] + lds2[3]);
+}
+
+__device__ __forceinline__ void per_store(float* __restrict__ p, float* __restrict__ cdf, int64_t n, int64_t r0,
+                                          const float4 (&x)[kScanQuads], const float4 (&s)[kScanQuads], float base,
+                                          float e) {
+#pragma unroll
+  for (int q = 0; q < kScanQuads; ++q) {
+    const int64_t r = r0 + 4 * q;
+    const float4 c =
+        make_float4(base + (e + s[q].x), base + (e + s[q].y), base + (e + s[q].z), base + (e + s[q].w));
+    if (r + 3 < n) {
+      *reinterpret_cast<float4*>(p + r) = x[q];
+      *reinterpret_cast<float4*>(cdf + r) = c;
+    } else {
+      if (r < n) { p[r] = x[q].x; cdf[r] = c.x; }
+      if (r + 1 < n) { p[r + 1] = x[q].y; cdf[r + 1] = c.y; }
+      if (r + 2 < n) { p[r + 2] = x[q].z; cdf[r + 2] = c.z; }
+    }
+  }
 }
 
 __global__ void __launch_bounds__(kScanThreads) k_per_scan(const float* __restrict__ prio, int64_t n, float alpha,
@@ -305,28 +349,14 @@ __global__ void __launch_bounds__(kScanThreads) k_per_scan(const float* __restri
                                                            float* __restrict__ cdf) {
   __shared__ float lds[kScanThreads / 64];
   __shared__ float lds2[kScanThreads / 64];
-  // the chunk's base: the totals of chunks 0 .. blockIdx.x - 1, thread t
-  // summing t, t + 256, ... in order, then a fixed tree
   float b = 0.0f;
   for (int64_t c = threadIdx.x; c < (int64_t)blockIdx.x; c += kScanThreads) b += chunk[c];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) b += __shfl_xor(b, o, 64);
-  if ((threadIdx.x & 63) == 0) lds2[threadIdx.x >> 6] = b;
-  float4 x, s;
-  const int64_t r0 = (int64_t)blockIdx.x * kScanChunk + 4 * (int64_t)threadIdx.x;
-  const float t = per_pow4(prio, n, r0, alpha, x, s);
+  float4 x[kScanQuads], s[kScanQuads];
+  const int64_t r0 = (int64_t)blockIdx.x * kScanChunk + kScanRows * (int64_t)threadIdx.x;
+  const float t = per_pow(prio, n, r0, alpha, x, s);
   float all;
-  const float e = per_block_excl(t, lds, all);  // its barrier orders lds2 too
-  const float base = (lds2[0] + lds2[1]) + (lds2[2] + lds2[3]);
-  const float4 c = make_float4(base + (e + s.x), base + (e + s.y), base + (e + s.z), base + (e + s.w));
-  if (r0 + 3 < n) {
-    *reinterpret_cast<float4*>(p + r0) = x;
-    *reinterpret_cast<float4*>(cdf + r0) = c;
-  } else {
-    if (r0 < n) { p[r0] = x.x; cdf[r0] = c.x; }
-    if (r0 + 1 < n) { p[r0 + 1] = x.y; cdf[r0 + 1] = c.y; }
-    if (r0 + 2 < n) { p[r0 + 2] = x.z; cdf[r0 + 2] = c.z; }
-  }
+  const float e = per_block_excl(t, lds, all);
+  per_store(p, cdf, n, r0, x, s, per_base(b, lds2), e);
 }
 
 // the batch max of w (one block, in LDS), every w normalised by it, then
@@ -1004,6 +1034,10 @@ __global__ void __launch_bounds__(256) k_adam4(ParamTable t, const float* __rest
 
 }  // namespace
 
+// narde_adam_clip's form: float4 passes (default) or round 5's scalar ones
+// (narde_learner_variant, for A/B timing)
+static bool adam_vec4 = true;
+
 extern "C" {
 
 int narde_per_sample(int device, const float* p, const float* cdf, int64_t n, int64_t batch, uint64_t seed,
@@ -1022,12 +1056,14 @@ int narde_per_sample(int device, const float* p, const float* cdf, int64_t n, in
 }
 
 int narde_per_prefix(int device, const float* prio, int64_t n, double alpha, float* p, float* cdf, float* chunk,
-                     void* stream) {
+                     int64_t chunks, void* stream) {
   if (!prio || !p || !cdf || !chunk) return bad("NULL argument");
   if (n <= 0 || n > (int64_t(1) << 31) - kScanChunk) return bad("need 0 < n < 2^31 - 1024");
   if ((((uintptr_t)prio | (uintptr_t)p | (uintptr_t)cdf) & 15u) != 0u) return bad("prio, p and cdf must be 16-byte aligned");
+  const int64_t blocks64 = (n + kScanChunk - 1) / kScanChunk;
+  if (chunks < blocks64) return bad("chunk holds fewer totals than n needs");
   DeviceGuard dg(device);
-  const unsigned blocks = (unsigned)((n + kScanChunk - 1) / kScanChunk);
+  const unsigned blocks = (unsigned)blocks64;
   k_per_chunk_sums<<<blocks, kScanThreads, 0, (hipStream_t)stream>>>(prio, n, (float)alpha, chunk);
   const int rc = check_launch("k_per_chunk_sums");
   if (rc != NARDE_OK) return rc;
@@ -1094,9 +1130,6 @@ int narde_dqn_heads_backward(int device, const float* g1, const float* g2, const
   return check_launch("k_heads_grad_w");
 }
 
-// narde_adam_clip's form: float4 passes (default) or round 5's scalar ones
-// (narde_learner_variant, for A/B timing)
-static bool adam_vec4 = true;
 
 int narde_relu_bias_grad(int device, const float* gh, const float* h, int64_t n, int64_t cols, float* g,
                          float* db, float* scratch, void* stream) {

@@ -558,7 +558,7 @@ class DeviceReplay:
         cdf = torch.empty_like(p)
         _lib.check(_lib.load().narde_per_prefix(
             p.device.index, _lib.ptr(self.prio), n, float(self.alpha), _lib.ptr(p), _lib.ptr(cdf),
-            _lib.ptr(self._chunk), _stream(p.device)), "narde_per_prefix")
+            _lib.ptr(self._chunk), self._chunk.numel(), _stream(p.device)), "narde_per_prefix")
         return p, cdf
 
     def sample_fused(self, batch, seed, u_out=None):

@@ -386,12 +386,13 @@ int narde_per_sample(int device, const float *p, const float *cdf, int64_t n, in
 
 /* narde_per_sample's inputs from the priorities prio f32[n] (round 6): p =
  * prio^alpha (powf) and cdf = its inclusive prefix sum, in chunks of 1,024
- * rows (chunk f32[ceil(n / 1024)] scratch: each chunk's total, then each
- * chunk's rows scanned on top of the totals before it) -- the same order on
- * every run; replaces `prio ** alpha` + torch.cumsum (train_deepq_pytorch.py
- * :279-342's probabilities).  prio, p, cdf 16-byte aligned.  Two launches. */
+ * rows (chunk f32[chunks] scratch, chunks >= ceil(n / 1024): each chunk's
+ * total, then each chunk's rows scanned on top of the totals before it) --
+ * the same order on every run; replaces `prio ** alpha` + torch.cumsum
+ * (train_deepq_pytorch.py:279-342's probabilities).  prio, p, cdf 16-byte
+ * aligned.  Two launches. */
 int narde_per_prefix(int device, const float *prio, int64_t n, double alpha, float *p, float *cdf,
-                     float *chunk, void *stream);
+                     float *chunk, int64_t chunks, void *stream);
 
 /* Minibatch rows idx i64[batch] of the replay ring (narde_dqn_transition's
  * layout): s = obs[idx], ns = obs[(idx + next_stride) % capacity] (f32

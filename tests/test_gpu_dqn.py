@@ -314,7 +314,7 @@ def test_per_sample_kernel_vs_torch():
     assert head == pytest.approx(float(p[:1000].sum() / total), rel=0.05)
 
 
-@pytest.mark.parametrize("n", [1, 3, 4, 1023, 1024, 1025, 4099, 300001])
+@pytest.mark.parametrize("n", [1, 3, 4, 17, 1023, 1024, 1025, 4097, 300001])
 def test_per_prefix_vs_torch_pow_cumsum(n):
     """narde_per_prefix (round 6): p == prio ** alpha to powf's rounding,
     cdf == the fp64 prefix sum of p to fp32 rounding, for ragged sizes and
