@@ -4,7 +4,8 @@
 For P in argv (default 1 2 5 10 20 40) prints the median over 30 trials of
 the host round trip (launch + torch.cuda.synchronize) and of the kernel's
 own span (hipExtLaunchKernel events), plus the back-to-back time per launch.
-$NARDE_LIB selects the library; argv[1] may be 'full4'."""
+$NARDE_LIB selects the library; argv[1] may be 'full4'; $NARDE_TOTALS=1
+gives the timed launch the totals rows, as bench.py's timed launch."""
 import json
 import os
 import sys
@@ -47,7 +48,12 @@ def main():
         span_of = lambda: e0.elapsed_ms(e1)  # noqa: E731
     for P in plies:
         b = env.rollout_buffers(P)
-        L = env.rollout_launcher(P, b, events=(e0, e1))
+        tot = None
+        if os.environ.get("NARDE_TOTALS") == "1":
+            from gym_narde import _lib
+
+            tot = torch.zeros((_lib.wg_rows(env.num_envs), 3), dtype=torch.int64, device="cuda:0")
+        L = env.rollout_launcher(P, b, events=(e0, e1), totals=tot)
         Lb = env.rollout_launcher(P, b)
         trip, span, bare = [], [], []
         for _ in range(30):
