@@ -29,7 +29,8 @@ ACT_DIMS = 198 * 256 + 256 * 256  # the feature layers (the heads run in k_head_
 
 
 def is_gemm(name):
-    return name.startswith("Cijk_") or "gemm" in name.lower() or "Gemm" in name
+    """hipBLASLt's kernels, and k_mlp2 (the feature layers on MFMA, round 6)."""
+    return name.startswith("Cijk_") or "gemm" in name.lower() or "Gemm" in name or "k_mlp2" in name
 
 
 def main():
@@ -67,8 +68,9 @@ def main():
     mean = {k: round(sum(s[k] for s in steps) / len(steps), 2) for k in steps[0]}
     act_flops = 2.0 * a.envs * ACT_DIMS
     mean["act_gemm_gflop"] = round(act_flops / 1e9, 2)
-    mean["act_gemm_tflops"] = round(act_flops / (mean["act_gemm_us"] * 1e-6) / 1e12, 1)
-    mean["act_gemm_frac_of_fp32_mfma_peak"] = round(act_flops / (mean["act_gemm_us"] * 1e-6) / FP32_MFMA_PEAK, 3)
+    g = mean["act_gemm_us"] * 1e-6
+    mean["act_gemm_tflops"] = round(act_flops / g / 1e12, 1) if g > 0 else None
+    mean["act_gemm_frac_of_fp32_mfma_peak"] = round(act_flops / g / FP32_MFMA_PEAK, 3) if g > 0 else None
     mean["steps_averaged"] = len(steps)
     mean["source"] = os.path.relpath(path)
     text = json.dumps(mean, indent=1)
