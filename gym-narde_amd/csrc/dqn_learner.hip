@@ -359,137 +359,6 @@ __global__ void __launch_bounds__(kScanThreads) k_per_scan(const float* __restri
   per_store(p, cdf, n, r0, x, s, per_base(b, lds2), e);
 }
 
-// ------------------------------------------------------- feature layers
-// DecomposedDQN.features (train_deepq_pytorch.py:184-231): f = relu(relu(x
-// W1^T + b1) W2^T + b2), x (M, K1 <= 256), both layers 256 wide, fp32 on
-// the f32-input MFMA (v_mfma_f32_16x16x4_f32: exact f32, a k-ordered fma
-// chain per output) in ONE launch -- hipBLASLt runs it as two GEMM
-// launches with h = relu(x W1^T + b1) written and read back between them.
-// A workgroup holds 16 rows (4,096 rows = 256 workgroups, one per CU) on 8
-// waves, two per SIMD; the x tile, then h, in LDS.  Wave w owns columns
-// 32 w .. 32 w + 31 (two 16 x 16 accumulators) and reads its own B operands
-// -- rows of W, 8 contiguous k per lane and chunk of 32 k -- straight from
-// global memory (L2: every workgroup reads the same 456 KB), all of a
-// layer's loads issued before its first MFMA: no LDS staging, no barrier
-// inside a layer.  MFMA step kk of chunk c takes k = 32 c + 8 (lane >> 4) +
-// kk for A and B alike.  h is written out when the caller keeps it (the
-// backward's ReLU mask and dW2 input).
-constexpr int kMlpRows = 16;
-constexpr int kMlpN = 256;
-constexpr int kMlpThreads = 512;
-constexpr int kMlpXPad = kMlpN + 4;  // x / h rows, 16-byte aligned for the b128 A reads
-typedef float mlp_f4 __attribute__((ext_vector_type(4)));
-
-// wave w's B operands of one layer: rows 32 w + 16 t + (lane & 15) of W
-// (K floats a row), k = 32 c + 8 (lane >> 4) + 0..7 for chunk c < NC; the
-// last chunk partial iff kTail (its loads clamped in bounds, values past K
-// zero) -- both known at compile time, so no branch joins the loads
-template <int NC, bool kTail>
-__device__ __forceinline__ void mlp_load_b(const float* __restrict__ w, int K, float2 (&b)[NC][2][4]) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int r = lane & 15, kq = lane >> 4;
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const float* row = w + (size_t)(wave * 32 + 16 * t + r) * K;
-      const int k0 = 32 * c + 8 * kq;
-      if (!kTail || c + 1 < NC) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) b[c][t][j] = *reinterpret_cast<const float2*>(row + k0 + 2 * j);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int k = k0 + 2 * j;
-          const float x0 = row[min(k, K - 1)], x1 = row[min(k + 1, K - 1)];
-          b[c][t][j] = make_float2(k < K ? x0 : 0.0f, k + 1 < K ? x1 : 0.0f);
-        }
-      }
-    }
-  }
-}
-
-// acc[t] (rows 0..15, columns 32 wave + 16 t + 0..15) = sum over the NC
-// chunks' k of xh[row][k] w[col][k]; MFMA step kk of chunk c takes k =
-// 32 c + 8 (lane >> 4) + kk for A and B alike
-template <int NC>
-__device__ __forceinline__ void mlp_mfma(const float (*xh)[kMlpXPad], const float2 (&b)[NC][2][4], mlp_f4 (&acc)[2]) {
-  const int lane = threadIdx.x & 63;
-  const int r = lane & 15, kq = lane >> 4;
-  acc[0] = mlp_f4{0.0f, 0.0f, 0.0f, 0.0f};
-  acc[1] = acc[0];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    const mlp_f4 a0 = *reinterpret_cast<const mlp_f4*>(&xh[r][32 * c + 8 * kq]);
-    const mlp_f4 a1 = *reinterpret_cast<const mlp_f4*>(&xh[r][32 * c + 8 * kq + 4]);
-    const float av[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const float bv = (kk & 1) ? b[c][t][kk >> 1].y : b[c][t][kk >> 1].x;
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[kk], bv, acc[t], 0, 0, 0);
-      }
-    }
-  }
-}
-
-template <int NC1, bool kTail1>
-__global__ void __launch_bounds__(kMlpThreads) k_mlp2(const float* __restrict__ x, int64_t ldx, int M, int K1,
-                                                      const float* __restrict__ w1, const float* __restrict__ b1,
-                                                      const float* __restrict__ w2, const float* __restrict__ b2,
-                                                      float* __restrict__ h, float* __restrict__ f) {
-  __shared__ float xh[kMlpRows][kMlpXPad];  // the x tile (zero past K1 and past M), then h
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int m0 = blockIdx.x * kMlpRows;
-  float2 bw1[NC1][2][4];
-  mlp_load_b<NC1, kTail1>(w1, K1, bw1);
-  // the x tile: every load in bounds (row and column clamped), the value
-  // selected -- no branch between the loads
-  float xv[kMlpRows * kMlpN / kMlpThreads];
-#pragma unroll
-  for (int q = 0; q < kMlpRows * kMlpN / kMlpThreads; ++q) {
-    const int e = threadIdx.x + q * kMlpThreads, r = e / kMlpN, k = e % kMlpN;
-    xv[q] = x[(size_t)min(m0 + r, M - 1) * ldx + min(k, K1 - 1)];
-  }
-  __builtin_amdgcn_sched_barrier(0);  // every load of the prologue goes out first
-#pragma unroll
-  for (int q = 0; q < kMlpRows * kMlpN / kMlpThreads; ++q) {
-    const int e = threadIdx.x + q * kMlpThreads, r = e / kMlpN, k = e % kMlpN;
-    xh[r][k] = (m0 + r < M && k < K1) ? xv[q] : 0.0f;
-  }
-  __syncthreads();
-  mlp_f4 acc[2];
-  mlp_mfma<NC1>(xh, bw1, acc);
-  float2 bw2[kMlpN / 32][2][4];
-  mlp_load_b<kMlpN / 32, false>(w2, kMlpN, bw2);  // in flight while h is formed
-  __builtin_amdgcn_sched_barrier(0);
-  __syncthreads();  // every wave's reads of x are done: h replaces it
-  const int col0 = wave * 32 + (lane & 15), row0 = 4 * (lane >> 4);
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int col = col0 + 16 * t;
-    const float bb = b1[col];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float v = fmaxf(acc[t][i] + bb, 0.0f);
-      xh[row0 + i][col] = v;
-      if (h && m0 + row0 + i < M) h[(size_t)(m0 + row0 + i) * kMlpN + col] = v;
-    }
-  }
-  __syncthreads();
-  mlp_mfma<kMlpN / 32>(xh, bw2, acc);
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int col = col0 + 16 * t;
-    const float bb = b2[col];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (m0 + row0 + i < M) f[(size_t)(m0 + row0 + i) * kMlpN + col] = fmaxf(acc[t][i] + bb, 0.0f);
-  }
-}
-
-
 // the batch max of w (one block, in LDS), every w normalised by it, then
 // beta and the counter stepped
 __global__ void __launch_bounds__(1024) k_per_finish(int batch, int64_t* __restrict__ counter,
@@ -1261,36 +1130,6 @@ int narde_dqn_heads_backward(int device, const float* g1, const float* g2, const
   return check_launch("k_heads_grad_w");
 }
 
-
-int narde_dqn_features_forward(int device, const float* x, int64_t ldx, int64_t m, int k1, const float* w1,
-                               const float* b1, const float* w2, const float* b2, float* h, float* f, void* stream) {
-  if (!x || !w1 || !b1 || !w2 || !b2 || !f) return bad("NULL argument");
-  if (m <= 0 || m > (int64_t(1) << 30) || k1 <= 0 || k1 > kMlpN || ldx < k1) return bad("need 0 < m <= 2^30, 0 < k1 <= 256, ldx >= k1");
-  if ((((uintptr_t)w1 | (uintptr_t)w2) & 7u) != 0u || (k1 & 1) != 0) return bad("w1 / w2 8-byte aligned, k1 even");
-  DeviceGuard dg(device);
-  const dim3 g((unsigned)((m + kMlpRows - 1) / kMlpRows)), bl(kMlpThreads);
-  hipStream_t st = (hipStream_t)stream;
-  switch (2 * ((k1 + 31) / 32) + (k1 % 32 != 0 ? 1 : 0)) {
-    case 2: k_mlp2<1, false><<<g, bl, 0, st>>>(x, ldx, (int)m, k1, w1, b1, w2, b2, h, f); break;
-    case 3: k_mlp2<1, true><<<g, bl, 0, st>>>(x, ldx, (int)m, k1, w1, b1, w2, b2, h, f); break;
-    case 4: k_mlp2<2, false><<<g, bl, 0, st>>>(x, ldx, (int)m, k1, w1, b1, w2, b2, h, f); break;
-    case 5: k_mlp2<2, true><<<g, bl, 0, st>>>(x, ldx, (int)m, k1, w1, b1, w2, b2, h, f); break;
-    case 6: k_mlp2<3, false><<<g, bl, 0, st>>>(x, ldx, (int)m, k1, w1, b1, w2, b2, h, f); break;
-    case 7: k_mlp2<3, true><<<g, bl, 0, st>>>(x, ldx, (int)m, k1, w1, b1, w2, b2, h, f); break;
-    case 8: k_mlp2<4, false><<<g, bl, 0, st>>>(x, ldx, (int)m, k1, w1, b1, w2, b2, h, f); break;
-    case 9: k_mlp2<4, true><<<g, bl, 0, st>>>(x, ldx, (int)m, k1, w1, b1, w2, b2, h, f); break;
-    case 10: k_mlp2<5, false><<<g, bl, 0, st>>>(x, ldx, (int)m, k1, w1, b1, w2, b2, h, f); break;
-    case 11: k_mlp2<5, true><<<g, bl, 0, st>>>(x, ldx, (int)m, k1, w1, b1, w2, b2, h, f); break;
-    case 12: k_mlp2<6, false><<<g, bl, 0, st>>>(x, ldx, (int)m, k1, w1, b1, w2, b2, h, f); break;
-    case 13: k_mlp2<6, true><<<g, bl, 0, st>>>(x, ldx, (int)m, k1, w1, b1, w2, b2, h, f); break;
-    case 14: k_mlp2<7, false><<<g, bl, 0, st>>>(x, ldx, (int)m, k1, w1, b1, w2, b2, h, f); break;
-    case 15: k_mlp2<7, true><<<g, bl, 0, st>>>(x, ldx, (int)m, k1, w1, b1, w2, b2, h, f); break;
-    case 16: k_mlp2<8, false><<<g, bl, 0, st>>>(x, ldx, (int)m, k1, w1, b1, w2, b2, h, f); break;
-    case 17: k_mlp2<8, true><<<g, bl, 0, st>>>(x, ldx, (int)m, k1, w1, b1, w2, b2, h, f); break;
-    default: return bad("k1");
-  }
-  return check_launch("k_mlp2");
-}
 
 int narde_relu_bias_grad(int device, const float* gh, const float* h, int64_t n, int64_t cols, float* g,
                          float* db, float* scratch, void* stream) {

@@ -75,7 +75,6 @@ SIGNATURES = {
                                     _vp, _vp, _vp, _i64, _vp]),
     "narde_per_sample": (_i32, [_i32, _vp, _vp, _i64, _i64, _u64, _vp, _vp, ctypes.c_double, _vp, _vp, _vp,
                                 _vp, _vp]),
-    "narde_dqn_features_forward": (_i32, [_i32, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "narde_per_prefix": (_i32, [_i32, _vp, _i64, ctypes.c_double, _vp, _vp, _vp, _i64, _vp]),
     "narde_gather_batch": (_i32, [_i32, _vp, _i64, _i32, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                   _vp, _vp]),

@@ -373,77 +373,6 @@ def features_fused(model, x, scratch):
     return LinearReLU.apply(h, l2.weight, l2.bias, scratch)
 
 
-def _mlp_params(model):
-    l1, l2 = model.feature_network[0], model.feature_network[2]
-    for t in (l1.weight, l1.bias, l2.weight, l2.bias):
-        if t.dtype != torch.float32 or not t.is_contiguous():
-            raise ValueError("contiguous float32 feature parameters")
-    if l1.weight.shape[0] != 256 or tuple(l2.weight.shape) != (256, 256):
-        raise ValueError("feature layers (256, K1) and (256, 256)")
-    return l1.weight, l1.bias, l2.weight, l2.bias
-
-
-def _mlp_call(x, w1, b1, w2, b2, h, f):
-    if x.dtype != torch.float32 or x.dim() != 2 or x.stride(1) != 1 or x.shape[1] != w1.shape[1]:
-        raise ValueError("x must be (M, K1) float32 with unit column stride")
-    _lib.check(_lib.load().narde_dqn_features_forward(
-        x.device.index, _lib.ptr(x), x.stride(0), x.shape[0], x.shape[1], _lib.ptr(w1), _lib.ptr(b1), _lib.ptr(w2),
-        _lib.ptr(b2), None if h is None else _f32(h), _f32(f), _stream(x.device)), "narde_dqn_features_forward")
-
-
-def features_mlp(model, x):
-    """model.features(x) for inference in ONE launch (k_mlp2: both layers on
-    the f32-input MFMA, h kept in LDS); no autograd.  Equal to the module
-    path to fp32 rounding (another summation order)."""
-    w1, b1, w2, b2 = _mlp_params(model)
-    f = torch.empty((x.shape[0], 256), dtype=torch.float32, device=x.device)
-    _mlp_call(x, w1, b1, w2, b2, None, f)
-    return f
-
-
-class MlpFeatures(torch.autograd.Function):
-    """model.features(x) with k_mlp2's one-launch forward (h written out for
-    the backward) and LinearReLU's backward per layer (narde_relu_bias_grad
-    + the hipBLASLt weight / input GEMMs)."""
-
-    @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, scratch):
-        h = torch.empty((x.shape[0], 256), dtype=torch.float32, device=x.device)
-        f = torch.empty_like(h)
-        _mlp_call(x, w1, b1, w2, b2, h, f)
-        ctx.save_for_backward(x, w1, h, w2, f)
-        ctx.scratch = scratch
-        return f
-
-    @staticmethod
-    def backward(ctx, gf):
-        x, w1, h, w2, f = ctx.saved_tensors
-        n, sc = f.shape[0], ctx.scratch
-        if sc.numel() < -(-n // 64) * 256:
-            raise ValueError("relu_bias_grad scratch too small")
-
-        def rbg(gh, out):
-            g = torch.empty_like(out)
-            db = torch.empty(256, dtype=torch.float32, device=out.device)
-            _lib.check(_lib.load().narde_relu_bias_grad(
-                out.device.index, _f32(gh), _f32(out), n, 256, _lib.ptr(g), _lib.ptr(db), _f32(sc),
-                _stream(out.device)), "narde_relu_bias_grad")
-            return g, db
-
-        g2, db2 = rbg(gf.contiguous(), f)
-        dh = g2 @ w2
-        g1, db1 = rbg(dh, h)
-        dx = g1 @ w1 if ctx.needs_input_grad[0] else None
-        return dx, g1.t() @ x, db1, g2.t() @ h, db2, None
-
-
-def features_mlp_grad(model, x, scratch):
-    """model.features(x) through MlpFeatures (same parameters; forward equal
-    to fp32 rounding, gradients by LinearReLU's backward)."""
-    w1, b1, w2, b2 = _mlp_params(model)
-    return MlpFeatures.apply(x, w1, b1, w2, b2, scratch)
-
-
 class DQNLoss(torch.autograd.Function):
     """The decomposed loss of train_deepq_pytorch.py:653-720 as one kernel
     (k_dqn_loss): forward returns the loss and writes the TD errors into
@@ -729,7 +658,7 @@ class BatchedDQNDriver:
                  learning_rate=1e-4, gamma=0.99, epsilon=1.0, epsilon_min=0.01,
                  epsilon_decay=0.995, target_update=10, updates_per_step=1, shaping=True,
                  seed=0, fused=True, fused_heads=True, gathered_heads=True, fused_features=True,
-                 explore="plays", greedy="accepted", one_launch_chains=True, mlp_features=0):
+                 explore="plays", greedy="accepted", one_launch_chains=True):
         if env.full:
             raise ValueError("the DQN driver plays the reference's (move1, move2) actions: rules='ref2'")
         if explore not in ("plays", "codes"):
@@ -780,9 +709,6 @@ class BatchedDQNDriver:
         self.fused_features = bool(fused_features)
         # round 6: the learner's one-block / one-launch chains (_update_fused6)
         self.one_launch_chains = bool(one_launch_chains)
-        # round 6: the feature layers in one launch (k_mlp2) -- bit 0: the
-        # learner's online and target forwards, bit 1: act()'s
-        self.mlp_features = int(mlp_features)
         self._rb_scratch = relu_bias_grad_scratch(self.train_batch, 256, self.dev)
         self.seed = seed
         self.tag_t = torch.zeros((), dtype=torch.int64, **z)
@@ -847,7 +773,7 @@ class BatchedDQNDriver:
         Exploring rows (one shared draw per row and step): explore="plays"
         draws one of act()'s (move1, move2) combinations uniformly
         (k_explore_plays), as random.choice(valid_move_combinations)."""
-        f = features_mlp(self.model, x) if self.mlp_features & 2 else self.model.features_nograd(x)
+        f = self.model.features_nograd(x)
         if self.fused_heads:
             # both heads inside the policy kernel, legal codes only
             # (k_head_policy576): no dense (B,256)x(256,576) GEMM per head
@@ -1059,17 +985,14 @@ class BatchedDQNDriver:
     def _update_fused6(self):
         rp = self.replay
         idx, w, s, ns, a, r, d = rp.sample_gather_fused(self.train_batch, self.seed)
-        if self.mlp_features & 1:
-            f = features_mlp_grad(self.model, s, self._rb_scratch)
-        else:
-            f = features_fused(self.model, s, self._rb_scratch) if self.fused_features else self.model.features(s)
+        f = features_fused(self.model, s, self._rb_scratch) if self.fused_features else self.model.features(s)
         if self.gathered_heads:
             q1, q2 = gathered_heads(self.model, f, a)
         else:
             q1 = self.model.move1_head(f).gather(1, a[:, :1]).squeeze(1)
             q2 = self.model.move2_from_features(f, a[:, 0]).gather(1, a[:, 1:]).squeeze(1)
         with torch.no_grad():
-            tf = features_mlp(self.target, ns) if self.mlp_features & 1 else self.target.features_nograd(ns)
+            tf = self.target.features_nograd(ns)
             nq1 = self.target.move1_head(tf)
             wt = self.target.move2_head.weight
             # (one GEMM of both heads' 1,152 columns measured slower: hipBLASLt

@@ -384,16 +384,6 @@ int narde_per_sample(int device, const float *p, const float *cdf, int64_t n, in
                      uint64_t seed, int64_t *counter, double *beta, double beta_inc, int64_t *idx,
                      float *w, float *u, uint32_t *scratch, void *stream);
 
-/* DecomposedDQN.features (train_deepq_pytorch.py:184-231) in one launch
- * (round 6): f = relu(relu(x w1^T + b1) w2^T + b2) for x f32[m][ldx] (the
- * first k1 columns), w1 f32[256][k1], w2 f32[256][256], b1 / b2 f32[256];
- * f f32[m][256] and, if non-NULL, h = relu(x w1^T + b1) f32[m][256].  fp32
- * on the f32-input MFMA (exact fma chains in k order: equal to a GEMM in
- * another order to fp32 rounding).  k1 <= 256 even; w1, w2 8-byte aligned. */
-int narde_dqn_features_forward(int device, const float *x, int64_t ldx, int64_t m, int k1,
-                               const float *w1, const float *b1, const float *w2, const float *b2,
-                               float *h, float *f, void *stream);
-
 /* narde_per_sample's inputs from the priorities prio f32[n] (round 6): p =
  * prio^alpha (powf) and cdf = its inclusive prefix sum, in chunks of 1,024
  * rows (chunk f32[chunks] scratch, chunks >= ceil(n / 1024): each chunk's

@@ -72,7 +72,6 @@ def test_argument_errors_are_einval_before_any_device_call():
         ("narde_violates_block_rule", (0, N, 4, N, N)),
         ("narde_per_sample", (0, N, N, 100, 64, 0, N, N, 0.001, N, N, N, N, N)),
         ("narde_per_prefix", (0, N, 100, 0.6, N, N, N, 1, N)),
-        ("narde_dqn_features_forward", (0, N, 198, 64, 198, N, N, N, N, N, N, N)),
         ("narde_gather_batch", (0, N, 64, 198, N, 64, 128, N, N, N, N, N, N, N, N, N)),
         ("narde_rowmax_addend", (0, N, 576, N, 576, N, 64, N, N)),
         ("narde_get_totals", (N, N, N)),

@@ -966,77 +966,3 @@ def test_one_launch_learner_equals_round5_learner():
     assert int(drv[0].replay.sample_ctr) == int(drv[1].replay.sample_ctr)
     assert float(drv[0].replay.beta_t) == float(drv[1].replay.beta_t)
     assert float(drv[0].eps_t) == float(drv[1].eps_t) and int(drv[0].tag_t) == int(drv[1].tag_t)
-
-
-# ------------------------------------------- round 6: k_mlp2 (feature layers)
-@pytest.mark.parametrize("m,k1", [(1, 198), (15, 198), (17, 24), (4096, 198), (4099, 256), (70000, 198)])
-def test_mlp_features_vs_fp64(m, k1):
-    """narde_dqn_features_forward (k_mlp2, both layers on the f32-input
-    MFMA in one launch): f and h against an fp64 evaluation of the module's
-    math, to fp32 accumulation error (a k-ordered fma chain per output),
-    for ragged row counts and both observation widths; the ReLU zeros
-    exact."""
-    from gym_narde.dqn import DecomposedDQN, _mlp_call, _mlp_params
-
-    torch.manual_seed(m + k1)
-    model = DecomposedDQN(k1).cuda()
-    with torch.no_grad():  # non-trivial biases: both signs of every pre-activation
-        for l in (model.feature_network[0], model.feature_network[2]):
-            l.bias.uniform_(-0.3, 0.3)
-    x = torch.randn((m, k1), device="cuda:0")
-    w1, b1, w2, b2 = _mlp_params(model)
-    h = torch.empty((m, 256), device="cuda:0")
-    f = torch.empty_like(h)
-    _mlp_call(x, w1, b1, w2, b2, h, f)
-    torch.cuda.synchronize()
-    xd = x.double()
-    h_ref = torch.relu(xd @ w1.double().t() + b1.double())
-    scale1 = (xd.abs() @ w1.double().abs().t()) + b1.double().abs()
-    assert bool(((h.double() - h_ref).abs() <= 1e-6 * scale1 + 1e-7).all())
-    f_ref = torch.relu(h.double() @ w2.double().t() + b2.double())  # from the kernel's own h
-    scale2 = (h.double().abs() @ w2.double().abs().t()) + b2.double().abs()
-    assert bool(((f.double() - f_ref).abs() <= 1e-6 * scale2 + 1e-7).all())
-    assert bool(((h == 0) == (h_ref <= 0)).float().mean() > 0.999)
-    # the module path (hipBLASLt) to fp32 rounding
-    assert torch.allclose(f, model.features_nograd(x), rtol=1e-4, atol=1e-5)
-
-
-def test_mlp_features_grad_equals_linear_relu_path():
-    """MlpFeatures (k_mlp2 forward, LinearReLU's per-layer backward) against
-    features_fused (two LinearReLU layers): the same forward and parameter
-    gradients to fp32 rounding."""
-    from gym_narde.dqn import DecomposedDQN, features_fused, features_mlp_grad, relu_bias_grad_scratch
-
-    torch.manual_seed(5)
-    model = DecomposedDQN(198).cuda()
-    x = torch.randn((4096, 198), device="cuda:0")
-    gf = torch.randn((4096, 256), device="cuda:0")
-    sc = relu_bias_grad_scratch(4096, 256, "cuda:0")
-    out = []
-    for fn in (features_mlp_grad, features_fused):
-        model.zero_grad(set_to_none=True)
-        f = fn(model, x, sc)
-        f.backward(gf)
-        out.append((f.detach().clone(), [p.grad.clone() for p in model.feature_network.parameters()]))
-    (fa, ga), (fb, gb) = out
-    assert torch.allclose(fa, fb, rtol=1e-4, atol=1e-5)
-    for a, b in zip(ga, gb):
-        assert torch.allclose(a, b, rtol=1e-3, atol=1e-3 * float(b.abs().max()))
-
-
-def test_driver_with_mlp_features_runs_and_replays():
-    """BatchedDQNDriver(mlp_features=3): the feature forwards of act(), the
-    learner and the target in k_mlp2; graph-captured steps give finite
-    losses and legal actions."""
-    from gym_narde.dqn import BatchedDQNDriver
-    from gym_narde.vector import VecNardeEnv
-
-    env = VecNardeEnv(4096, device="cuda:0", seed=23)
-    drv = BatchedDQNDriver(env, capacity=1 << 14, train_batch=1024, seed=2, mlp_features=3)
-    for _ in range(5):
-        drv.step()
-    drv.capture_graph(warmup=2)
-    losses = [drv.step() for _ in range(4)]
-    torch.cuda.synchronize()
-    assert all(l is not None and bool(torch.isfinite(l)) for l in losses)
-    assert all(bool(torch.isfinite(p).all()) for p in drv.model.parameters())

@@ -29,8 +29,7 @@ ACT_DIMS = 198 * 256 + 256 * 256  # the feature layers (the heads run in k_head_
 
 
 def is_gemm(name):
-    """hipBLASLt's kernels, and k_mlp2 (the feature layers on MFMA, round 6)."""
-    return name.startswith("Cijk_") or "gemm" in name.lower() or "Gemm" in name or "k_mlp2" in name
+    return name.startswith("Cijk_") or "gemm" in name.lower() or "Gemm" in name
 
 
 def main():

@@ -2,9 +2,7 @@
 B envs, graph-captured step, N replays.  argv: [B] [steps] [eager];
 $NARDE_GATHERED=0 takes the dense online heads in the learner,
 $NARDE_FUSED_FEATURES=0 autograd's feature-layer backward, $NARDE_ONE_LAUNCH=0
-round 5's learner (no one-launch chains, scalar clip + Adam), $NARDE_MLP
-the driver's mlp_features bits (1: the learner's feature forwards in one
-launch, 2: act()'s)."""
+round 5's learner (no one-launch chains, scalar clip + Adam)."""
 import os
 import sys
 import time
@@ -24,8 +22,7 @@ env = VecNardeEnv(B, device="cuda:0", seed=1)
 drv = BatchedDQNDriver(env, train_batch=4096, capacity=max(1 << 20, 4 * B),
                        gathered_heads=os.environ.get("NARDE_GATHERED", "1") == "1",
                        fused_features=os.environ.get("NARDE_FUSED_FEATURES", "1") == "1",
-                       one_launch_chains=os.environ.get("NARDE_ONE_LAUNCH", "1") == "1",
-                       **({"mlp_features": int(os.environ["NARDE_MLP"])} if "NARDE_MLP" in os.environ else {}))
+                       one_launch_chains=os.environ.get("NARDE_ONE_LAUNCH", "1") == "1")
 if os.environ.get("NARDE_ONE_LAUNCH", "1") != "1":  # round 5's learner forms throughout
     from gym_narde.dqn import learner_variant
 

@@ -78,21 +78,5 @@ libab)  # bench.py's default (1,000-ply) and driver lines per library in $TAGS, 
     && NARDE_LIB=$PWD/tools/diag/build/libnarde_$tag.so timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
       --no-cpu-baseline > "$OUT/drv_${tag}_$rep.json" 2> "$OUT/drv_${tag}_$rep.err" || exit 1
   done; done ;;
-mlp)  # k_mlp2: its tests, the DQN tests, then the driver timed per mlp_features setting (alternating) and traced
-  timeout -k 10 300 $T tests/test_gpu_dqn.py -m gpu -k mlp > "$OUT/pytest_mlp.log" 2>&1 || { tail -40 "$OUT/pytest_mlp.log"; exit 1; }
-  tail -2 "$OUT/pytest_mlp.log"
-  timeout -k 10 400 $T tests/test_gpu_dqn.py -m gpu > "$OUT/pytest_dqn.log" 2>&1 || { tail -30 "$OUT/pytest_dqn.log"; exit 1; }
-  tail -1 "$OUT/pytest_dqn.log"
-  for rep in 1 2; do for v in 0 1 2 3; do
-    echo -n "mlp=$v " >> "$OUT/dqn_time.log"
-    NARDE_MLP=$v timeout -k 10 120 python3 tools/dqn_target.py 65536 30 2>/dev/null >> "$OUT/dqn_time.log" || exit 1
-  done; done
-  cat "$OUT/dqn_time.log"
-  for v in 0 3; do
-    (cd /tmp && NARDE_MLP=$v timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/dqn_trace_m$v" -o dqn \
-        -- python3 "$ROOT/tools/dqn_target.py" 65536 20 > "$ROOT/$OUT/dqn_trace_m$v.log" 2>&1) \
-      && python3 tools/dqn_breakdown.py "$OUT/dqn_trace_m$v" --out "$OUT/dqn_breakdown_m$v.json" > /dev/null || exit 1
-  done
-  grep -h '"act_us"\|"update_us"' "$OUT"/dqn_breakdown_m*.json ;;
 *) echo "unknown phase $PHASE"; exit 2 ;;
 esac
