@@ -469,6 +469,12 @@ constexpr int kPcRShort = 2;
 constexpr int kPcShortPlies = 32;
 
 struct PcLds {
+  // 64 unused bytes ahead of the rings: with the rings at the start of the
+  // workgroup's LDS a 20-ply launch ran ~1 us slower (back-to-back 31.2 ->
+  // 30.2 us, sustained 0.156 -> 0.151 ms per 100 plies at 20 plies, 0.126 ->
+  // 0.125 at 1,000; any lead of 16-512 bytes alike, one box, two rounds,
+  // profiles/r06/lds_lead/)
+  uint4 lead_[4];
   uint2 draw[kPcSlots][kPcR][kPcEnvs];        // the ply's (wa, wb) per env and ply
   // ply results (kOut only), structure-of-arrays (a wave's reads of one
   // field are contiguous; 1 % faster than three uint4 per env, and 8 KiB

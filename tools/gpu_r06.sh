@@ -51,6 +51,7 @@ single)  # one 20-ply launch after an idle synchronize (the driver's shape), per
   for rep in 1 2; do for tag in $TAGS; do
     echo -n "$tag ref2 "
     NARDE_LIB=$PWD/tools/diag/build/libnarde_$tag.so NARDE_EVENTS=nofence timeout -k 5 120 python tools/diag/single_launch.py 20 2>/dev/null | tail -1 || exit 1
+    [ "${REF2_ONLY:-0}" = 1 ] && continue
     echo -n "$tag full4 "
     NARDE_LIB=$PWD/tools/diag/build/libnarde_$tag.so NARDE_EVENTS=nofence timeout -k 5 120 python tools/diag/single_launch.py full4 20 2>/dev/null | tail -1 || exit 1
   done; done > "$OUT/single.log" 2>&1
