@@ -733,14 +733,17 @@ __global__ void __launch_bounds__(kPcThreads) k_rollout_pc(Planes pl, int n, Rng
 // fence after the counter load orders the other side's.
 constexpr int kPpR = 8;  // ring depth in plies
 
+// (the draw rings behind the result rings: sustained 0.352 -> 0.350 ms per
+// 100 plies at 20 plies, 0.252 -> 0.251 at 1,000, two rounds, one box,
+// profiles/r06/lds_lead/sus_full4_layouts.log)
 struct PpLds {
-  uint4 draw_w[kPcGroups][kPpR][64];   // the ply's pick words (turn_words)
-  uint32_t draw_d[kPcGroups][kPpR][64];  // ply_dice_word: dh | dl << 4 | reset side << 8
   uint4 nib0[kPcGroups][kPpR][64];
   uint2 nib1[kPcGroups][kPpR][64];
   uint2 legal[kPcGroups][kPpR][64];
   uint2 played[kPcGroups][kPpR][64];
   uint32_t rtt[kPcGroups][kPpR][64];
+  uint4 draw_w[kPcGroups][kPpR][64];   // the ply's pick words (turn_words)
+  uint32_t draw_d[kPcGroups][kPpR][64];  // ply_dice_word: dh | dl << 4 | reset side << 8
   uint32_t drawn[kPcGroups], produced[kPcGroups], emitted[kPcGroups];
 };
 // gfx950 has 160 KiB of LDS per CU: a k_rollout_pp_full workgroup holds
