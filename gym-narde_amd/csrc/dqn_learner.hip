@@ -828,20 +828,60 @@ __global__ void __launch_bounds__(kLearnThreads) k_dqn_loss_prio(
     int64_t* __restrict__ counter, double* __restrict__ beta, double beta_inc) {
 #pragma clang fp contract(off)
   __shared__ float red[kLearnThreads / 64];
+  __shared__ float red3[3][kLearnThreads / 64];
+  // the device scalars first: their loads overlap the batch's (thread 0)
+  float mp0 = 0.0f, e0 = 0.0f;
+  int64_t cur0 = 0, tag0 = 0, ctr0 = 0;
+  double beta0 = 0.0;
+  if (threadIdx.x == 0) {
+    mp0 = *max_prio;
+    if (epsilon) e0 = *epsilon;
+    if (cursor) cur0 = *cursor;
+    if (tag) tag0 = *tag;
+    beta0 = *beta;
+    ctr0 = *counter;
+  }
+  // the first kLossCache rows of each thread in registers, loaded with w
+  // (one memory round trip for both passes; larger batches read the rest
+  // in the second pass)
+  constexpr int kLossCache = 4;
+  float cw[kLossCache], cd[kLossCache], cr[kLossCache], cm1[kLossCache], cm2[kLossCache], cq1[kLossCache],
+      cq2[kLossCache];
+  int64_t ci[kLossCache];
   // k_per_finish: the batch max (from 0, as there), then every w normalised
   float wm = 0.0f;
-  for (int i = threadIdx.x; i < batch; i += kLearnThreads) wm = fmaxf(wm, w[i]);
+#pragma unroll
+  for (int c = 0; c < kLossCache; ++c) {
+    const int j = threadIdx.x + c * kLearnThreads;
+    if (j < batch) {
+      cw[c] = w[j];
+      cd[c] = d[j];
+      cr[c] = r[j];
+      cm1[c] = m1[j];
+      cm2[c] = m2[j];
+      cq1[c] = q1[j];
+      cq2[c] = q2[j];
+      ci[c] = idx[j];
+      wm = fmaxf(wm, cw[c]);
+    }
+  }
+  for (int j = threadIdx.x + kLossCache * kLearnThreads; j < batch; j += kLearnThreads) wm = fmaxf(wm, w[j]);
   const float wmax = block_max(wm, red);
   const float inv_b = 1.0f / (float)batch;
   float s1 = 0.0f, s2 = 0.0f, pm = -__builtin_inff();
-  for (int j = threadIdx.x; j < batch; j += kLearnThreads) {
-    const float wj = w[j] / wmax;
+  for (int j = threadIdx.x, c = 0; j < batch; j += kLearnThreads, ++c) {
+    const bool hit = c < kLossCache;
+    const float wr = hit ? cw[c] : w[j], dj = hit ? cd[c] : d[j], rj = hit ? cr[c] : r[j];
+    const float m1j = hit ? cm1[c] : m1[j], m2j = hit ? cm2[c] : m2[j];
+    const float q1j = hit ? cq1[c] : q1[j], q2j = hit ? cq2[c] : q2[j];
+    const int64_t ij = hit ? ci[c] : idx[j];
+    const float wj = wr / wmax;
     w[j] = wj;
-    const float nd = (1.0f - d[j]) * gamma;
-    const float t1 = r[j] + nd * m1[j];
-    const float t2 = r[j] + nd * m2[j];
-    const float e1 = q1[j] - t1, e2 = q2[j] - t2;
-    const float a = fabsf(t1 - q1[j]) + fabsf(t2 - q2[j]);
+    const float nd = (1.0f - dj) * gamma;
+    const float t1 = rj + nd * m1j;
+    const float t2 = rj + nd * m2j;
+    const float e1 = q1j - t1, e2 = q2j - t2;
+    const float a = fabsf(t1 - q1j) + fabsf(t2 - q2j);
     const float tdj = fminf(fmaxf(a, 0.0f), 100.0f);
     td[j] = tdj;
     s1 += wj * (e1 * e1);
@@ -850,26 +890,46 @@ __global__ void __launch_bounds__(kLearnThreads) k_dqn_loss_prio(
     g1[j] = gw * (2.0f * e1);
     g2[j] = gw * (2.0f * e2);
     const float pr = tdj + eps;
-    prio[idx[j]] = pr;
+    prio[ij] = pr;
     pm = fmaxf(pm, pr);
   }
-  s1 = block_sum(s1, red);
-  s2 = block_sum(s2, red);
-  pm = block_max(pm, red);
+  // block_sum(s1), block_sum(s2), block_max(pm) -- the same trees -- in one
+  // pass of barriers
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+    pm = fmaxf(pm, __shfl_xor(pm, o, 64));
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) {
+    red3[0][wave] = s1;
+    red3[1][wave] = s2;
+    red3[2][wave] = pm;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    s1 = lane < kLearnThreads / 64 ? red3[0][lane] : 0.0f;
+    s2 = lane < kLearnThreads / 64 ? red3[1][lane] : 0.0f;
+    pm = lane < kLearnThreads / 64 ? red3[2][lane] : -__builtin_inff();
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      s1 += __shfl_xor(s1, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+      pm = fmaxf(pm, __shfl_xor(pm, o, 64));
+    }
+  }
   if (threadIdx.x == 0) {
     const float l = s1 / (float)batch + s2 / (float)batch;
     *loss = l;
     if (loss_copy) *loss_copy = l;
-    *max_prio = fmaxf(*max_prio, pm);
-    if (epsilon) {
-      const float e = *epsilon;
-      *epsilon = e > eps_min ? e * eps_decay : e;
-    }
-    if (cursor) *cursor = (*cursor + cursor_add) % cursor_mod;
-    if (tag) *tag += 1;
-    const double b = *beta + beta_inc;
+    *max_prio = fmaxf(mp0, pm);
+    if (epsilon) *epsilon = e0 > eps_min ? e0 * eps_decay : e0;
+    if (cursor) *cursor = (cur0 + cursor_add) % cursor_mod;
+    if (tag) *tag = tag0 + 1;
+    const double b = beta0 + beta_inc;
     *beta = b < 1.0 ? b : 1.0;
-    *counter += 1;
+    *counter = ctr0 + 1;
   }
 }
 

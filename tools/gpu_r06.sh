@@ -79,5 +79,18 @@ libab)  # bench.py's default (1,000-ply) and driver lines per library in $TAGS, 
     && NARDE_LIB=$PWD/tools/diag/build/libnarde_$tag.so timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 \
       --no-cpu-baseline > "$OUT/drv_${tag}_$rep.json" 2> "$OUT/drv_${tag}_$rep.err" || exit 1
   done; done ;;
+libdqn)  # the DQN tests on the product, then the driver timed with libnarde_$BASE.so and the product, alternating, then traced
+  timeout -k 10 400 $T tests/test_gpu_dqn.py -m gpu > "$OUT/pytest_dqn.log" 2>&1 || { tail -30 "$OUT/pytest_dqn.log"; exit 1; }
+  tail -1 "$OUT/pytest_dqn.log"
+  for rep in 1 2 3; do
+    echo -n "$BASE " >> "$OUT/dqn_time.log"
+    NARDE_LIB=$PWD/tools/diag/build/libnarde_$BASE.so timeout -k 10 120 python3 tools/dqn_target.py 65536 30 2>/dev/null >> "$OUT/dqn_time.log" || exit 1
+    echo -n "product " >> "$OUT/dqn_time.log"
+    timeout -k 10 120 python3 tools/dqn_target.py 65536 30 2>/dev/null >> "$OUT/dqn_time.log" || exit 1
+  done
+  cat "$OUT/dqn_time.log"
+  (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/dqn_trace" -o dqn \
+      -- python3 "$ROOT/tools/dqn_target.py" 65536 20 > "$ROOT/$OUT/dqn_trace.log" 2>&1) \
+    && python3 tools/dqn_breakdown.py "$OUT/dqn_trace" --out "$OUT/dqn_breakdown.json" > /dev/null ;;
 *) echo "unknown phase $PHASE"; exit 2 ;;
 esac
