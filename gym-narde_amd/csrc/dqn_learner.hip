@@ -242,7 +242,7 @@ __global__ void __launch_bounds__(64 * kSampleWaves) k_per_sample_gather(
 // kScanChunk (1,024), 4 consecutive rows per thread: k_per_chunk_sums
 // writes each chunk's total, k_per_scan adds a chunk's base (the totals of
 // the chunks before it, one fixed-order tree per block) to the block scan of
-// its rows -- 7.0 + 8.7 us per 1M-row ring.  The same operation order on
+// its rows -- 6.7 + 7.8 us per 1M-row ring.  The same operation order on
 // every run; a prefix sum in another association (torch's) differs by
 // rounding only.  (Measured and dropped: 4,096-row chunks, 9.2 + 12.4 us;
 // one launch whose blocks take tickets and read the earlier chunks' totals
@@ -349,8 +349,19 @@ __global__ void __launch_bounds__(kScanThreads) k_per_scan(const float* __restri
                                                            float* __restrict__ cdf) {
   __shared__ float lds[kScanThreads / 64];
   __shared__ float lds2[kScanThreads / 64];
+  // thread t's totals t, t + 256, ... in order, four loads at a time (the
+  // missing ones 0: adding +0 to a sum of non-negative terms changes nothing)
   float b = 0.0f;
-  for (int64_t c = threadIdx.x; c < (int64_t)blockIdx.x; c += kScanThreads) b += chunk[c];
+  for (int64_t c0 = threadIdx.x; c0 < (int64_t)blockIdx.x; c0 += 4 * kScanThreads) {
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t c = c0 + q * kScanThreads;
+      v[q] = c < (int64_t)blockIdx.x ? chunk[c] : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) b += v[q];
+  }
   float4 x[kScanQuads], s[kScanQuads];
   const int64_t r0 = (int64_t)blockIdx.x * kScanChunk + kScanRows * (int64_t)threadIdx.x;
   const float t = per_pow(prio, n, r0, alpha, x, s);
