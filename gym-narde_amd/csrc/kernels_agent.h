@@ -102,13 +102,13 @@ __device__ __forceinline__ void tes_point4(uint32_t v, float* f) {
   f[3] = v >= 3u ? (float)(v - 3u) / 2.0f : 0.0f;
 }
 
-__global__ void __launch_bounds__(kBlock) k_tesauro198_rows(Planes pl, int n, float* __restrict__ tes) {
-  __shared__ __attribute__((aligned(16))) float rows[kBlock / 64][kTesEnvs * 198];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int e0 = (blockIdx.x * (kBlock / 64) + wave) * kTesEnvs;  // first env of the wave
+// the wave's 16 rows (envs e0 .. e0 + 15, those below n) into wave_rows
+// (LDS, 16 x 198 floats); the caller hands them over with wave_lds_handoff
+__device__ __forceinline__ void tes_stage_rows(const Planes& pl, int n, int e0, float* wave_rows) {
+  const int lane = threadIdx.x & 63;
   const int le = lane & 15, q = lane >> 4;
   const int i = e0 + le;
-  float* row = rows[wave] + le * 198;
+  float* row = wave_rows + le * 198;
   if (i < n) {
     const uint4 a = pl.p0[i], b = pl.p1[i];
     const int side = q >> 1, upper = q & 1;
@@ -135,6 +135,13 @@ __global__ void __launch_bounds__(kBlock) k_tesauro198_rows(Planes pl, int n, fl
     for (int k = 0; k < 26; ++k)
       if (2 * k < nf) *reinterpret_cast<float2*>(row + c0 + 2 * k) = make_float2(f[2 * k], f[2 * k + 1]);
   }
+}
+
+__global__ void __launch_bounds__(kBlock) k_tesauro198_rows(Planes pl, int n, float* __restrict__ tes) {
+  __shared__ __attribute__((aligned(16))) float rows[kBlock / 64][kTesEnvs * 198];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int e0 = (blockIdx.x * (kBlock / 64) + wave) * kTesEnvs;  // first env of the wave
+  tes_stage_rows(pl, n, e0, rows[wave]);
   wave_lds_handoff();  // the wave reads only its own rows
   // the wave's rows: [e0, min(e0 + 16, n)) -> 16-B pieces, lane-major
   const int rows_here = max(0, min(kTesEnvs, n - e0));
@@ -219,40 +226,47 @@ __global__ void __launch_bounds__(kBlock) k_dqn_transition(TransArgs t, int obs_
     trans_scalars(t, i, slot, nslot, t.pl.p1[i]);
     return;
   }
-  const uint32_t total = (uint32_t)t.n * 198u;  // n * 198 < 2^31 (checked on the host)
-  const uint32_t e0 = 4u * (blockIdx.x * kBlock + threadIdx.x);
-  if (e0 >= total) return;
-  const bool vec = (q0 * 198) % 4 == 0 && q0 + t.n <= t.capacity && e0 + 4u <= total;
-  const int i0 = (int)(e0 / 198u);
-  const int c0 = (int)(e0 - (uint32_t)i0 * 198u);
-  const uint4 a0 = t.pl.p0[i0], b0 = t.pl.p1[i0];
-  // the 4 floats span rows i0 and (if c0 > 194) i0 + 1
-  const bool split = c0 > 194 && i0 + 1 < t.n;
-  uint4 a1 = a0, b1 = b0;
-  if (split) { a1 = t.pl.p0[i0 + 1]; b1 = t.pl.p1[i0 + 1]; }
-  float nv[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int c = c0 + q;
-    const bool nx = c >= 198;  // the record first, then one evaluation (not both)
-    nv[q] = tes_value(nx ? a1 : a0, nx ? b1 : b0, nx ? c - 198 : c);
+  // s' of the wave's 16 envs, staged once in LDS (tes_stage_rows, as
+  // k_tesauro198_rows), then stored twice: the state rows (contiguous) and
+  // the ring rows (q0 + e0 + r) % capacity, non-temporally (read only when
+  // sampled) -- 8-byte pieces, as a ring row starts 8-byte aligned
+  __shared__ __attribute__((aligned(16))) float rows[kBlock / 64][kTesEnvs * 198];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int e0 = (blockIdx.x * (kBlock / 64) + wave) * kTesEnvs;
+  tes_stage_rows(t.pl, t.n, e0, rows[wave]);
+  wave_lds_handoff();
+  const int rows_here = max(0, min(kTesEnvs, t.n - e0));
+  const uint32_t bytes = (uint32_t)rows_here * kTesRowB;
+  const float4* src = reinterpret_cast<const float4*>(rows[wave]);
+  float4* dst = reinterpret_cast<float4*>(t.state + (size_t)e0 * 198);
+  for (uint32_t k = (uint32_t)lane; 16u * k < bytes; k += 64u) {
+    if (16u * k + 16u <= bytes) {
+      dst[k] = src[k];
+    } else {
+      *reinterpret_cast<float2*>(reinterpret_cast<float*>(dst + k)) = *reinterpret_cast<const float2*>(src + k);
+    }
   }
-  if (vec) {
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    const v4f nn = {nv[0], nv[1], nv[2], nv[3]};
-    __builtin_nontemporal_store(nn, reinterpret_cast<v4f*>(t.r_obs + (size_t)q0 * 198 + e0));
-    *reinterpret_cast<float4*>(t.state + e0) = make_float4(nv[0], nv[1], nv[2], nv[3]);
-  } else {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t e = e0 + (uint32_t)q;
-      if (e >= total) break;
-      const int i = (int)(e / 198u);
-      const int col = (int)(e - (uint32_t)i * 198u);
-      int64_t qs = q0 + i;
-      if (qs >= t.capacity) qs -= t.capacity;
-      t.r_obs[qs * 198 + col] = nv[q];
-      t.state[e] = nv[q];
+  int64_t r0 = q0 + e0;
+  if (r0 >= t.capacity) r0 -= t.capacity;
+  const float2* src2 = reinterpret_cast<const float2*>(rows[wave]);
+  typedef float v2f __attribute__((ext_vector_type(2)));
+  if (r0 + rows_here <= t.capacity) {  // no wrap inside the wave's rows: one run
+    v2f* d2 = reinterpret_cast<v2f*>(t.r_obs + (size_t)r0 * 198);
+    for (uint32_t k = (uint32_t)lane; 8u * k < bytes; k += 64u) {
+      const float2 v = src2[k];
+      const v2f x = {v.x, v.y};
+      __builtin_nontemporal_store(x, d2 + k);
+    }
+  } else {  // the ring wraps inside them: row by row
+    for (int r = 0; r < rows_here; ++r) {
+      int64_t rr = r0 + r;
+      if (rr >= t.capacity) rr -= t.capacity;
+      v2f* d2 = reinterpret_cast<v2f*>(t.r_obs + (size_t)rr * 198);
+      for (int k = lane; k < 99; k += 64) {
+        const float2 v = src2[r * 99 + k];
+        const v2f x = {v.x, v.y};
+        __builtin_nontemporal_store(x, d2 + k);
+      }
     }
   }
 }

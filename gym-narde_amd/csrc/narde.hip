@@ -555,8 +555,8 @@ int narde_dqn_transition(narde_env* e, float* state, const int64_t* actions, con
   DeviceGuard dg(e->device);
   TransArgs t{e->pl, (int)e->n, shaping, state, actions, reward, terminated, truncated, legal, misc, off_seen,
               r_obs, r_action, r_reward, r_done, r_prio, max_prio, pos, capacity};
-  const int64_t quads = (e->n * 198 + 3) / 4;
-  const int obs_blocks = (int)((quads + kBlock - 1) / kBlock);
+  const int64_t per_block = (int64_t)kTesEnvs * (kBlock / 64);  // s' rows per obs workgroup
+  const int obs_blocks = (int)((e->n + per_block - 1) / per_block);
   k_dqn_transition<<<(unsigned)(obs_blocks + grid(e->n)), kBlock, 0, (hipStream_t)stream>>>(t, obs_blocks);
   return check_launch("k_dqn_transition");
 }

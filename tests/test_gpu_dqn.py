@@ -211,7 +211,7 @@ def test_policy_kernel_device_scalars_and_fused_addend():
     assert torch.equal(got, masked_argmax(q + tab[rows], m))
 
 
-@pytest.mark.parametrize("shaping,pos", [(True, "wrap"), (False, "wrap"), (True, "aligned")])
+@pytest.mark.parametrize("shaping,pos", [(True, "wrap"), (False, "wrap"), (True, "aligned"), (True, "wrap_next")])
 def test_fused_transition_matches_torch_restatement(shaping, pos):
     """k_dqn_transition (observation + reward shaping + replay write + s <- s')
     is bit-exact against the driver's torch restatement on the same step,
@@ -232,8 +232,9 @@ def test_fused_transition_matches_torch_restatement(shaping, pos):
     off0 = torch.randint(0, 16, (n, 2), device="cuda:0", generator=g).float()
     state0, misc0 = drv.state.clone(), drv.misc.clone()
     rp = drv.replay
-    # ring wrap of the s' rows (per-float path) / 16-B aligned contiguous rows (vector path)
-    p0 = 3 * n - 100 if pos == "wrap" else n
+    # ring wrap of this step's rows / of its s' rows (inside a 16-row group
+    # of the staged store: row by row) / contiguous rows
+    p0 = {"wrap": 3 * n - 100, "wrap_next": 2 * n - 99, "aligned": n}[pos]
     rp.max_prio.fill_(2.5)
     a = drv.act(drv.state)
     _, reward, term, trunc, info = env.step(a.to(torch.int16))
