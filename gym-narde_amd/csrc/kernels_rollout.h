@@ -446,11 +446,14 @@ constexpr int kPcThreads = 2 * kPcEnvs;         // producers + one consumer wave
 constexpr int kPcR = 4;                         // plies per full barrier block
 constexpr int kPcSlots = 2;                     // ring slots (block b uses slot b & 1)
 
-// Barrier blocks of 1, 2, then kPcR plies: the output stream (the
-// consumers' stores of block b - 1 while the rule waves play block b) only
-// starts after the first block, and the kernel is store-bound, so a short
-// first block shortens the stretch with no stores -- worth ~3 us of a 20-ply
-// launch (~35 us), nothing at 1,000 plies.
+// Barrier blocks of 1, then R plies: the output stream (the consumers'
+// stores of block b - 1 while the rule waves play block b) only starts
+// after the first block, and the kernel is store-bound, so a short first
+// block shortens the stretch with no stores -- worth ~3 us of a 20-ply
+// launch (~35 us), nothing at 1,000 plies.  (Round 5's 1, 2, then R: one
+// 20-ply launch 32.0 -> 31.2-31.7 us, sustained 0.1518 -> 0.1498 ms per 100
+// plies at 20 plies, 1,000 plies unchanged; 1, 1, then R lost at 1,000
+// plies, 0.1288; profiles/r06/blocks/)
 // R: the full blocks' plies (<= kPcR, the rings' depth) -- kPcRShort in
 // launches of at most kPcShortPlies plies, where the more frequent barriers
 // cost less than the stretch with no stores at the end (one launch's last
@@ -458,11 +461,11 @@ constexpr int kPcSlots = 2;                     // ring slots (block b uses slot
 // event span with 2-ply blocks (3: 33.4, 1: 36.1; two rounds, one box,
 // profiles/r06/blocks/)
 __device__ __forceinline__ int pc_nblocks(int plies, int R) {
-  return plies <= 1 ? 1 : (plies <= 3 ? 2 : 2 + (plies - 3 + R - 1) / R);
+  return plies <= 1 ? 1 : 1 + (plies - 1 + R - 1) / R;
 }
 __device__ __forceinline__ void pc_block(int b, int plies, int R, int& p0, int& np) {
-  p0 = b == 0 ? 0 : (b == 1 ? 1 : 3 + (b - 2) * R);
-  const int sz = b == 0 ? 1 : (b == 1 ? 2 : R);
+  p0 = b == 0 ? 0 : 1 + (b - 1) * R;
+  const int sz = b == 0 ? 1 : R;
   np = max(0, min(sz, plies - p0));
 }
 constexpr int kPcRShort = 2;
